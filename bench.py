@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: distributed 2-D 5-point Jacobi (fp64) on MI355X.
+
+Metric (BASELINE.json): "DAXPY GB/s + 2D stencil MLUPS at 1/2/4/8 MI355X;
+halo-exchange latency".  The headline ``value`` is the whole-job stencil rate
+in MLUPS (million lattice-point updates per second, summed over all GPUs) on
+the BASELINE multi-GPU config "mpi_stencil2d 32768² ... (2×4 decomp), halo
+exchange/interior overlap".  The global domain is FIXED at 32768² for every N
+(strong scaling: N = 8 is exactly the named 2×4 config).  The same JSON line
+also carries the single-GPU DAXPY bandwidth (N = 2^28 fp64, BASELINE config
+"daxpy N=2^28 fp64 on one MI355X") and the measured halo-exchange latency.
+
+One step = halo exchange (RCCL over xGMI, overlapped with the interior sweep
+on a second stream) + one full Jacobi sweep of the global domain.  Nothing is
+skipped inside the timed region.
+
+Launch (driver contract):
+    python bench.py --gpus 1 --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from gpu_mpi_tests_amd import ops  # noqa: E402
+from gpu_mpi_tests_amd.models.jacobi import Jacobi2D  # noqa: E402
+from gpu_mpi_tests_amd.parallel import dist as gdist  # noqa: E402
+
+
+def _sync(env):
+    if env.is_gpu:
+        torch.cuda.synchronize(env.device)
+
+
+def bench_jacobi(env, n, steps, warmup, overlap, dims):
+    solver = Jacobi2D(n, n, env=env, dims=dims, overlap=overlap)
+    for _ in range(warmup):
+        solver.step()
+    gdist.barrier(env)
+    _sync(env)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        solver.step()
+    _sync(env)
+    gdist.barrier(env)
+    dt = time.perf_counter() - t0
+    dt = gdist.allreduce_max(dt, env)
+    resid = solver.global_residual()  # one extra (untimed) step: sanity that values are finite
+    return solver, dt, resid
+
+
+def bench_halo(env, solver, iters):
+    """Halo-exchange latency: start()+finish() alone, mean over iters (max over ranks)."""
+    ex = solver.ex[id(solver.u)]
+    if not ex.active:
+        return None, 0
+    for _ in range(5):
+        ex.exchange()
+    gdist.barrier(env)
+    _sync(env)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        ex.exchange()
+    _sync(env)
+    dt = (time.perf_counter() - t0) / iters
+    return gdist.allreduce_max(dt, env), ex.bytes_per_exchange()
+
+
+def bench_daxpy(env, n, iters):
+    """Per-GPU DAXPY rate (each rank on its own GPU), reported as whole-job GB/s."""
+    dev = env.device
+    x = torch.rand(n, dtype=torch.float64, device=dev)
+    y = torch.rand(n, dtype=torch.float64, device=dev)
+    for _ in range(3):
+        ops.daxpy(2.0, x, y)
+    _sync(env)
+    gdist.barrier(env)
+    if env.is_gpu:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            ops.daxpy(2.0, x, y)
+        e1.record()
+        e1.synchronize()
+        dt = e0.elapsed_time(e1) / 1e3 / iters
+    else:
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            ops.daxpy(2.0, x, y)
+        dt = (time.perf_counter() - t0) / iters
+    dt = gdist.allreduce_max(dt, env)
+    del x, y
+    return 24.0 * n / dt / 1e9 * env.world_size, dt
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--size", type=int, default=32768, help="global domain is size x size (default 32768)")
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--dims", type=str, default=None, help="process grid PYxPX, e.g. 4x2")
+    ap.add_argument("--daxpy-n", type=int, default=1 << 28)
+    ap.add_argument("--skip-extras", action="store_true", help="headline stencil only")
+    ap.add_argument("--variant", type=int, default=0, help="jacobi kernel variant (0 auto,1 reg,2 lds,3 scalar)")
+    ap.add_argument("--device", type=str, default=None, help="cuda|cpu (default: cuda if available)")
+    args = ap.parse_args(argv)
+
+    env = gdist.init(device=args.device)
+    if args.gpus != env.world_size and env.rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
+    if env.is_gpu and args.variant:
+        ops.set_jacobi_variant(args.variant)
+    dims = tuple(int(v) for v in args.dims.lower().split("x")) if args.dims else None
+
+    solver, dt, resid = bench_jacobi(env, args.size, args.steps, args.warmup, not args.no_overlap, dims)
+    points = solver.points
+    mlups = points * args.steps / dt / 1e6
+    ms_per_step = dt / args.steps * 1e3
+    extras = {}
+    if not args.skip_extras:
+        hl, hbytes = bench_halo(env, solver, iters=max(20, args.steps))
+        extras["halo_exchange_us"] = None if hl is None else round(hl * 1e6, 2)
+        extras["halo_bytes_per_rank"] = hbytes
+        del solver
+        if env.is_gpu:
+            torch.cuda.empty_cache()
+        gbps, ddt = bench_daxpy(env, args.daxpy_n, iters=20)
+        extras["daxpy_GBps"] = round(gbps, 1)
+        extras["daxpy_GBps_per_gpu"] = round(gbps / env.world_size, 1)
+        extras["daxpy_n"] = args.daxpy_n
+        extras["daxpy_ms"] = round(ddt * 1e3, 4)
+    py, px = (1, 1)
+    if env.world_size > 1 or True:
+        from gpu_mpi_tests_amd.parallel.decomp import choose_dims
+        py, px = dims if dims else choose_dims(env.world_size, args.size, args.size)
+    if env.rank == 0:
+        rec = {
+            "metric": "2D 5-pt Jacobi stencil MLUPS (fp64, halo exchange overlapped)",
+            "value": round(mlups, 1),
+            "unit": "MLUPS",
+            "n_gpus": env.world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "fp64",
+            "data": "synthetic (seeded uniform random interior, Dirichlet lid BC)",
+            "config": {
+                "model": f"mpi_stencil2d jacobi5 {args.size}x{args.size} fp64",
+                "global_batch": points,
+                "seq_len": None,
+                "parallelism": f"spatial2d px{px} x py{py} ({px}x{py} decomp), "
+                               f"{'overlap' if not args.no_overlap else 'serial'}",
+                "transport": env.backend if env.world_size > 1 else "none",
+                "device": str(env.device),
+            },
+            "residual_l2": resid,
+            **extras,
+        }
+        print(json.dumps(rec), flush=True)
+    gdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,110 @@
+/*
+ * gmt/kernels.h — C ABI of the hand-written gfx950 kernels in libgmt.so.
+ *
+ * Every entry point is asynchronous on the given HIP stream (pass the raw
+ * hipStream_t as `void*`; NULL = the legacy default stream) and returns a
+ * hipError_t as int (0 = success). The same ABI is used by the native MPI
+ * apps (csrc/apps) and by the Python package through ctypes
+ * (gpu_mpi_tests_amd/_native.py), so there is exactly one kernel code path.
+ *
+ * Layout convention (matches the reference's column-major arrays, e.g.
+ * /root/reference/mpi_stencil2d_sycl.cc:40-43 `idx2`): a 2-D field is stored
+ * as `ny` rows of `ld` elements; x (the reference's "dim 0") is the contiguous
+ * axis, y ("dim 1") is the strided axis. In torch terms that is a row-major
+ * tensor of shape [ny, ld].
+ */
+#ifndef GMT_KERNELS_H
+#define GMT_KERNELS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- K1/K2: y <- a*x + y (fp64).  reference: daxpy.cu:73, mpi_daxpy_gt.cc:81 */
+int gmt_daxpy(int64_t n, double a, const double* x, double* y, void* stream);
+
+/* ---- K3: 1-D 5-tap stencil, out[i] = scale * sum_k c[k]*in[i+k], k=0..4.
+ *      `in` has n_out+4 elements.  reference: mpi_stencil_gt.cc:54-59 */
+int gmt_stencil5_1d(int64_t n_out, const double* coef5, double scale,
+                    const double* in, double* out, void* stream);
+
+/* ---- K4/K5/K11: 2-D field, 5-tap stencil along `dim` (0 = contiguous x,
+ *      1 = strided y).  `in` is (ny_out [+4 if dim==1]) rows of ld_in,
+ *      holding nx_out [+4 if dim==0] valid columns.
+ *      reference: mpi_stencil2d_gt.cc:84-110, mpi_stencil2d_sycl.cc:53-75 */
+int gmt_stencil5_2d(int dim, int64_t nx_out, int64_t ny_out, const double* coef5,
+                    double scale, const double* in, int64_t ld_in, double* out,
+                    int64_t ld_out, void* stream);
+
+/* ---- K6/K7/K8: batched strided 2-D copy (halo pack / unpack, fused L+R).
+ *      Each descriptor copies `height` rows of `width` elements of
+ *      `elem_bytes` (4 or 8) from src (row pitch src_ld elements) to dst
+ *      (row pitch dst_ld elements).  Up to GMT_MAX_COPY2D descriptors are
+ *      fused into one launch.  reference: mpi_stencil2d_gt.cc:166-174,239,251 */
+#define GMT_MAX_COPY2D 8
+typedef struct gmt_copy2d_desc {
+  const void* src;
+  void* dst;
+  int64_t src_ld;
+  int64_t dst_ld;
+  int64_t width;
+  int64_t height;
+} gmt_copy2d_desc;
+int gmt_copy2d_batched(int n_desc, const gmt_copy2d_desc* descs, int elem_bytes,
+                       void* stream);
+
+/* ---- K9: axis sums of a 2-D field of nx x ny (row pitch ld).
+ *      keep_dim == 0: out[x] = sum_y z[y][x]   (length nx)
+ *      keep_dim == 1: out[y] = sum_x z[y][x]   (length ny)
+ *      `workspace` must hold gmt_sum_axis_workspace(...) doubles.
+ *      reference: mpi_stencil2d_gt.cc:611,620 (gt::sum_axis_to) */
+int64_t gmt_sum_axis_workspace(int keep_dim, int64_t nx, int64_t ny);
+int gmt_sum_axis(int keep_dim, int64_t nx, int64_t ny, const double* z, int64_t ld,
+                 double* out, double* workspace, void* stream);
+
+/* ---- K10/K12: out[0] = sum over the nx x ny region of (a - b)^2
+ *      (NOT square-rooted, so partial results can be all-reduced).
+ *      `workspace` must hold gmt_diff_sq_workspace(...) doubles.
+ *      reference: mpi_stencil2d_gt.cc:555, mpi_stencil2d_sycl.cc:165-181 */
+int64_t gmt_diff_sq_workspace(int64_t nx, int64_t ny);
+int gmt_diff_sq(int64_t nx, int64_t ny, const double* a, int64_t lda, const double* b,
+                int64_t ldb, double* out, double* workspace, void* stream);
+
+/* ---- analytic fill z[y][x] = (x0+i*dx)^3 + (y0+j*dy)^2 over nx x ny (device
+ *      side replacement of the reference's host init loops,
+ *      mpi_stencil2d_gt.cc:439-497).  mode 0: x^3+y^2 (z), 1: 3x^2 (dz/dx),
+ *      2: 2y (dz/dy). */
+int gmt_fill_poly(int mode, int64_t nx, int64_t ny, double x0, double dx, double y0,
+                  double dy, double* z, int64_t ld, void* stream);
+
+/* ---- 2-D 5-point Jacobi sweep (the BASELINE "5-pt Jacobi" extension):
+ *      for y in [y0, y0+ny), x in [x0, x0+nx) (absolute array coordinates):
+ *        un[y][x] = c0*(u[y][x-1]+u[y][x+1]+u[y-1][x]+u[y+1][x]) + c1*f[y][x]
+ *      f may be NULL (Laplace).  If resid_partial != NULL, the kernel also
+ *      accumulates sum (un-u)^2 and leaves the total in resid_partial[0]
+ *      (resid_partial must hold gmt_jacobi_resid_workspace(...) doubles). */
+int64_t gmt_jacobi_resid_workspace(int64_t nx, int64_t ny);
+int gmt_jacobi5(int64_t x0, int64_t nx, int64_t y0, int64_t ny, const double* u,
+                double* un, int64_t ld, const double* f, int64_t ldf, double c0,
+                double c1, double* resid_partial, void* stream);
+/* Same sweep for a list of rectangles in one launch (the boundary "frame" of
+ * an overlapped step: up to 4 strips).  rect = {x0, nx, y0, ny}. */
+int gmt_jacobi5_rects(int n_rect, const int64_t* rects, const double* u, double* un,
+                      int64_t ld, const double* f, int64_t ldf, double c0, double c1,
+                      void* stream);
+/* Kernel variant selection for A/B measurement: 0 = auto, 1 = register
+ * sliding window (vector x2), 2 = LDS-tiled, 3 = scalar reference kernel. */
+void gmt_jacobi5_set_variant(int variant);
+int gmt_jacobi5_get_variant(void);
+
+/* ---- misc */
+const char* gmt_error_string(int err);
+int gmt_device_synchronize(void);
+const char* gmt_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GMT_KERNELS_H */

@@ -1,0 +1,247 @@
+// K9 axis sums, K10/K12 squared-difference norms, analytic fills — gfx950.
+//
+// Reference: gt::sum_axis_to (mpi_stencil2d_gt.cc:611,620), host
+// gt::sum_squares(h_num - h_act) (mpi_stencil_gt.cc:222,
+// mpi_stencil2d_gt.cc:555), the SYCL diff_norm reduction
+// (mpi_stencil2d_sycl.cc:165-181) and the host analytic init loops
+// (mpi_stencil2d_gt.cc:439-497).
+//
+// All reductions are two-pass and deterministic: pass 1 writes one partial
+// per (tile), pass 2 reduces the partials in a fixed order.  No float atomics
+// (run-to-run bit-identical results, which the distributed err-norm checks
+// rely on).
+#include "common.hpp"
+#include "gmt/kernels.h"
+
+namespace gmt {
+
+// ---------------- keep_dim == 0: column sums out[x] = sum_y z[y][x]
+// pass 1: block (bx, p) sums rows [p*RC, (p+1)*RC) of 512 columns into
+// ws[p][x]; pass 2: out[x] = sum_p ws[p][x] (coalesced over x).
+constexpr int64_t kColTargetBlocks = 4096;
+
+__global__ __launch_bounds__(kBlock) void colsum_pass1(int64_t nx, int64_t ny,
+                                                       const double* __restrict__ z, int64_t ld,
+                                                       double* __restrict__ ws, int64_t nbx,
+                                                       int64_t rc, bool vec) {
+  const int64_t b = blockIdx.x;
+  const int64_t bx = b % nbx, p = b / nbx;
+  const int64_t x = (bx * kBlock + threadIdx.x) * 2;
+  if (x >= nx) return;
+  const int64_t y0 = p * rc;
+  const int64_t y1 = (y0 + rc) < ny ? (y0 + rc) : ny;
+  if (vec && x + 1 < nx) {
+    d2 a0 = {0.0, 0.0}, a1 = {0.0, 0.0};
+    int64_t y = y0;
+    for (; y + 1 < y1; y += 2) {
+      a0 += ld2(z + y * ld + x);
+      a1 += ld2(z + (y + 1) * ld + x);
+    }
+    if (y < y1) a0 += ld2(z + y * ld + x);
+    st2(ws + p * nx + x, a0 + a1);
+  } else {
+    for (int64_t xx = x; xx < x + 2 && xx < nx; ++xx) {
+      double a = 0.0;
+      for (int64_t y = y0; y < y1; ++y) a += z[y * ld + xx];
+      ws[p * nx + xx] = a;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void colsum_pass2(int64_t nx, int64_t np,
+                                                       const double* __restrict__ ws,
+                                                       double* __restrict__ out) {
+  const int64_t x = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (x >= nx) return;
+  double a = 0.0;
+  for (int64_t p = 0; p < np; ++p) a += ws[p * nx + x];
+  out[x] = a;
+}
+
+// ---------------- keep_dim == 1: row sums out[y] = sum_x z[y][x]
+// pass 1: block (c, y) reduces chunk c (CH elements) of row y to ws[y][c];
+// pass 2: one wave per row sums its chunks.
+constexpr int64_t kRowChunk = 2 * kBlock * 8;  // 4096 doubles per block
+
+__global__ __launch_bounds__(kBlock) void rowsum_pass1(int64_t nx, int64_t ny,
+                                                       const double* __restrict__ z, int64_t ld,
+                                                       double* __restrict__ ws, int64_t nch,
+                                                       bool vec) {
+  const int64_t b = blockIdx.x;
+  const int64_t c = b % nch, y = b / nch;
+  const double* row = z + y * ld;
+  const int64_t x0 = c * kRowChunk;
+  const int64_t x1 = (x0 + kRowChunk) < nx ? (x0 + kRowChunk) : nx;
+  double a = 0.0;
+  if (vec) {
+    d2 v = {0.0, 0.0};
+    for (int64_t x = x0 + 2 * threadIdx.x; x + 1 < x1; x += 2 * kBlock) v += ld2(row + x);
+    a = v.x + v.y;
+    if (((x1 - x0) & 1) && threadIdx.x == 0) a += row[x1 - 1];
+  } else {
+    for (int64_t x = x0 + threadIdx.x; x < x1; x += kBlock) a += row[x];
+  }
+  a = block_sum(a);
+  if (threadIdx.x == 0) ws[y * nch + c] = a;
+}
+
+__global__ __launch_bounds__(kBlock) void rowsum_pass2(int64_t ny, int64_t nch,
+                                                       const double* __restrict__ ws,
+                                                       double* __restrict__ out) {
+  const int64_t y = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + threadIdx.x / kWave;
+  if (y >= ny) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  double a = 0.0;
+  for (int64_t c = lane; c < nch; c += kWave) a += ws[y * nch + c];
+  a = wave_sum(a);
+  if (lane == 0) out[y] = a;
+}
+
+static void col_plan(int64_t nx, int64_t ny, int64_t* nbx, int64_t* np, int64_t* rc) {
+  *nbx = (nx + 2 * kBlock - 1) / (2 * kBlock);
+  int64_t p = (kColTargetBlocks + *nbx - 1) / *nbx;
+  const int64_t max_p = (ny + 15) / 16;  // at least 16 rows per partial
+  if (p > max_p) p = max_p;
+  if (p < 1) p = 1;
+  *rc = (ny + p - 1) / p;
+  *np = (ny + *rc - 1) / *rc;
+}
+
+// ---------------- sum of squared differences over a 2-D region
+constexpr int64_t kDiffTile = 2 * kBlock * 8;
+
+__global__ __launch_bounds__(kBlock) void diffsq_pass1(int64_t nx, int64_t ny,
+                                                       const double* __restrict__ a,
+                                                       int64_t lda, const double* __restrict__ b,
+                                                       int64_t ldb, double* __restrict__ ws,
+                                                       int64_t nch, bool vec) {
+  const int64_t blk = blockIdx.x;
+  const int64_t c = blk % nch, y = blk / nch;
+  const int64_t x0 = c * kDiffTile;
+  const int64_t x1 = (x0 + kDiffTile) < nx ? (x0 + kDiffTile) : nx;
+  const double* pa = a + y * lda;
+  const double* pb = b + y * ldb;
+  double acc = 0.0;
+  if (vec) {
+    d2 v = {0.0, 0.0};
+    for (int64_t x = x0 + 2 * threadIdx.x; x + 1 < x1; x += 2 * kBlock) {
+      const d2 d = ld2(pa + x) - ld2(pb + x);
+      v += d * d;
+    }
+    acc = v.x + v.y;
+    if (((x1 - x0) & 1) && threadIdx.x == 0) {
+      const double d = pa[x1 - 1] - pb[x1 - 1];
+      acc += d * d;
+    }
+  } else {
+    for (int64_t x = x0 + threadIdx.x; x < x1; x += kBlock) {
+      const double d = pa[x] - pb[x];
+      acc += d * d;
+    }
+  }
+  acc = block_sum(acc);
+  if (threadIdx.x == 0) ws[blk] = acc;
+}
+
+__global__ __launch_bounds__(kBlock) void sum_all(const double* __restrict__ ws, int64_t n,
+                                                  double* __restrict__ out) {
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += kBlock) acc += ws[i];
+  acc = block_sum(acc);
+  if (threadIdx.x == 0) out[0] = acc;
+}
+
+// ---------------- analytic fills (reference fn / fn_dzdx / fn_dzdy lambdas,
+// mpi_stencil2d_gt.cc:431-433)
+__global__ __launch_bounds__(kBlock) void fill_poly_kernel(int mode, int64_t nx, int64_t ny,
+                                                           double x0, double dx, double y0,
+                                                           double dy, double* __restrict__ z,
+                                                           int64_t ld) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= nx * ny) return;
+  const int64_t ix = i % nx, iy = i / nx;
+  const double x = x0 + ix * dx, y = y0 + iy * dy;
+  double v;
+  if (mode == 0)
+    v = x * x * x + y * y;
+  else if (mode == 1)
+    v = 3 * x * x;
+  else
+    v = 2 * y;
+  z[iy * ld + ix] = v;
+}
+
+}  // namespace gmt
+
+extern "C" int64_t gmt_sum_axis_workspace(int keep_dim, int64_t nx, int64_t ny) {
+  using namespace gmt;
+  if (keep_dim == 0) {
+    int64_t nbx, np, rc;
+    col_plan(nx, ny, &nbx, &np, &rc);
+    return np * nx;
+  }
+  const int64_t nch = (nx + kRowChunk - 1) / kRowChunk;
+  return ny * nch;
+}
+
+extern "C" int gmt_sum_axis(int keep_dim, int64_t nx, int64_t ny, const double* z, int64_t ld,
+                            double* out, double* ws, void* stream) {
+  using namespace gmt;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (nx <= 0 || ny <= 0) return 0;
+  const bool vec = aligned16(z) && (ld % 2 == 0);
+  if (keep_dim == 0) {
+    int64_t nbx, np, rc;
+    col_plan(nx, ny, &nbx, &np, &rc);
+    colsum_pass1<<<grid_1d(nbx * np), kBlock, 0, s>>>(nx, ny, z, ld, ws, nbx, rc,
+                                                      vec && aligned16(ws) && nx % 2 == 0);
+    colsum_pass2<<<grid_1d((nx + kBlock - 1) / kBlock), kBlock, 0, s>>>(nx, np, ws, out);
+  } else if (keep_dim == 1) {
+    const int64_t nch = (nx + kRowChunk - 1) / kRowChunk;
+    rowsum_pass1<<<grid_1d(nch * ny), kBlock, 0, s>>>(nx, ny, z, ld, ws, nch, vec);
+    const int64_t rows_per_block = kBlock / kWave;
+    rowsum_pass2<<<grid_1d((ny + rows_per_block - 1) / rows_per_block), kBlock, 0, s>>>(
+        ny, nch, ws, out);
+  } else {
+    return static_cast<int>(hipErrorInvalidValue);
+  }
+  GMT_RET_LAUNCH();
+}
+
+extern "C" int64_t gmt_diff_sq_workspace(int64_t nx, int64_t ny) {
+  using namespace gmt;
+  return ((nx + kDiffTile - 1) / kDiffTile) * ny;
+}
+
+extern "C" int gmt_diff_sq(int64_t nx, int64_t ny, const double* a, int64_t lda, const double* b,
+                           int64_t ldb, double* out, double* ws, void* stream) {
+  using namespace gmt;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (nx <= 0 || ny <= 0) return static_cast<int>(hipMemsetAsync(out, 0, sizeof(double), s));
+  const bool vec = aligned16(a) && aligned16(b) && lda % 2 == 0 && ldb % 2 == 0;
+  const int64_t nch = (nx + kDiffTile - 1) / kDiffTile;
+  diffsq_pass1<<<grid_1d(nch * ny), kBlock, 0, s>>>(nx, ny, a, lda, b, ldb, ws, nch, vec);
+  sum_all<<<1, kBlock, 0, s>>>(ws, nch * ny, out);
+  GMT_RET_LAUNCH();
+}
+
+extern "C" int gmt_fill_poly(int mode, int64_t nx, int64_t ny, double x0, double dx, double y0,
+                             double dy, double* z, int64_t ld, void* stream) {
+  using namespace gmt;
+  if (nx <= 0 || ny <= 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  fill_poly_kernel<<<grid_1d((nx * ny + kBlock - 1) / kBlock), kBlock, 0, s>>>(
+      mode, nx, ny, x0, dx, y0, dy, z, ld);
+  GMT_RET_LAUNCH();
+}
+
+extern "C" const char* gmt_error_string(int err) {
+  return hipGetErrorString(static_cast<hipError_t>(err));
+}
+
+extern "C" int gmt_device_synchronize(void) { return static_cast<int>(hipDeviceSynchronize()); }
+
+extern "C" const char* gmt_build_info(void) {
+  return "libgmt gfx950 (CDNA4) kernels: daxpy, stencil5 1d/2d, jacobi5 (reg/lds/scalar), "
+         "copy2d_batched, sum_axis, diff_sq, fill_poly; built " __DATE__ " " __TIME__;
+}

@@ -1,0 +1,260 @@
+"""Torch-facing wrappers of the libgmt gfx950 kernels.
+
+Device tensors dispatch to the hand-written HIP kernels (``csrc/kernels``)
+on the caller's current HIP stream; CPU tensors run the PyTorch reference
+(``reference.py``).  There is no silent device fallback: if libgmt is
+missing, device calls raise (see ``_native.lib``).
+
+2-D fields follow ``gmt/kernels.h``: a tensor of shape ``[ny, nx]`` with
+``stride(1) == 1`` (x contiguous = the reference's "dim 0"); ``stride(0)``
+is the row pitch ``ld``, so views into padded / ghosted storage are accepted
+without copies.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import torch
+
+from .. import _native
+from . import reference as ref
+from .reference import DERIV5
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _is_dev(t: torch.Tensor) -> bool:
+    return t.device.type == "cuda"
+
+
+def _check2d(t: torch.Tensor, name: str):
+    if t.dim() != 2 or (t.shape[1] > 1 and t.stride(1) != 1):
+        raise ValueError(f"{name}: expected a 2-D tensor with unit x-stride, got {tuple(t.shape)} "
+                         f"strides {t.stride()}")
+    if t.dtype != torch.float64:
+        raise TypeError(f"{name}: kernels are fp64 (reference precision), got {t.dtype}")
+
+
+class _Coef:
+    """Keeps the ctypes array alive for the duration of the (synchronous) launch call."""
+
+    def __init__(self, coef):
+        self.arr = (ctypes.c_double * 5)(*[float(c) for c in coef])
+        self.ptr = ctypes.cast(self.arr, ctypes.c_void_p)
+
+
+# --------------------------------------------------------------------- DAXPY
+def daxpy(a: float, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """In-place ``y <- a*x + y`` (fp64, contiguous).  K1/K2."""
+    if x.numel() != y.numel():
+        raise ValueError("daxpy: size mismatch")
+    if not (x.is_contiguous() and y.is_contiguous()):
+        raise ValueError("daxpy: contiguous vectors required (incx = incy = 1)")
+    if not _is_dev(y):
+        return ref.daxpy(a, x, y)
+    L = _native.lib()
+    _native.check(L.gmt_daxpy(y.numel(), float(a), x.data_ptr(), y.data_ptr(), _stream(y)),
+                  "gmt_daxpy")
+    return y
+
+
+# ------------------------------------------------------------ 5-tap stencils
+def stencil5_1d(inp: torch.Tensor, out: torch.Tensor | None = None, scale: float = 1.0,
+                coef=DERIV5) -> torch.Tensor:
+    """``out[i] = scale * sum_k coef[k]*inp[i+k]``; len(out) = len(inp)-4.  K3."""
+    n = inp.numel() - 4
+    if not _is_dev(inp):
+        r = ref.stencil5_1d(inp, scale, coef)
+        if out is None:
+            return r
+        out.copy_(r)
+        return out
+    if out is None:
+        out = torch.empty(n, dtype=inp.dtype, device=inp.device)
+    assert inp.is_contiguous() and out.is_contiguous() and out.numel() == n
+    L = _native.lib()
+    cf = _Coef(coef)
+    _native.check(L.gmt_stencil5_1d(n, cf.ptr, float(scale), inp.data_ptr(),
+                                    out.data_ptr(), _stream(inp)), "gmt_stencil5_1d")
+    return out
+
+
+def stencil5_2d(inp: torch.Tensor, dim: int, out: torch.Tensor | None = None,
+                scale: float = 1.0, coef=DERIV5) -> torch.Tensor:
+    """5-tap stencil along ``dim`` (0 = contiguous x, 1 = strided y).  K4/K5."""
+    _check2d(inp, "stencil5_2d.inp")
+    ny_in, nx_in = inp.shape
+    nx_out, ny_out = (nx_in - 4, ny_in) if dim == 0 else (nx_in, ny_in - 4)
+    if not _is_dev(inp):
+        r = ref.stencil5_2d(inp, dim, scale, coef)
+        if out is None:
+            return r
+        out.copy_(r)
+        return out
+    if out is None:
+        out = torch.empty(ny_out, nx_out, dtype=inp.dtype, device=inp.device)
+    _check2d(out, "stencil5_2d.out")
+    assert tuple(out.shape) == (ny_out, nx_out), (out.shape, ny_out, nx_out)
+    L = _native.lib()
+    cf = _Coef(coef)
+    _native.check(L.gmt_stencil5_2d(dim, nx_out, ny_out, cf.ptr, float(scale),
+                                    inp.data_ptr(), inp.stride(0), out.data_ptr(),
+                                    out.stride(0), _stream(inp)), "gmt_stencil5_2d")
+    return out
+
+
+# ------------------------------------------------------- halo pack / unpack
+def copy2d_batched(pairs: Sequence[tuple[torch.Tensor, torch.Tensor]]) -> None:
+    """Copy each ``src`` 2-D view into ``dst`` (same shape) in ONE launch.  K6/K7/K8."""
+    pairs = [(s, d) for s, d in pairs if s.numel() > 0]
+    if not pairs:
+        return
+    if not _is_dev(pairs[0][1]):
+        for s, d in pairs:
+            d.copy_(s)
+        return
+    L = _native.lib()
+    elem = pairs[0][0].element_size()
+    stream = _stream(pairs[0][1])
+    for i in range(0, len(pairs), _native.MAX_COPY2D):
+        chunk = pairs[i : i + _native.MAX_COPY2D]
+        arr = (_native.Copy2dDesc * len(chunk))()
+        for k, (s, d) in enumerate(chunk):
+            if s.dim() == 1:
+                s = s.view(1, -1)
+            if d.dim() == 1:
+                d = d.view(1, -1)
+            if tuple(s.shape) != tuple(d.shape):
+                raise ValueError(f"copy2d: shape mismatch {tuple(s.shape)} vs {tuple(d.shape)}")
+            if s.element_size() != elem or d.element_size() != elem:
+                raise TypeError("copy2d: mixed element sizes")
+            if (s.shape[1] > 1 and s.stride(1) != 1) or (d.shape[1] > 1 and d.stride(1) != 1):
+                raise ValueError("copy2d: unit inner stride required")
+            arr[k].src = s.data_ptr()
+            arr[k].dst = d.data_ptr()
+            arr[k].src_ld = s.stride(0)
+            arr[k].dst_ld = d.stride(0)
+            arr[k].width = s.shape[1]
+            arr[k].height = s.shape[0]
+        _native.check(L.gmt_copy2d_batched(len(chunk), ctypes.cast(arr, ctypes.c_void_p), elem,
+                                           stream), "gmt_copy2d_batched")
+
+
+# ---------------------------------------------------------------- reductions
+def sum_axis(z: torch.Tensor, keep_dim: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Axis sums; keep_dim 0 -> length nx (sum over y), 1 -> length ny.  K9."""
+    _check2d(z, "sum_axis.z")
+    ny, nx = z.shape
+    n_out = nx if keep_dim == 0 else ny
+    if not _is_dev(z):
+        r = ref.sum_axis(z, keep_dim)
+        if out is None:
+            return r
+        out.copy_(r)
+        return out
+    if out is None:
+        out = torch.empty(n_out, dtype=z.dtype, device=z.device)
+    L = _native.lib()
+    ws = torch.empty(max(1, L.gmt_sum_axis_workspace(keep_dim, nx, ny)), dtype=torch.float64,
+                     device=z.device)
+    _native.check(L.gmt_sum_axis(keep_dim, nx, ny, z.data_ptr(), z.stride(0), out.data_ptr(),
+                                 ws.data_ptr(), _stream(z)), "gmt_sum_axis")
+    return out
+
+
+def diff_sq(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """0-d tensor ``sum((a-b)^2)`` (un-rooted so it can be all-reduced).  K10/K12."""
+    if a.dim() == 1:
+        a, b = a.view(1, -1), b.view(1, -1)
+    _check2d(a, "diff_sq.a")
+    _check2d(b, "diff_sq.b")
+    if tuple(a.shape) != tuple(b.shape):
+        raise ValueError("diff_sq: shape mismatch")
+    if not _is_dev(a):
+        return ref.diff_sq(a, b)
+    ny, nx = a.shape
+    L = _native.lib()
+    ws = torch.empty(max(1, L.gmt_diff_sq_workspace(nx, ny)), dtype=torch.float64, device=a.device)
+    out = torch.empty((), dtype=torch.float64, device=a.device)
+    _native.check(L.gmt_diff_sq(nx, ny, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
+                                out.data_ptr(), ws.data_ptr(), _stream(a)), "gmt_diff_sq")
+    return out
+
+
+def diff_norm(a: torch.Tensor, b: torch.Tensor) -> float:
+    return float(diff_sq(a, b).sqrt())
+
+
+# -------------------------------------------------------------- initialisers
+def fill_poly(z: torch.Tensor, mode: int, x0: float, dx: float, y0: float, dy: float) -> torch.Tensor:
+    """z = x^3 + y^2 (mode 0), 3x^2 (mode 1) or 2y (mode 2) on a uniform grid."""
+    if z.dim() == 1:
+        z2 = z.view(1, -1)
+    else:
+        z2 = z
+    _check2d(z2, "fill_poly.z")
+    ny, nx = z2.shape
+    if not _is_dev(z):
+        z2.copy_(ref.poly(mode, nx, ny, x0, dx, y0, dy, dtype=z.dtype))
+        return z
+    L = _native.lib()
+    _native.check(L.gmt_fill_poly(mode, nx, ny, float(x0), float(dx), float(y0), float(dy),
+                                  z2.data_ptr(), z2.stride(0), _stream(z)), "gmt_fill_poly")
+    return z
+
+
+# -------------------------------------------------------------------- Jacobi
+def jacobi5(u: torch.Tensor, un: torch.Tensor, region: tuple[int, int, int, int],
+            f: torch.Tensor | None = None, c0: float = 0.25, c1: float = 0.0,
+            resid: bool = False) -> torch.Tensor | None:
+    """One 5-point Jacobi sweep of ``region = (x0, nx, y0, ny)`` (absolute
+    coordinates in the 2-D storage ``u``/``un``).  Returns the 0-d tensor
+    ``sum((un-u)^2)`` over the region if ``resid``."""
+    _check2d(u, "jacobi5.u")
+    _check2d(un, "jacobi5.un")
+    x0, nx, y0, ny = (int(v) for v in region)
+    if not _is_dev(u):
+        r = ref.jacobi5(u, un, x0, nx, y0, ny, f, c0, c1)
+        return r if resid else None
+    if u.stride(0) != un.stride(0):
+        raise ValueError("jacobi5: u and un must share a row pitch")
+    L = _native.lib()
+    r = None
+    rp = 0
+    if resid:
+        r = torch.empty(max(2, L.gmt_jacobi_resid_workspace(nx, ny)), dtype=torch.float64,
+                        device=u.device)
+        rp = r.data_ptr()
+    _native.check(L.gmt_jacobi5(x0, nx, y0, ny, u.data_ptr(), un.data_ptr(), u.stride(0),
+                                f.data_ptr() if f is not None else 0,
+                                f.stride(0) if f is not None else 0, float(c0), float(c1), rp,
+                                _stream(u)), "gmt_jacobi5")
+    return r[0] if resid else None
+
+
+def jacobi5_rects(u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, int, int, int]],
+                  f: torch.Tensor | None = None, c0: float = 0.25, c1: float = 0.0) -> None:
+    """Sweep up to 4 rectangles (the boundary frame of an overlapped step) in one launch."""
+    rects = [tuple(int(v) for v in r) for r in rects if r[1] > 0 and r[3] > 0]
+    if not rects:
+        return
+    if not _is_dev(u):
+        for (x0, nx, y0, ny) in rects:
+            ref.jacobi5(u, un, x0, nx, y0, ny, f, c0, c1)
+        return
+    assert len(rects) <= 4
+    L = _native.lib()
+    arr = (ctypes.c_int64 * (4 * len(rects)))(*[v for r in rects for v in r])
+    _native.check(L.gmt_jacobi5_rects(len(rects), ctypes.cast(arr, ctypes.c_void_p),
+                                      u.data_ptr(), un.data_ptr(), u.stride(0),
+                                      f.data_ptr() if f is not None else 0,
+                                      f.stride(0) if f is not None else 0, float(c0), float(c1),
+                                      _stream(u)), "gmt_jacobi5_rects")
+
+
+def set_jacobi_variant(v: int) -> None:
+    """0 auto, 1 register sliding window, 2 LDS-tiled, 3 scalar (A/B measurement)."""
+    _native.lib().gmt_jacobi5_set_variant(int(v))

@@ -1,0 +1,68 @@
+import pytest
+
+from gpu_mpi_tests_amd.parallel.decomp import CartDecomp, choose_dims
+from gpu_mpi_tests_amd.parallel.dist import select_device
+from gpu_mpi_tests_amd.parallel.field import Field2D
+
+
+def test_choose_dims_prefers_row_splits():
+    assert choose_dims(1, 100, 100) == (1, 1)
+    assert choose_dims(2, 32768, 32768) == (2, 1)
+    assert choose_dims(4, 32768, 32768) == (4, 1)
+    assert choose_dims(8, 32768, 32768) == (4, 2)  # BASELINE "2x4 decomp": px=2, py=4
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 6, 8])
+@pytest.mark.parametrize("shape", [(17, 23), (64, 64), (1000, 7)])
+def test_partition_covers_domain(world, shape):
+    ny, nx = shape
+    seen = [[0] * nx for _ in range(ny)]
+    for r in range(world):
+        d = CartDecomp.create(world, r, ny, nx)
+        (oy, ly), (ox, lx) = d.local_y, d.local_x
+        for y in range(oy, oy + ly):
+            for x in range(ox, ox + lx):
+                seen[y][x] += 1
+    assert all(v == 1 for row in seen for v in row)
+
+
+def test_neighbors_non_periodic():
+    d = CartDecomp.create(8, 0, 64, 64, (4, 2))
+    nb = d.neighbors()
+    assert nb == {"north": None, "south": 2, "west": None, "east": 1}
+    d = CartDecomp.create(8, 5, 64, 64, (4, 2))  # cy=2, cx=1
+    assert d.neighbors() == {"north": 3, "south": 7, "west": 4, "east": None}
+    # symmetry: if a is b's south, b is a's north
+    for r in range(8):
+        dr = CartDecomp.create(8, r, 64, 64, (4, 2))
+        for k, opp in (("north", "south"), ("west", "east")):
+            p = dr.neighbors()[k]
+            if p is not None:
+                assert CartDecomp.create(8, p, 64, 64, (4, 2)).neighbors()[opp] == r
+
+
+def test_slab_matches_reference_axes():
+    d0 = CartDecomp.slab(4, 1, 512, 4096, axis=0)
+    assert (d0.py, d0.px) == (1, 4) and d0.local_shape == (512, 1024)
+    d1 = CartDecomp.slab(4, 1, 4096, 512, axis=1)
+    assert (d1.py, d1.px) == (4, 1) and d1.local_shape == (1024, 512)
+
+
+def test_select_device_reference_semantics():
+    # mpi_daxpy.cc:43-54: block mapping when oversubscribed
+    assert select_device(0, 1, 1) == (0, 1)
+    assert select_device(3, 8, 8) == (3, 1)
+    assert [select_device(r, 4, 1)[0] for r in range(4)] == [0, 0, 0, 0]
+    assert [select_device(r, 4, 2)[0] for r in range(4)] == [0, 0, 1, 1]
+    with pytest.raises(RuntimeError, match="not a multiple"):
+        select_device(0, 3, 2)
+
+
+def test_field_alignment():
+    f = Field2D(10, 33, 1, 1)
+    assert f.xo % 8 == 0 and f.ld % 64 == 0
+    assert f.interior.shape == (10, 33)
+    assert f.interior.stride(0) == f.ld
+    assert (f.interior.data_ptr() % 16) == 0
+    g = Field2D(5, 7, 2, 0)
+    assert g.xo == 0 and g.storage.shape[0] == 9

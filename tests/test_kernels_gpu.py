@@ -1,0 +1,211 @@
+"""Numerics of every hand-written HIP kernel vs a plain PyTorch fp64 reference.
+
+GPU-only (``-m gpu``).  Sizes include odd extents, non-multiples of 64/512,
+unaligned views (scalar fallback paths) and multi-block tails.
+"""
+import pytest
+import torch
+
+from gpu_mpi_tests_amd import _native, ops
+from gpu_mpi_tests_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _native.lib()  # must be the native path — fail loudly otherwise
+
+
+def _rand(*shape, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.rand(*shape, generator=g, dtype=torch.float64).to(DEV)
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 1023, 1024, 2048 * 3 + 5, 1 << 20])
+def test_daxpy(n):
+    x, y = _rand(n, seed=1), _rand(n, seed=2)
+    exp = 2.0 * x + y
+    ops.daxpy(2.0, x, y)
+    torch.cuda.synchronize()
+    assert torch.equal(y, exp)
+
+
+def test_daxpy_unaligned():
+    x, y = _rand(1001, seed=3), _rand(1001, seed=4)
+    xs, ys = x[1:], y[1:]  # 8-B aligned only -> scalar kernel
+    exp = 3.5 * xs + ys  # kernel contracts to one FMA: compare to 1 ulp-ish
+    ops.daxpy(3.5, xs, ys)
+    torch.testing.assert_close(ys, exp, rtol=1e-15, atol=1e-15)
+
+
+def test_daxpy_reference_closed_form():
+    # daxpy.cu:55-87: x = i+1, y = -(i+1), a = 2 -> SUM = n(n+1)/2 = 524800
+    x = torch.arange(1, 1025, dtype=torch.float64, device=DEV)
+    y = -x.clone()
+    ops.daxpy(2.0, x, y)
+    assert float(y.sum()) == 524800.0
+
+
+@pytest.mark.parametrize("n", [1, 5, 513, 65536, 65536 * 3 + 17])
+def test_stencil5_1d(n):
+    inp = _rand(n + 4, seed=5)
+    out = ops.stencil5_1d(inp, scale=3.0)
+    exp = ref.stencil5_1d(inp.cpu(), 3.0).to(DEV)
+    torch.testing.assert_close(out, exp, rtol=1e-13, atol=1e-13)
+
+
+@pytest.mark.parametrize("dim", [0, 1])
+@pytest.mark.parametrize("ny,nx", [(1, 9), (7, 13), (33, 1030), (130, 516), (64, 2049)])
+def test_stencil5_2d(dim, ny, nx):
+    z = _rand(ny + (4 if dim == 1 else 0), nx + (4 if dim == 0 else 0), seed=6)
+    out = ops.stencil5_2d(z, dim, scale=2.0)
+    exp = ref.stencil5_2d(z.cpu(), dim, 2.0).to(DEV)
+    torch.testing.assert_close(out, exp, rtol=1e-13, atol=1e-13)
+
+
+@pytest.mark.parametrize("dim", [0, 1])
+def test_stencil5_2d_strided_views(dim):
+    big = _rand(100, 700, seed=7)
+    inp = big[3:3 + 40 + (4 if dim == 1 else 0), 2:2 + 300 + (4 if dim == 0 else 0)]
+    outbig = torch.zeros(60, 800, dtype=torch.float64, device=DEV)
+    out = outbig[5:45, 10:310]
+    ops.stencil5_2d(inp, dim, out=out, scale=1.5)
+    exp = ref.stencil5_2d(inp.cpu(), dim, 1.5).to(DEV)
+    torch.testing.assert_close(out, exp, rtol=1e-13, atol=1e-13)
+    # untouched outside the view
+    assert float(outbig[:5].abs().sum()) == 0.0
+
+
+def test_stencil_exact_for_cubic():
+    # 4th-order central difference is exact for x^3
+    n, dx = 4096, 1e-3
+    z = torch.empty(16, n + 4, dtype=torch.float64, device=DEV)
+    ops.fill_poly(z, 0, -2 * dx, dx, 0.0, 0.1)
+    dz = ops.stencil5_2d(z, 0, scale=1.0 / dx)
+    exact = torch.empty_like(dz)
+    ops.fill_poly(exact, 1, 0.0, dx, 0.0, 0.1)
+    assert ops.diff_norm(dz, exact) < 1e-7
+
+
+@pytest.mark.parametrize("elem", [torch.float64, torch.float32])
+def test_copy2d_batched(elem):
+    src = torch.arange(50 * 40, dtype=elem, device=DEV).view(50, 40)
+    bufs = [torch.zeros(50, 2, dtype=elem, device=DEV), torch.zeros(50, 1, dtype=elem, device=DEV),
+            torch.zeros(3, 40, dtype=elem, device=DEV), torch.zeros(7, 33, dtype=elem, device=DEV)]
+    views = [src[:, 2:4], src[:, 39:40], src[10:13, :], src[1:8, 3:36]]
+    ops.copy2d_batched(list(zip(views, bufs)))
+    for v, b in zip(views, bufs):
+        assert torch.equal(v, b)
+    # unpack back into a different array
+    dst = torch.zeros_like(src)
+    ops.copy2d_batched([(b, dst[:, 2:4]) for b in bufs[:1]] + [(bufs[2], dst[10:13, :])])
+    assert torch.equal(dst[:, 2:4], src[:, 2:4]) and torch.equal(dst[10:13], src[10:13])
+
+
+def test_copy2d_many_descriptors():
+    src = _rand(64, 64, seed=8)
+    pairs = [(src[i : i + 1, :], torch.empty(1, 64, dtype=torch.float64, device=DEV)) for i in range(11)]
+    ops.copy2d_batched(pairs)
+    for s, d in pairs:
+        assert torch.equal(s, d)
+
+
+@pytest.mark.parametrize("keep", [0, 1])
+@pytest.mark.parametrize("ny,nx", [(1, 1), (3, 5), (1000, 1024), (1024, 9000), (77, 4097)])
+def test_sum_axis(keep, ny, nx):
+    z = _rand(ny, nx, seed=9)
+    out = ops.sum_axis(z, keep)
+    exp = ref.sum_axis(z.cpu(), keep).to(DEV)
+    torch.testing.assert_close(out, exp, rtol=1e-12, atol=1e-12)
+
+
+def test_sum_axis_reference_allreduce_value():
+    # test_sum: fill PI/world (world=1) -> each sum = PI * extent (mpi_stencil2d_gt.cc:598-611)
+    z = torch.full((2048, 1024), 3.141592653589793, dtype=torch.float64, device=DEV)
+    out = ops.sum_axis(z, 0)
+    torch.testing.assert_close(out, torch.full((1024,), 3.141592653589793 * 2048, dtype=torch.float64,
+                                               device=DEV), rtol=1e-13, atol=0)
+
+
+@pytest.mark.parametrize("ny,nx", [(1, 1), (5, 7), (300, 4100), (2, 100000)])
+def test_diff_sq(ny, nx):
+    a, b = _rand(ny, nx, seed=10), _rand(ny, nx, seed=11)
+    got = float(ops.diff_sq(a, b))
+    exp = float(ref.diff_sq(a.cpu(), b.cpu()))
+    assert abs(got - exp) <= 1e-12 * max(1.0, exp)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_fill_poly(mode):
+    z = torch.empty(37, 129, dtype=torch.float64, device=DEV)
+    ops.fill_poly(z, mode, -0.3, 0.01, 0.2, 0.02)
+    exp = ref.poly(mode, 129, 37, -0.3, 0.01, 0.2, 0.02).to(DEV)
+    torch.testing.assert_close(z, exp, rtol=1e-14, atol=1e-14)
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("ny,nx", [(1, 2), (3, 7), (33, 513), (64, 1024), (100, 1030)])
+def test_jacobi5(variant, ny, nx):
+    ops.set_jacobi_variant(variant)
+    try:
+        u = _rand(ny + 2, nx + 16, seed=12)
+        f = _rand(ny + 2, nx + 16, seed=13)
+        for ff, c1 in ((None, 0.0), (f, -0.01)):
+            un = torch.zeros_like(u)
+            un_ref = torch.zeros(u.shape, dtype=torch.float64)
+            r = ops.jacobi5(u, un, (8, nx, 1, ny), f=ff, c1=c1, resid=True)
+            r_ref = ref.jacobi5(u.cpu(), un_ref, 8, nx, 1, ny,
+                                ff.cpu() if ff is not None else None, 0.25, c1)
+            torch.testing.assert_close(un.cpu(), un_ref, rtol=1e-14, atol=1e-14)
+            assert abs(float(r) - float(r_ref)) <= 1e-11 * max(1.0, float(r_ref))
+    finally:
+        ops.set_jacobi_variant(0)
+
+
+def test_jacobi5_odd_origin_scalar_path():
+    u = _rand(20, 40, seed=14)
+    un, un_ref = torch.zeros_like(u), torch.zeros(20, 40, dtype=torch.float64)
+    ops.jacobi5(u, un, (3, 31, 2, 15))
+    ref.jacobi5(u.cpu(), un_ref, 3, 31, 2, 15)
+    torch.testing.assert_close(un.cpu(), un_ref, rtol=1e-14, atol=1e-14)
+
+
+def test_jacobi5_rects_frame():
+    u = _rand(34, 80, seed=15)
+    un, un_ref = torch.zeros_like(u), torch.zeros(34, 80, dtype=torch.float64)
+    rects = [(8, 64, 1, 1), (8, 64, 32, 1), (8, 2, 2, 30), (70, 2, 2, 30)]
+    ops.jacobi5_rects(u, un, rects)
+    for r in rects:
+        ref.jacobi5(u.cpu(), un_ref, *r)
+    torch.testing.assert_close(un.cpu(), un_ref, rtol=1e-14, atol=1e-14)
+
+
+def test_jacobi_model_single_gpu_matches_cpu():
+    from gpu_mpi_tests_amd.models.jacobi import Jacobi2D
+    from gpu_mpi_tests_amd.parallel import dist as gdist
+
+    env_gpu = gdist.DistEnv(device=torch.device("cuda", 0), n_devices=1)
+    env_cpu = gdist.DistEnv(device=torch.device("cpu"))
+    a = Jacobi2D(70, 90, env=env_gpu)
+    b = Jacobi2D(70, 90, env=env_cpu)
+    for _ in range(7):
+        a.step()
+        b.step()
+    torch.testing.assert_close(a.u.interior.cpu(), b.u.interior, rtol=1e-13, atol=1e-13)
+
+
+def test_stream_semantics():
+    """Kernels run on the caller's current stream."""
+    s = torch.cuda.Stream()
+    x, y = _rand(1 << 20, seed=16), _rand(1 << 20, seed=17)
+    exp = 2.0 * x + y
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        ops.daxpy(2.0, x, y)
+    s.synchronize()
+    assert torch.equal(y, exp)
