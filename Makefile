@@ -1,46 +1,117 @@
 # gpu-mpi-tests-amd — native build (gfx950 / CDNA4 only).
 #
-#   make            -> libgmt.so (kernels, C ABI) + native MPI apps in build/bin
-#   make lib        -> gpu_mpi_tests_amd/_lib/libgmt.so only
-#   make apps       -> build/bin/{daxpy, mpi_daxpy, mpi_stencil2d_gt, ...}
+#   make            -> HIP libs + host libs + every native MPI app (HIP and host builds)
+#   make lib        -> gpu_mpi_tests_amd/_lib/libgmt.so (+ libgmt_ccl.so): kernels, runtime, RCCL
+#   make host       -> build/lib-host/libgmt.so (+ libgmt_ccl.so): the CPU backend (same ABI)
+#   make apps       -> build/bin/<app> (HIP) and build/bin-host/<app> (CPU backend)
 #
-# No CUDA, no SYCL, no gtensor: every kernel is hand-written HIP for gfx950
-# and every binary is plain C++17 + HIP + MPI (+ RCCL, roctx).
+# The apps are compiled ONCE (plain C++17 + MPI against gmt/rt.h, gmt/kernels.h,
+# gmt/ccl.h) and linked twice; only the runtime library differs.  No CUDA, no
+# SYCL, no gtensor, no #ifdef dual paths: the kernels are hand-written HIP for gfx950.
 
 ROCM      ?= /opt/rocm
 MPI_HOME  ?= /opt/conda
 ARCH      ?= gfx950
 HIPCC     ?= $(ROCM)/bin/hipcc
-CXX_HOST  ?= g++
+CXX       := g++
 
 BUILD     := build
 OBJ       := $(BUILD)/obj
 BIN       := $(BUILD)/bin
+BINH      := $(BUILD)/bin-host
 LIBDIR    := gpu_mpi_tests_amd/_lib
+LIBH_DIR  := $(BUILD)/lib-host
 LIB       := $(LIBDIR)/libgmt.so
+LIB_CCL   := $(LIBDIR)/libgmt_ccl.so
+LIBH      := $(LIBH_DIR)/libgmt.so
+LIBH_CCL  := $(LIBH_DIR)/libgmt_ccl.so
 
 HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
              -Icsrc/include -munsafe-fp-atomics
-HOSTFLAGS := -O2 -std=c++17 -fPIC -Wall -Icsrc/include -I$(ROCM)/include -D__HIP_PLATFORM_AMD__=1
+ROCM_HOST := -O2 -std=c++17 -fPIC -Wall -Icsrc/include -I$(ROCM)/include -D__HIP_PLATFORM_AMD__=1
+HOSTFLAGS := -O3 -std=c++17 -fPIC -Wall -Icsrc/include
+APPFLAGS  := -O2 -std=c++17 -Wall -Icsrc/include -Icsrc/apps -I$(MPI_HOME)/include
+MPI_LIBS  := $(MPI_HOME)/lib/libmpi.so -Wl,-rpath,$(MPI_HOME)/lib -static-libstdc++ -static-libgcc
 
 KERNEL_SRCS := $(wildcard csrc/kernels/*.hip)
 KERNEL_OBJS := $(patsubst csrc/kernels/%.hip,$(OBJ)/kernels/%.o,$(KERNEL_SRCS))
 KERNEL_HDRS := $(wildcard csrc/kernels/*.hpp) csrc/include/gmt/kernels.h
+RT_OBJ      := $(OBJ)/runtime/rt_hip.o
+CCL_OBJ     := $(OBJ)/runtime/ccl_rccl.o
+HOST_OBJS   := $(OBJ)/host/kernels_host.o $(OBJ)/host/rt_host.o
+HOSTCCL_OBJ := $(OBJ)/host/ccl_stub.o
+COMM_OBJS   := $(OBJ)/comm/transport.o
+APP_HDRS    := $(wildcard csrc/include/gmt/*.hpp csrc/include/gmt/*.h csrc/apps/*.hpp)
 
-.PHONY: all lib apps clean
-all: lib apps
+# reference binary names (Makefile:2, CMakeLists.txt:22-82) + MI355X additions
+APPS := daxpy daxpy_nvtx mpi_daxpy mpi_daxpy_nvtx_managed mpi_daxpy_nvtx_unmanaged \
+        mpienv mpigatherinplace mpi_daxpy_gt mpi_stencil_gt mpi_stencil2d_gt \
+        mpi_stencil2d_sycl mpi_stencil2d_sycl_oo mpi_jacobi2d mpi_halo_bench
 
-lib: $(LIB)
+.PHONY: all lib host apps clean
+all: lib host apps
+
+lib: $(LIB) $(LIB_CCL)
+host: $(LIBH) $(LIBH_CCL)
 
 $(OBJ)/kernels/%.o: csrc/kernels/%.hip $(KERNEL_HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(KERNEL_OBJS)
-	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libgmt.so
+$(OBJ)/runtime/%.o: csrc/runtime/%.cpp csrc/include/gmt/rt.h csrc/include/gmt/ccl.h
+	@mkdir -p $(dir $@)
+	$(CXX) $(ROCM_HOST) -c $< -o $@
 
--include apps.mk
+$(LIB): $(KERNEL_OBJS) $(RT_OBJ)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libgmt.so \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lrocprofiler-sdk-roctx -ldl
+
+$(LIB_CCL): $(CCL_OBJ) $(LIB)
+	$(CXX) -shared -fPIC -o $@ $(CCL_OBJ) -Wl,-soname,libgmt_ccl.so \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lrccl -lamdhip64
+
+$(OBJ)/host/%.o: csrc/host/%.cpp csrc/include/gmt/rt.h csrc/include/gmt/kernels.h csrc/include/gmt/ccl.h
+	@mkdir -p $(dir $@)
+	$(CXX) $(HOSTFLAGS) -c $< -o $@
+
+$(LIBH): $(HOST_OBJS)
+	@mkdir -p $(LIBH_DIR)
+	$(CXX) -shared -fPIC -o $@ $^ -Wl,-soname,libgmt.so
+
+$(LIBH_CCL): $(HOSTCCL_OBJ)
+	@mkdir -p $(LIBH_DIR)
+	$(CXX) -shared -fPIC -o $@ $^ -Wl,-soname,libgmt_ccl.so
+
+$(OBJ)/comm/%.o: csrc/comm/%.cpp $(APP_HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(APPFLAGS) -c $< -o $@
+
+$(OBJ)/apps/%.o: csrc/apps/%.cpp $(APP_HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(APPFLAGS) -c $< -o $@
+
+$(OBJ)/apps/mpi_daxpy_nvtx_managed.o: csrc/apps/mpi_daxpy_nvtx.cpp $(APP_HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(APPFLAGS) -DGMT_MANAGED -c $< -o $@
+
+$(OBJ)/apps/mpi_daxpy_nvtx_unmanaged.o: csrc/apps/mpi_daxpy_nvtx.cpp $(APP_HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(APPFLAGS) -c $< -o $@
+
+apps: $(addprefix $(BIN)/,$(APPS)) $(addprefix $(BINH)/,$(APPS))
+
+$(BIN)/%: $(OBJ)/apps/%.o $(COMM_OBJS) $(LIB) $(LIB_CCL)
+	@mkdir -p $(BIN)
+	$(CXX) -o $@ $< $(COMM_OBJS) -L$(LIBDIR) -lgmt -lgmt_ccl \
+	  -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,$(ROCM)/lib $(MPI_LIBS)
+
+$(BINH)/%: $(OBJ)/apps/%.o $(COMM_OBJS) $(LIBH) $(LIBH_CCL)
+	@mkdir -p $(BINH)
+	$(CXX) -o $@ $< $(COMM_OBJS) -L$(LIBH_DIR) -lgmt -lgmt_ccl \
+	  -Wl,-rpath,'$$ORIGIN/../lib-host' $(MPI_LIBS)
+
+.SECONDARY:
 
 clean:
-	rm -rf $(BUILD) $(LIB)
+	rm -rf $(BUILD) $(LIB) $(LIB_CCL)

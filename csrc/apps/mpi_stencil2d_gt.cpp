@@ -1,0 +1,136 @@
+// mpi_stencil2d_gt — the reference's main benchmark, MI355X-native.
+//
+// Reference: /root/reference/mpi_stencil2d_gt.cc:651-734.  Same positional
+// CLI `[n_local_deriv] [n_iter]`, same header, same 8 test_deriv lines
+// ({dim0, dim1} x {device, managed} x {buf 1, 0}) and 4 test_sum lines, same
+// timing semantics (exchange wall time summed over timed iterations and over
+// ranks, MPI_Reduce to rank 0).
+//
+// Options (not in the reference):
+//   --transport=auto|mpi-host|mpi-direct|rccl|ipc   force one data plane
+//   --no-managed          skip the managed-memory variants (TEST_MANAGED off)
+//   --tests=deriv,sum     subset
+//   --host-init --host-verify   reference host loops instead of GPU fill/check
+//   --alloc-per-call      re-create halo buffers inside the timed region (gt parity)
+//   --json=FILE           one JSON record per test (per-exchange µs, GB/s, transport)
+#include <mpi.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+
+#include "deriv_common.hpp"
+#include "gmt/device.hpp"
+
+using namespace gmt;
+using namespace gmt::apps;
+
+int main(int argc, char** argv) {
+  Cli cli(argc, argv);
+  size_t n_local_deriv = 1024;
+  int n_iter = 1000;
+  const int n_warmup = 5;
+  if (cli.positional(0)) n_local_deriv = std::atol(cli.positional(0));
+  if (cli.positional(1)) n_iter = std::atoi(cli.positional(1));
+  const size_t n_global_other = static_cast<size_t>(cli.geti("n-other", 512 * 1024));
+  const bool managed = !cli.flag("no-managed");
+  const std::string tests = cli.get("tests", "deriv,sum");
+  const std::string json = cli.get("json", "");
+
+  GMT_MPI_CHECK(MPI_Init(&argc, &argv));
+  int world_size = 1, world_rank = 0;
+  GMT_MPI_CHECK(MPI_Comm_size(MPI_COMM_WORLD, &world_size));
+  GMT_MPI_CHECK(MPI_Comm_rank(MPI_COMM_WORLD, &world_rank));
+  const size_t n_global_deriv = n_local_deriv * world_size;
+
+  RankBinding b = set_rank_device(MPI_COMM_WORLD, false);
+
+  if (world_rank == 0) {
+    std::printf("n procs        = %d\n", world_size);
+    std::printf("n_global_deriv = %zu\n", n_global_deriv);
+    std::printf("n_global_other = %zu\n", n_global_other);
+    std::printf("n_iter         = %d\n", n_iter);
+    std::printf("n_warmup       = %d\n", n_warmup);
+    std::printf("# backend=%s device=%s arch=%s managed_memory=%d xnack=%d\n",
+                gmt_rt_backend_name(), b.info.name, b.info.arch, b.info.managed_memory,
+                b.info.xnack);
+  }
+  std::fflush(stdout);
+
+  auto pool_owner = std::make_unique<TransportPool>(MPI_COMM_WORLD, b);
+  TransportPool& pool = *pool_owner;
+  const comm::Kind want = comm::parse_kind(cli.get("transport", "auto"));
+
+  auto report = [&](const char* name, int dim, int space, bool buf, const DerivResult& r) {
+    double time_sum = 0, err_sum = 0;
+    MPI_Reduce(&r.total_time, &time_sum, 1, MPI_DOUBLE, MPI_SUM, 0, MPI_COMM_WORLD);
+    MPI_Reduce(&r.err_norm, &err_sum, 1, MPI_DOUBLE, MPI_SUM, 0, MPI_COMM_WORLD);
+    double med = r.iters.median(), mx = 0;
+    MPI_Allreduce(&med, &mx, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+    if (world_rank == 0) {
+      std::printf("TEST dim:%d, %s, buf:%d; %0.8f, err=%0.8f\n", dim,
+                  space == GMT_SPACE_MANAGED ? "managed" : "device ", buf ? 1 : 0, time_sum,
+                  err_sum);
+      JsonRecord j;
+      j.add("app", "mpi_stencil2d_gt").add("test", name).add("dim", dim)
+          .add("mem", space == GMT_SPACE_MANAGED ? "managed" : "device").add("buf", buf)
+          .add("ranks", world_size).add("transport", r.transport).add("n_local_deriv", n_local_deriv)
+          .add("n_other", n_global_other).add("iters", n_iter).add("time_sum_s", time_sum)
+          .add("err_sum", err_sum).add("exchange_us_median_max_rank", mx * 1e6)
+          .add("bytes_per_exchange", r.bytes_per_exchange)
+          .add("GBps_per_rank", mx > 0 ? r.bytes_per_exchange / mx / 1e9 : 0.0);
+      j.append_to(json);
+    }
+    std::fflush(stdout);
+  };
+
+  if (tests.find("deriv") != std::string::npos) {
+    for (int dim = 0; dim < 2; ++dim) {
+      for (int m = 0; m < (managed ? 2 : 1); ++m) {
+        for (int buf = 1; buf >= 0; --buf) {
+          DerivConfig c;
+          c.dim = dim;
+          c.n_local = n_local_deriv;
+          c.n_other = n_global_other;
+          c.n_iter = n_iter;
+          c.n_warmup = n_warmup;
+          c.space = m ? GMT_SPACE_MANAGED : GMT_SPACE_DEVICE;
+          c.buf = buf;
+          c.transport = want;
+          c.host_init = cli.flag("host-init");
+          c.host_verify = cli.flag("host-verify");
+          c.realloc_per_call = cli.flag("alloc-per-call");
+          DerivResult r = run_deriv(c, b, MPI_COMM_WORLD, pool);
+          report("deriv", dim, c.space, buf, r);
+        }
+      }
+    }
+  }
+  if (tests.find("sum") != std::string::npos) {
+    for (int dim = 0; dim < 2; ++dim) {
+      for (int m = 0; m < (managed ? 2 : 1); ++m) {
+        const int space = m ? GMT_SPACE_MANAGED : GMT_SPACE_DEVICE;
+        SumResult r = run_sum(dim, space, n_local_deriv, n_global_other, n_iter, n_warmup, want,
+                              b, pool);
+        double time_sum = 0, err = r.max_abs_err, err_max = 0;
+        MPI_Reduce(&r.total_time, &time_sum, 1, MPI_DOUBLE, MPI_SUM, 0, MPI_COMM_WORLD);
+        MPI_Reduce(&err, &err_max, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
+        if (world_rank == 0) {
+          std::printf("TEST dim:%d, %s, buf:0; allreduce=%0.8f\n", dim,
+                      m ? "managed" : "device ", time_sum);
+          if (err_max > 1e-9) std::printf("# WARNING allreduce value rel err %g\n", err_max);
+          JsonRecord j;
+          j.add("app", "mpi_stencil2d_gt").add("test", "sum").add("dim", dim)
+              .add("mem", m ? "managed" : "device").add("ranks", world_size)
+              .add("transport", r.transport).add("iters", n_iter).add("time_sum_s", time_sum)
+              .add("allreduce_us_median", r.iters.median() * 1e6).add("value_rel_err", err_max);
+          j.append_to(json);
+        }
+        std::fflush(stdout);
+      }
+    }
+  }
+  pool_owner.reset();
+  MPI_Finalize();
+  return EXIT_SUCCESS;
+}

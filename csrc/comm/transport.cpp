@@ -1,0 +1,453 @@
+// Transport implementations: mpi-host, mpi-direct, rccl, ipc (gmt/comm.hpp).
+#include <algorithm>
+#include <climits>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+
+#include "gmt/buffer.hpp"
+#include "gmt/comm.hpp"
+
+namespace gmt {
+namespace comm {
+
+namespace {
+
+// MPI counts are int: send doubles when possible so 8-B aligned payloads up
+// to 16 GiB fit in one message (mpigatherinplace moves 1 GiB per rank).
+void mpi_count(size_t bytes, MPI_Datatype* t, int* n) {
+  if (bytes % 8 == 0 && bytes / 8 <= static_cast<size_t>(INT_MAX)) {
+    *t = MPI_DOUBLE;
+    *n = static_cast<int>(bytes / 8);
+  } else if (bytes <= static_cast<size_t>(INT_MAX)) {
+    *t = MPI_BYTE;
+    *n = static_cast<int>(bytes);
+  } else {
+    std::printf("gmt::comm: message of %zu bytes exceeds one MPI message\n", bytes);
+    abort_job(2);
+  }
+}
+
+void isend(const void* p, size_t bytes, int peer, int tag, MPI_Comm c, MPI_Request* r) {
+  MPI_Datatype t;
+  int n;
+  mpi_count(bytes, &t, &n);
+  GMT_MPI_CHECK(MPI_Isend(p, n, t, peer, tag, c, r));
+}
+void irecv(void* p, size_t bytes, int peer, int tag, MPI_Comm c, MPI_Request* r) {
+  MPI_Datatype t;
+  int n;
+  mpi_count(bytes, &t, &n);
+  GMT_MPI_CHECK(MPI_Irecv(p, n, t, peer, tag, c, r));
+}
+void waitall(std::vector<MPI_Request>& reqs, const char* what) {
+  if (reqs.empty()) return;
+  std::vector<MPI_Status> st(reqs.size());
+  int rv = MPI_Waitall(static_cast<int>(reqs.size()), reqs.data(), st.data());
+  if (rv != MPI_SUCCESS) {
+    std::printf("%s error: %d (%d)\n", what, rv, st[0].MPI_ERROR);
+    abort_job(2);
+  }
+  reqs.clear();
+}
+
+// Host-staged collectives shared by the mpi-host and ipc transports.
+void staged_allreduce(MPI_Comm c, double* buf, size_t n, gmt_stream_t s) {
+  Buffer<double> h(n, GMT_SPACE_PINNED);
+  GMT_CHECK("allreduce D2H", gmt_rt_memcpy_async(h.data(), buf, n * sizeof(double), s));
+  GMT_CHECK("allreduce sync", gmt_rt_stream_synchronize(s));
+  GMT_MPI_CHECK(MPI_Allreduce(MPI_IN_PLACE, h.data(), static_cast<int>(n), MPI_DOUBLE, MPI_SUM, c));
+  GMT_CHECK("allreduce H2D", gmt_rt_memcpy_async(buf, h.data(), n * sizeof(double), s));
+  GMT_CHECK("allreduce sync", gmt_rt_stream_synchronize(s));
+}
+void staged_allgather(MPI_Comm c, int rank, int size, const void* send, void* recv, size_t bpr,
+                      gmt_stream_t s) {
+  Buffer<char> h(bpr * size, GMT_SPACE_PINNED);
+  GMT_CHECK("allgather D2H", gmt_rt_memcpy_async(h.data() + rank * bpr, send, bpr, s));
+  GMT_CHECK("allgather sync", gmt_rt_stream_synchronize(s));
+  MPI_Datatype t;
+  int n;
+  mpi_count(bpr, &t, &n);
+  GMT_MPI_CHECK(MPI_Allgather(MPI_IN_PLACE, 0, t, h.data(), n, t, c));
+  GMT_CHECK("allgather H2D", gmt_rt_memcpy_async(recv, h.data(), bpr * size, s));
+  GMT_CHECK("allgather sync", gmt_rt_stream_synchronize(s));
+}
+
+// ------------------------------------------------------------------ mpi-host
+class MpiHostExchange : public Exchange {
+ public:
+  MpiHostExchange(MPI_Comm c, std::vector<Msg> r, std::vector<Msg> s)
+      : c_(c), recvs_(std::move(r)), sends_(std::move(s)) {
+    for (auto& m : recvs_) rstage_.emplace_back(m.bytes, GMT_SPACE_PINNED);
+    for (auto& m : sends_) sstage_.emplace_back(m.bytes, GMT_SPACE_PINNED);
+    GMT_CHECK("event", gmt_rt_event_create(&h2d_done_, 0));
+  }
+  ~MpiHostExchange() override { gmt_rt_event_destroy(h2d_done_); }
+  void start(gmt_stream_t s) override {
+    // the previous exchange's H2D copies must have drained the recv staging
+    if (armed_) GMT_CHECK("staging reuse", gmt_rt_event_synchronize(h2d_done_));
+    for (size_t i = 0; i < recvs_.size(); ++i) {
+      reqs_.emplace_back();
+      irecv(rstage_[i].data(), recvs_[i].bytes, recvs_[i].peer, recvs_[i].tag, c_, &reqs_.back());
+    }
+    for (size_t i = 0; i < sends_.size(); ++i)
+      GMT_CHECK("stage D2H", gmt_rt_memcpy_async(sstage_[i].data(), sends_[i].buf,
+                                                 sends_[i].bytes, s));
+    GMT_CHECK("stage sync", gmt_rt_stream_synchronize(s));
+    for (size_t i = 0; i < sends_.size(); ++i) {
+      reqs_.emplace_back();
+      isend(sstage_[i].data(), sends_[i].bytes, sends_[i].peer, sends_[i].tag, c_, &reqs_.back());
+    }
+  }
+  void wait(gmt_stream_t s) override {
+    waitall(reqs_, "mpi-host exchange");
+    for (size_t i = 0; i < recvs_.size(); ++i)
+      GMT_CHECK("stage H2D", gmt_rt_memcpy_async(recvs_[i].buf, rstage_[i].data(),
+                                                 recvs_[i].bytes, s));
+    GMT_CHECK("event", gmt_rt_event_record(h2d_done_, s));
+    armed_ = true;
+  }
+
+ private:
+  MPI_Comm c_;
+  std::vector<Msg> recvs_, sends_;
+  std::vector<Buffer<char>> rstage_, sstage_;
+  std::vector<MPI_Request> reqs_;
+  gmt_event_t h2d_done_ = nullptr;
+  bool armed_ = false;
+};
+
+class MpiHostTransport : public Transport {
+ public:
+  explicit MpiHostTransport(MPI_Comm c) : Transport(c) {}
+  Kind kind() const override { return Kind::MpiHost; }
+  const char* name() const override { return "mpi-host"; }
+  std::unique_ptr<Exchange> plan(const std::vector<Msg>& r, const std::vector<Msg>& s) override {
+    return std::make_unique<MpiHostExchange>(comm_, r, s);
+  }
+  void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override {
+    staged_allreduce(comm_, buf, n, s);
+  }
+  void allgather(const void* send, void* recv, size_t bpr, gmt_stream_t s) override {
+    staged_allgather(comm_, rank_, size_, send, recv, bpr, s);
+  }
+};
+
+// ---------------------------------------------------------------- mpi-direct
+class MpiDirectExchange : public Exchange {
+ public:
+  MpiDirectExchange(MPI_Comm c, std::vector<Msg> r, std::vector<Msg> s)
+      : c_(c), recvs_(std::move(r)), sends_(std::move(s)) {}
+  void start(gmt_stream_t s) override {
+    // one sync covers both "send data produced" and "earlier readers of the
+    // ghost cells are done" before MPI may write them
+    GMT_CHECK("direct sync", gmt_rt_stream_synchronize(s));
+    for (auto& m : recvs_) {
+      reqs_.emplace_back();
+      irecv(m.buf, m.bytes, m.peer, m.tag, c_, &reqs_.back());
+    }
+    for (auto& m : sends_) {
+      reqs_.emplace_back();
+      isend(m.buf, m.bytes, m.peer, m.tag, c_, &reqs_.back());
+    }
+  }
+  void wait(gmt_stream_t) override { waitall(reqs_, "mpi-direct exchange"); }
+
+ private:
+  MPI_Comm c_;
+  std::vector<Msg> recvs_, sends_;
+  std::vector<MPI_Request> reqs_;
+};
+
+class MpiDirectTransport : public Transport {
+ public:
+  explicit MpiDirectTransport(MPI_Comm c) : Transport(c) {}
+  Kind kind() const override { return Kind::MpiDirect; }
+  const char* name() const override { return "mpi-direct"; }
+  std::unique_ptr<Exchange> plan(const std::vector<Msg>& r, const std::vector<Msg>& s) override {
+    return std::make_unique<MpiDirectExchange>(comm_, r, s);
+  }
+  void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override {
+    GMT_CHECK("allreduce sync", gmt_rt_stream_synchronize(s));
+    GMT_MPI_CHECK(MPI_Allreduce(MPI_IN_PLACE, buf, static_cast<int>(n), MPI_DOUBLE, MPI_SUM, comm_));
+  }
+  void allgather(const void* send, void* recv, size_t bpr, gmt_stream_t s) override {
+    GMT_CHECK("allgather sync", gmt_rt_stream_synchronize(s));
+    MPI_Datatype t;
+    int n;
+    mpi_count(bpr, &t, &n);
+    const bool inplace = send == static_cast<const char*>(recv) + rank_ * bpr;
+    GMT_MPI_CHECK(MPI_Allgather(inplace ? MPI_IN_PLACE : send, inplace ? 0 : n, t, recv, n, t, comm_));
+  }
+};
+
+// ---------------------------------------------------------------------- rccl
+class RcclExchange : public Exchange {
+ public:
+  RcclExchange(gmt_ccl_comm_t cc, std::vector<Msg> r, std::vector<Msg> s)
+      : cc_(cc), recvs_(std::move(r)), sends_(std::move(s)) {
+    // Within one group, messages between a pair of ranks are matched in
+    // issue order: sort both sides by (peer, tag) so the k-th send to B is
+    // B's k-th receive from us.
+    auto key = [](const Msg& a, const Msg& b) {
+      return a.peer != b.peer ? a.peer < b.peer : a.tag < b.tag;
+    };
+    std::sort(recvs_.begin(), recvs_.end(), key);
+    std::sort(sends_.begin(), sends_.end(), key);
+  }
+  void start(gmt_stream_t s) override {
+    GMT_CCL_CHECK("group start", gmt_ccl_group_start());
+    for (auto& m : recvs_) GMT_CCL_CHECK("recv", gmt_ccl_recv(m.buf, m.bytes, m.peer, cc_, s));
+    for (auto& m : sends_) GMT_CCL_CHECK("send", gmt_ccl_send(m.buf, m.bytes, m.peer, cc_, s));
+    GMT_CCL_CHECK("group end", gmt_ccl_group_end());
+  }
+  void wait(gmt_stream_t) override {}  // stream-ordered on s already
+
+ private:
+  gmt_ccl_comm_t cc_;
+  std::vector<Msg> recvs_, sends_;
+};
+
+class RcclTransport : public Transport {
+ public:
+  RcclTransport(MPI_Comm c, const RankBinding& b) : Transport(c) {
+    if (!gmt_ccl_available()) {
+      std::printf("ERROR: transport rccl requested but this build has no RCCL (%s backend)\n",
+                  gmt_rt_backend_name());
+      abort_job(EXIT_FAILURE);
+    }
+    int worst = b.ranks_per_device;
+    MPI_Allreduce(MPI_IN_PLACE, &worst, 1, MPI_INT, MPI_MAX, c);
+    if (worst > 1) {
+      std::printf("ERROR: transport rccl needs one rank per GPU (%d ranks share a GPU); "
+                  "use --transport=ipc or mpi-host\n", worst);
+      abort_job(EXIT_FAILURE);
+    }
+    gmt_ccl_id id;
+    std::memset(&id, 0, sizeof(id));
+    if (rank_ == 0) GMT_CCL_CHECK("unique id", gmt_ccl_get_unique_id(&id));
+    GMT_MPI_CHECK(MPI_Bcast(&id, sizeof(id), MPI_BYTE, 0, c));
+    GMT_CCL_CHECK("comm init", gmt_ccl_comm_init(&cc_, size_, &id, rank_));
+  }
+  ~RcclTransport() override { gmt_ccl_comm_destroy(cc_); }
+  Kind kind() const override { return Kind::Rccl; }
+  const char* name() const override { return "rccl"; }
+  std::unique_ptr<Exchange> plan(const std::vector<Msg>& r, const std::vector<Msg>& s) override {
+    return std::make_unique<RcclExchange>(cc_, r, s);
+  }
+  void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override {
+    GMT_CCL_CHECK("allreduce", gmt_ccl_allreduce_sum_f64(buf, buf, n, cc_, s));
+  }
+  void allgather(const void* send, void* recv, size_t bpr, gmt_stream_t s) override {
+    GMT_CCL_CHECK("allgather", gmt_ccl_allgather(send, recv, bpr, cc_, s));
+  }
+
+ private:
+  gmt_ccl_comm_t cc_ = nullptr;
+};
+
+// ----------------------------------------------------------------------- ipc
+constexpr int kHandleTag = 30000, kReadyTag = 10000, kDoneTag = 20000;
+
+struct IpcWire {
+  gmt_ipc_handle h;
+  uint64_t offset;
+};
+
+// hipIpcOpenMemHandle maps an allocation once per process: cache by handle.
+class IpcCache {
+ public:
+  void* open(const gmt_ipc_handle& h) {
+    std::string k(reinterpret_cast<const char*>(h.bytes), sizeof(h.bytes));
+    auto it = map_.find(k);
+    if (it != map_.end()) {
+      ++it->second.refs;
+      return it->second.base;
+    }
+    void* base = nullptr;
+    GMT_CHECK("ipc open", gmt_rt_ipc_open(&base, &h));
+    map_[k] = {base, 1};
+    return base;
+  }
+  void close(void* base) {
+    for (auto it = map_.begin(); it != map_.end(); ++it)
+      if (it->second.base == base && --it->second.refs == 0) {
+        GMT_WARN("ipc close", gmt_rt_ipc_close(base));
+        map_.erase(it);
+        return;
+      }
+  }
+
+ private:
+  struct E {
+    void* base;
+    int refs;
+  };
+  std::map<std::string, E> map_;
+};
+
+class IpcExchange : public Exchange {
+ public:
+  IpcExchange(MPI_Comm c, int rank, IpcCache* cache, gmt_stream_t copy_stream, std::vector<Msg> r,
+              std::vector<Msg> s)
+      : c_(c), rank_(rank), cache_(cache), cs_(copy_stream), recvs_(std::move(r)),
+        sends_(std::move(s)) {
+    // export every receive buffer to the rank that will write it
+    std::vector<IpcWire> out(recvs_.size()), in(sends_.size());
+    std::vector<MPI_Request> reqs;
+    for (size_t i = 0; i < sends_.size(); ++i) {
+      if (sends_[i].peer == rank_) continue;
+      reqs.emplace_back();
+      GMT_MPI_CHECK(MPI_Irecv(&in[i], sizeof(IpcWire), MPI_BYTE, sends_[i].peer,
+                              sends_[i].tag + kHandleTag, c_, &reqs.back()));
+    }
+    for (size_t i = 0; i < recvs_.size(); ++i) {
+      if (recvs_[i].peer == rank_) continue;
+      size_t off = 0;
+      GMT_CHECK("ipc get handle", gmt_rt_ipc_get_handle(&out[i].h, &off, recvs_[i].buf));
+      out[i].offset = off;
+      reqs.emplace_back();
+      GMT_MPI_CHECK(MPI_Isend(&out[i], sizeof(IpcWire), MPI_BYTE, recvs_[i].peer,
+                              recvs_[i].tag + kHandleTag, c_, &reqs.back()));
+    }
+    waitall(reqs, "ipc handle exchange");
+    remote_.resize(sends_.size(), nullptr);
+    for (size_t i = 0; i < sends_.size(); ++i) {
+      if (sends_[i].peer == rank_) {
+        // a message to ourselves (periodic single rank): local copy
+        for (auto& m : recvs_)
+          if (m.peer == rank_ && m.tag == sends_[i].tag) remote_[i] = m.buf;
+        if (!remote_[i]) {
+          std::printf("ipc: no self-receive for tag %d\n", sends_[i].tag);
+          abort_job(2);
+        }
+        continue;
+      }
+      void* base = cache_->open(in[i].h);
+      opened_.push_back(base);
+      remote_[i] = static_cast<char*>(base) + in[i].offset;
+    }
+  }
+  ~IpcExchange() override {
+    for (void* b : opened_) cache_->close(b);
+  }
+  void start(gmt_stream_t s) override {
+    // (1) our send data is produced and every earlier reader of our ghost
+    //     cells has finished, so (2) we may grant our writers access
+    GMT_CHECK("ipc sync", gmt_rt_stream_synchronize(s));
+    std::vector<MPI_Request> ready;
+    for (auto& m : recvs_)
+      if (m.peer != rank_) {
+        ready.emplace_back();
+        GMT_MPI_CHECK(MPI_Isend(&token_, 0, MPI_BYTE, m.peer, m.tag + kReadyTag, c_, &ready.back()));
+      }
+    for (auto& m : sends_)
+      if (m.peer != rank_) {
+        ready.emplace_back();
+        GMT_MPI_CHECK(MPI_Irecv(&token_, 0, MPI_BYTE, m.peer, m.tag + kReadyTag, c_, &ready.back()));
+      }
+    waitall(ready, "ipc ready");
+    // (3) write straight into the neighbours' receive buffers (xGMI / same GPU)
+    for (size_t i = 0; i < sends_.size(); ++i)
+      GMT_CHECK("ipc copy", gmt_rt_memcpy_async(remote_[i], sends_[i].buf, sends_[i].bytes, cs_));
+    GMT_CHECK("ipc copy sync", gmt_rt_stream_synchronize(cs_));
+    // (4) tell the receivers their data has landed
+    for (auto& m : sends_)
+      if (m.peer != rank_) {
+        done_.emplace_back();
+        GMT_MPI_CHECK(MPI_Isend(&token_, 0, MPI_BYTE, m.peer, m.tag + kDoneTag, c_, &done_.back()));
+      }
+    for (auto& m : recvs_)
+      if (m.peer != rank_) {
+        done_.emplace_back();
+        GMT_MPI_CHECK(MPI_Irecv(&token_, 0, MPI_BYTE, m.peer, m.tag + kDoneTag, c_, &done_.back()));
+      }
+  }
+  void wait(gmt_stream_t) override { waitall(done_, "ipc done"); }
+
+ private:
+  MPI_Comm c_;
+  int rank_;
+  IpcCache* cache_;
+  gmt_stream_t cs_;
+  std::vector<Msg> recvs_, sends_;
+  std::vector<void*> remote_, opened_;
+  std::vector<MPI_Request> done_;
+  char token_ = 0;
+};
+
+class IpcTransport : public Transport {
+ public:
+  explicit IpcTransport(MPI_Comm c) : Transport(c) {
+    GMT_CHECK("ipc copy stream", gmt_rt_stream_create(&cs_, 1));
+  }
+  ~IpcTransport() override { gmt_rt_stream_destroy(cs_); }
+  Kind kind() const override { return Kind::Ipc; }
+  const char* name() const override { return "ipc"; }
+  std::unique_ptr<Exchange> plan(const std::vector<Msg>& r, const std::vector<Msg>& s) override {
+    return std::make_unique<IpcExchange>(comm_, rank_, &cache_, cs_, r, s);
+  }
+  void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override {
+    staged_allreduce(comm_, buf, n, s);
+  }
+  void allgather(const void* send, void* recv, size_t bpr, gmt_stream_t s) override {
+    staged_allgather(comm_, rank_, size_, send, recv, bpr, s);
+  }
+
+ private:
+  gmt_stream_t cs_ = nullptr;
+  IpcCache cache_;
+};
+
+}  // namespace
+
+Kind parse_kind(const std::string& s) {
+  if (s == "auto" || s.empty()) return Kind::Auto;
+  if (s == "mpi-host" || s == "host" || s == "staged") return Kind::MpiHost;
+  if (s == "mpi-direct" || s == "direct" || s == "mpi") return Kind::MpiDirect;
+  if (s == "rccl" || s == "nccl") return Kind::Rccl;
+  if (s == "ipc" || s == "hip-ipc") return Kind::Ipc;
+  std::printf("ERROR: unknown transport '%s' (auto|mpi-host|mpi-direct|rccl|ipc)\n", s.c_str());
+  abort_job(EXIT_FAILURE);
+}
+
+const char* kind_name(Kind k) {
+  switch (k) {
+    case Kind::MpiHost: return "mpi-host";
+    case Kind::MpiDirect: return "mpi-direct";
+    case Kind::Rccl: return "rccl";
+    case Kind::Ipc: return "ipc";
+    default: return "auto";
+  }
+}
+
+bool mpi_gpu_aware() {
+  const char* e = std::getenv("GMT_MPI_GPU_AWARE");
+  return e && e[0] == '1';
+}
+
+Kind resolve(Kind k, const RankBinding& b, bool buffers_managed) {
+  if (const char* e = std::getenv("GMT_TRANSPORT")) {
+    if (k == Kind::Auto) k = parse_kind(e);
+  }
+  if (k != Kind::Auto) return k;
+  if (gmt_rt_backend() == GMT_BACKEND_HOST || buffers_managed || mpi_gpu_aware())
+    return Kind::MpiDirect;
+  if (gmt_ccl_available() && b.ranks_per_device == 1) return Kind::Rccl;
+  return Kind::Ipc;
+}
+
+std::unique_ptr<Transport> make_transport(Kind k, MPI_Comm comm, const RankBinding& b) {
+  switch (resolve(k, b)) {
+    case Kind::MpiHost: return std::make_unique<MpiHostTransport>(comm);
+    case Kind::MpiDirect: return std::make_unique<MpiDirectTransport>(comm);
+    case Kind::Rccl: return std::make_unique<RcclTransport>(comm, b);
+    case Kind::Ipc: return std::make_unique<IpcTransport>(comm);
+    default: break;
+  }
+  abort_job(EXIT_FAILURE);
+}
+
+}  // namespace comm
+}  // namespace gmt

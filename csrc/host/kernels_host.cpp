@@ -1,0 +1,166 @@
+// Host (CPU) implementation of the gmt/kernels.h C ABI.
+//
+// The CPU backend mirrors the reference's gtensor `host` device
+// (/root/reference/CMakeLists.txt:59-69: the *_gt binaries compiled as plain
+// C++), so that the native MPI apps and their tests run on machines with no
+// GPU.  Semantics match csrc/kernels/*.hip exactly (same formulas, same
+// summation structure where it matters for the err_norm checks); `stream`
+// arguments are ignored — every call completes before returning.  Serial on
+// purpose: several MPI ranks share the CPU in the tests, and a rank-local
+// thread pool would only oversubscribe it.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "gmt/kernels.h"
+
+namespace {
+int g_variant = 0;
+}
+
+extern "C" {
+
+int gmt_daxpy(int64_t n, double a, const double* x, double* y, void*) {
+  for (int64_t i = 0; i < n; ++i) y[i] = a * x[i] + y[i];
+  return 0;
+}
+
+int gmt_stencil5_1d(int64_t n_out, const double* c, double scale, const double* in, double* out,
+                    void*) {
+  const double c0 = c[0] * scale, c1 = c[1] * scale, c2 = c[2] * scale, c3 = c[3] * scale,
+               c4 = c[4] * scale;
+  for (int64_t i = 0; i < n_out; ++i)
+    out[i] = c0 * in[i] + c1 * in[i + 1] + c2 * in[i + 2] + c3 * in[i + 3] + c4 * in[i + 4];
+  return 0;
+}
+
+int gmt_stencil5_2d(int dim, int64_t nx_out, int64_t ny_out, const double* c, double scale,
+                    const double* in, int64_t ld_in, double* out, int64_t ld_out, void*) {
+  if (dim != 0 && dim != 1) return 1;
+  const double c0 = c[0] * scale, c1 = c[1] * scale, c2 = c[2] * scale, c3 = c[3] * scale,
+               c4 = c[4] * scale;
+  const int64_t sx = dim == 0 ? 1 : ld_in;
+  for (int64_t y = 0; y < ny_out; ++y) {
+    const double* p = in + y * ld_in;
+    double* q = out + y * ld_out;
+    for (int64_t x = 0; x < nx_out; ++x) {
+      const double* s = p + x;
+      q[x] = c0 * s[0] + c1 * s[sx] + c2 * s[2 * sx] + c3 * s[3 * sx] + c4 * s[4 * sx];
+    }
+  }
+  return 0;
+}
+
+int gmt_copy2d_batched(int n_desc, const gmt_copy2d_desc* d, int elem_bytes, void*) {
+  if (n_desc < 0 || n_desc > GMT_MAX_COPY2D || (elem_bytes != 4 && elem_bytes != 8)) return 1;
+  for (int k = 0; k < n_desc; ++k) {
+    const char* s = static_cast<const char*>(d[k].src);
+    char* t = static_cast<char*>(d[k].dst);
+    const size_t row = static_cast<size_t>(d[k].width) * elem_bytes;
+    for (int64_t r = 0; r < d[k].height; ++r)
+      std::memmove(t + r * d[k].dst_ld * elem_bytes, s + r * d[k].src_ld * elem_bytes, row);
+  }
+  return 0;
+}
+
+int64_t gmt_sum_axis_workspace(int, int64_t, int64_t) { return 1; }
+
+int gmt_sum_axis(int keep_dim, int64_t nx, int64_t ny, const double* z, int64_t ld, double* out,
+                 double*, void*) {
+  if (keep_dim == 0) {
+    for (int64_t x = 0; x < nx; ++x) out[x] = 0.0;
+    for (int64_t y = 0; y < ny; ++y)
+      for (int64_t x = 0; x < nx; ++x) out[x] += z[y * ld + x];
+  } else if (keep_dim == 1) {
+    for (int64_t y = 0; y < ny; ++y) {
+      double s = 0.0;
+      for (int64_t x = 0; x < nx; ++x) s += z[y * ld + x];
+      out[y] = s;
+    }
+  } else {
+    return 1;
+  }
+  return 0;
+}
+
+int64_t gmt_diff_sq_workspace(int64_t, int64_t) { return 1; }
+
+int gmt_diff_sq(int64_t nx, int64_t ny, const double* a, int64_t lda, const double* b,
+                int64_t ldb, double* out, double*, void*) {
+  double s = 0.0;
+  for (int64_t y = 0; y < ny; ++y)
+    for (int64_t x = 0; x < nx; ++x) {
+      const double d = a[y * lda + x] - b[y * ldb + x];
+      s += d * d;
+    }
+  out[0] = s;
+  return 0;
+}
+
+int gmt_fill_poly(int mode, int64_t nx, int64_t ny, double x0, double dx, double y0, double dy,
+                  double* z, int64_t ld, void*) {
+  for (int64_t j = 0; j < ny; ++j)
+    for (int64_t i = 0; i < nx; ++i) {
+      const double x = x0 + i * dx, y = y0 + j * dy;
+      z[j * ld + i] = mode == 0 ? x * x * x + y * y : (mode == 1 ? 3 * x * x : 2 * y);
+    }
+  return 0;
+}
+
+int64_t gmt_jacobi_resid_workspace(int64_t, int64_t) { return 2; }
+
+static void jacobi_rect(int64_t x0, int64_t nx, int64_t y0, int64_t ny, const double* u, double* un,
+                        int64_t ld, const double* f, int64_t ldf, double c0, double c1,
+                        double* acc_out) {
+  double acc = 0.0;
+  for (int64_t y = y0; y < y0 + ny; ++y)
+    for (int64_t x = x0; x < x0 + nx; ++x) {
+      const double* p = u + y * ld + x;
+      double o = c0 * ((p[-1] + p[1]) + (p[-ld] + p[ld]));
+      if (f) o += c1 * f[y * ldf + x];
+      const double d = o - p[0];
+      acc += d * d;
+      un[y * ld + x] = o;
+    }
+  if (acc_out) *acc_out = acc;
+}
+
+int gmt_jacobi5(int64_t x0, int64_t nx, int64_t y0, int64_t ny, const double* u, double* un,
+                int64_t ld, const double* f, int64_t ldf, double c0, double c1, double* resid,
+                void*) {
+  double acc = 0.0;
+  if (nx > 0 && ny > 0) jacobi_rect(x0, nx, y0, ny, u, un, ld, f, ldf, c0, c1, &acc);
+  if (resid) resid[0] = acc;
+  return 0;
+}
+
+int gmt_jacobi5_rects(int n_rect, const int64_t* r, const double* u, double* un, int64_t ld,
+                      const double* f, int64_t ldf, double c0, double c1, void*) {
+  if (n_rect > 4) return 1;
+  for (int k = 0; k < n_rect; ++k)
+    if (r[4 * k + 1] > 0 && r[4 * k + 3] > 0)
+      jacobi_rect(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3], u, un, ld, f, ldf, c0, c1,
+                  nullptr);
+  return 0;
+}
+
+void gmt_jacobi5_set_variant(int v) { g_variant = v; }
+int gmt_jacobi5_get_variant(void) { return g_variant; }
+
+const char* gmt_error_string(int err) {
+  switch (err) {
+    case 0: return "success";
+    case 1: return "invalid value";
+    case 2: return "out of memory";
+    case 3: return "not supported by the host backend";
+    case 4: return "not ready";
+    default: return "unknown host-backend error";
+  }
+}
+int gmt_device_synchronize(void) { return 0; }
+const char* gmt_build_info(void) {
+  return "libgmt host (CPU) backend: daxpy, stencil5 1d/2d, jacobi5, copy2d_batched, sum_axis, "
+         "diff_sq, fill_poly; built " __DATE__ " " __TIME__;
+}
+
+}  // extern "C"

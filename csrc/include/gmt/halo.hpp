@@ -1,0 +1,156 @@
+// gmt/halo.hpp — ghost-cell exchange for column-major 2-D fields.
+//
+// Reference: boundary_exchange_x (dim 0, non-contiguous, packed through
+// device buffers, optional host staging; mpi_stencil2d_gt.cc:135-255),
+// boundary_exchange_y (dim 1, contiguous, in place or through device
+// buffers; :257-373), the 1-D exchange (mpi_stencil_gt.cc:83-122) and the
+// SYCL versions with persistent static buffers (mpi_stencil2d_sycl.cc:211-375,
+// mpi_stencil2d_sycl_oo.cc:362-515).
+//
+// One class covers all of them and the 2-D Cartesian case (up to four
+// neighbours): x faces ("dim 0", rows of the column-major array) are packed
+// by ONE fused gfx950 kernel launch for all faces and unpacked by one; y
+// faces ("dim 1", whole columns) go zero-copy unless `pack_y`.  Buffers are
+// allocated once.  start()/finish() are split so a caller can overlap the
+// interior update with the transfer (the reference never overlaps).
+//
+// Tag convention of the reference (mpi_stencil2d_gt.cc:186-223): a message
+// to the lower neighbour uses 456, to the upper 123; y faces add 1000.
+#pragma once
+
+#include <memory>
+#include <vector>
+
+#include "gmt/buffer.hpp"
+#include "gmt/comm.hpp"
+
+namespace gmt {
+
+struct Neighbors {
+  int west = -1, east = -1;    // x / dim 0 (contiguous axis) lower / upper
+  int south = -1, north = -1;  // y / dim 1 (strided axis) lower / upper
+};
+
+class Halo2D {
+ public:
+  static constexpr int kTagLow = 456, kTagHigh = 123, kTagY = 1000;
+
+  // field: the whole ghosted array, nrows = nx + 2*gx (contiguous), ncols = ny + 2*gy
+  Halo2D(comm::Transport& t, Span2D<double> field, int gx, int gy, Neighbors nb, bool pack_y,
+         int buf_space)
+      : t_(t), f_(field), gx_(gx), gy_(gy), nb_(nb) {
+    nx_ = f_.nrows - 2 * gx;
+    ny_ = f_.ncols - 2 * gy;
+    std::vector<comm::Msg> recvs, sends;
+    auto x_face = [&](int peer, size_t send_row, size_t recv_row, int send_tag, int recv_tag) {
+      Face fc;
+      fc.sbuf = Buffer<double>(static_cast<size_t>(gx) * ny_, buf_space);
+      fc.rbuf = Buffer<double>(static_cast<size_t>(gx) * ny_, buf_space);
+      fc.send = f_.sub(send_row, gx, gy, ny_);
+      fc.recv = f_.sub(recv_row, gx, gy, ny_);
+      sends.push_back({fc.sbuf.data(), fc.sbuf.bytes(), peer, send_tag});
+      recvs.push_back({fc.rbuf.data(), fc.rbuf.bytes(), peer, recv_tag});
+      xfaces_.push_back(std::move(fc));
+    };
+    if (gx > 0) {
+      if (nb.west >= 0) x_face(nb.west, gx, 0, kTagLow, kTagHigh);
+      if (nb.east >= 0) x_face(nb.east, nx_, gx + nx_, kTagHigh, kTagLow);
+    }
+    auto y_face = [&](int peer, size_t send_col, size_t recv_col, int send_tag, int recv_tag) {
+      // whole columns: contiguous from the first row of column c to the last
+      // row of column c+gy-1 (exact, so a view into a padded allocation never
+      // reads or writes past the field)
+      const size_t n = static_cast<size_t>(gy - 1) * f_.ld + f_.nrows;
+      double* s = &f_(0, send_col);
+      double* r = &f_(0, recv_col);
+      if (pack_y) {
+        Face fc;
+        fc.sbuf = Buffer<double>(n, buf_space);
+        fc.rbuf = Buffer<double>(n, buf_space);
+        fc.ysrc = s;
+        fc.ydst = r;
+        fc.ybytes = n * sizeof(double);
+        sends.push_back({fc.sbuf.data(), fc.sbuf.bytes(), peer, send_tag + kTagY});
+        recvs.push_back({fc.rbuf.data(), fc.rbuf.bytes(), peer, recv_tag + kTagY});
+        yfaces_.push_back(std::move(fc));
+      } else {
+        sends.push_back({s, n * sizeof(double), peer, send_tag + kTagY});
+        recvs.push_back({r, n * sizeof(double), peer, recv_tag + kTagY});
+      }
+    };
+    if (gy > 0) {
+      if (nb.south >= 0) y_face(nb.south, gy, 0, kTagLow, kTagHigh);
+      if (nb.north >= 0) y_face(nb.north, ny_, gy + ny_, kTagHigh, kTagLow);
+    }
+    for (auto& m : sends) bytes_ += m.bytes;
+    nmsg_ = sends.size();
+    if (!sends.empty() || !recvs.empty()) ex_ = t_.plan(recvs, sends);
+  }
+
+  bool active() const { return ex_ != nullptr; }
+  size_t bytes_sent() const { return bytes_; }
+  size_t messages() const { return nmsg_; }
+
+  void start(gmt_stream_t s) {
+    if (!ex_) return;
+    pack(s);
+    ex_->start(s);
+  }
+  void finish(gmt_stream_t s) {
+    if (!ex_) return;
+    ex_->wait(s);
+    unpack(s);
+  }
+  // Blocking exchange, reference semantics: ghosts valid and the stream
+  // drained on return.
+  void exchange(gmt_stream_t s) {
+    start(s);
+    finish(s);
+    GMT_CHECK("halo sync", gmt_rt_stream_synchronize(s));
+  }
+
+ private:
+  struct Face {
+    Buffer<double> sbuf, rbuf;
+    Span2D<double> send, recv;  // x faces
+    double* ysrc = nullptr;     // packed y faces
+    double* ydst = nullptr;
+    size_t ybytes = 0;
+  };
+
+  void pack(gmt_stream_t s) {
+    if (!xfaces_.empty()) {
+      gmt_copy2d_desc d[GMT_MAX_COPY2D];
+      int n = 0;
+      for (auto& fc : xfaces_)
+        d[n++] = {fc.send.data, fc.sbuf.data(), static_cast<int64_t>(fc.send.ld),
+                  static_cast<int64_t>(gx_), gx_, static_cast<int64_t>(ny_)};
+      GMT_CHECK("halo pack", gmt_copy2d_batched(n, d, sizeof(double), s));
+    }
+    for (auto& fc : yfaces_)
+      GMT_CHECK("halo pack y", gmt_rt_memcpy_async(fc.sbuf.data(), fc.ysrc, fc.ybytes, s));
+  }
+  void unpack(gmt_stream_t s) {
+    if (!xfaces_.empty()) {
+      gmt_copy2d_desc d[GMT_MAX_COPY2D];
+      int n = 0;
+      for (auto& fc : xfaces_)
+        d[n++] = {fc.rbuf.data(), fc.recv.data, static_cast<int64_t>(gx_),
+                  static_cast<int64_t>(fc.recv.ld), gx_, static_cast<int64_t>(ny_)};
+      GMT_CHECK("halo unpack", gmt_copy2d_batched(n, d, sizeof(double), s));
+    }
+    for (auto& fc : yfaces_)
+      GMT_CHECK("halo unpack y", gmt_rt_memcpy_async(fc.ydst, fc.rbuf.data(), fc.ybytes, s));
+  }
+
+  comm::Transport& t_;
+  Span2D<double> f_;
+  int gx_, gy_;
+  size_t nx_ = 0, ny_ = 0;
+  Neighbors nb_;
+  std::vector<Face> xfaces_, yfaces_;
+  std::unique_ptr<comm::Exchange> ex_;
+  size_t bytes_ = 0, nmsg_ = 0;
+};
+
+}  // namespace gmt
