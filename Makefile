@@ -25,13 +25,16 @@ LIB       := $(LIBDIR)/libgmt.so
 LIB_CCL   := $(LIBDIR)/libgmt_ccl.so
 LIBH      := $(LIBH_DIR)/libgmt.so
 LIBH_CCL  := $(LIBH_DIR)/libgmt_ccl.so
+LIB_ENG   := $(LIBDIR)/libgmt_engine.so
+LIBH_ENG  := $(LIBH_DIR)/libgmt_engine.so
 
 HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
              -Icsrc/include -munsafe-fp-atomics
 ROCM_HOST := -O2 -std=c++17 -fPIC -Wall -Icsrc/include -I$(ROCM)/include -D__HIP_PLATFORM_AMD__=1
 HOSTFLAGS := -O3 -std=c++17 -fPIC -Wall -Icsrc/include
 APPFLAGS  := -O2 -std=c++17 -Wall -Icsrc/include -Icsrc/apps -I$(MPI_HOME)/include
-MPI_LIBS  := $(MPI_HOME)/lib/libmpi.so -Wl,-rpath,$(MPI_HOME)/lib -static-libstdc++ -static-libgcc
+ENGFLAGS  := -O2 -std=c++17 -Wall -fPIC -Icsrc/include
+MPI_LIBS  := $(MPI_HOME)/lib/libmpi.so -Wl,-rpath,$(MPI_HOME)/lib -static-libstdc++ -static-libgcc -Wl,--allow-shlib-undefined
 
 KERNEL_SRCS := $(wildcard csrc/kernels/*.hip)
 KERNEL_OBJS := $(patsubst csrc/kernels/%.hip,$(OBJ)/kernels/%.o,$(KERNEL_SRCS))
@@ -40,7 +43,8 @@ RT_OBJ      := $(OBJ)/runtime/rt_hip.o
 CCL_OBJ     := $(OBJ)/runtime/ccl_rccl.o
 HOST_OBJS   := $(OBJ)/host/kernels_host.o $(OBJ)/host/rt_host.o
 HOSTCCL_OBJ := $(OBJ)/host/ccl_stub.o
-COMM_OBJS   := $(OBJ)/comm/transport.o
+COMM_OBJS   := $(OBJ)/comm/transport_mpi.o $(OBJ)/comm/transport_core.o $(OBJ)/engine/jacobi.o
+ENG_OBJS    := $(OBJ)/comm/transport_core.o $(OBJ)/engine/jacobi.o $(OBJ)/engine/engine_capi.o
 APP_HDRS    := $(wildcard csrc/include/gmt/*.hpp csrc/include/gmt/*.h csrc/apps/*.hpp)
 
 # reference binary names (Makefile:2, CMakeLists.txt:22-82) + MI355X additions
@@ -51,8 +55,8 @@ APPS := daxpy daxpy_nvtx mpi_daxpy mpi_daxpy_nvtx_managed mpi_daxpy_nvtx_unmanag
 .PHONY: all lib host apps clean
 all: lib host apps
 
-lib: $(LIB) $(LIB_CCL)
-host: $(LIBH) $(LIBH_CCL)
+lib: $(LIB) $(LIB_CCL) $(LIB_ENG)
+host: $(LIBH) $(LIBH_CCL) $(LIBH_ENG)
 
 $(OBJ)/kernels/%.o: csrc/kernels/%.hip $(KERNEL_HDRS)
 	@mkdir -p $(dir $@)
@@ -85,7 +89,20 @@ $(LIBH_CCL): $(HOSTCCL_OBJ)
 
 $(OBJ)/comm/%.o: csrc/comm/%.cpp $(APP_HDRS)
 	@mkdir -p $(dir $@)
-	$(CXX) $(APPFLAGS) -c $< -o $@
+	$(CXX) $(APPFLAGS) -fPIC -c $< -o $@
+
+$(OBJ)/engine/%.o: csrc/engine/%.cpp $(APP_HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(ENGFLAGS) -c $< -o $@
+
+# MPI-free engine library for Python (torch.distributed bootstraps RCCL)
+$(LIB_ENG): $(ENG_OBJS) $(LIB) $(LIB_CCL)
+	$(CXX) -shared -fPIC -o $@ $(ENG_OBJS) -Wl,-soname,libgmt_engine.so -L$(LIBDIR) -lgmt -lgmt_ccl \
+	  -Wl,-rpath,'$$ORIGIN' -static-libstdc++ -static-libgcc
+
+$(LIBH_ENG): $(ENG_OBJS) $(LIBH) $(LIBH_CCL)
+	$(CXX) -shared -fPIC -o $@ $(ENG_OBJS) -Wl,-soname,libgmt_engine.so -L$(LIBH_DIR) -lgmt -lgmt_ccl \
+	  -Wl,-rpath,'$$ORIGIN' -static-libstdc++ -static-libgcc
 
 $(OBJ)/apps/%.o: csrc/apps/%.cpp $(APP_HDRS)
 	@mkdir -p $(dir $@)

@@ -21,6 +21,7 @@
 
 #include "gmt/buffer.hpp"
 #include "gmt/device.hpp"
+#include "gmt/comm.hpp"
 #include "gmt/halo.hpp"
 #include "gmt/util.hpp"
 

@@ -1,4 +1,5 @@
-// Transport implementations: mpi-host, mpi-direct, rccl, ipc (gmt/comm.hpp).
+// MPI-based transports: mpi-host, mpi-direct, ipc, and the factory that
+// bootstraps rccl over MPI (gmt/comm.hpp, gmt/transport.hpp).
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
@@ -8,6 +9,7 @@
 
 #include "gmt/buffer.hpp"
 #include "gmt/comm.hpp"
+#include "gmt/mpi.hpp"
 
 namespace gmt {
 namespace comm {
@@ -74,6 +76,22 @@ void staged_allgather(MPI_Comm c, int rank, int size, const void* send, void* re
   GMT_CHECK("allgather sync", gmt_rt_stream_synchronize(s));
 }
 
+class MpiTransport : public Transport {
+ protected:
+  explicit MpiTransport(MPI_Comm c) : Transport(rank_of(c), size_of(c)), comm_(c) {}
+  static int rank_of(MPI_Comm c) {
+    int r = 0;
+    MPI_Comm_rank(c, &r);
+    return r;
+  }
+  static int size_of(MPI_Comm c) {
+    int n = 1;
+    MPI_Comm_size(c, &n);
+    return n;
+  }
+  MPI_Comm comm_;
+};
+
 // ------------------------------------------------------------------ mpi-host
 class MpiHostExchange : public Exchange {
  public:
@@ -118,9 +136,9 @@ class MpiHostExchange : public Exchange {
   bool armed_ = false;
 };
 
-class MpiHostTransport : public Transport {
+class MpiHostTransport : public MpiTransport {
  public:
-  explicit MpiHostTransport(MPI_Comm c) : Transport(c) {}
+  explicit MpiHostTransport(MPI_Comm c) : MpiTransport(c) {}
   Kind kind() const override { return Kind::MpiHost; }
   const char* name() const override { return "mpi-host"; }
   std::unique_ptr<Exchange> plan(const std::vector<Msg>& r, const std::vector<Msg>& s) override {
@@ -160,9 +178,9 @@ class MpiDirectExchange : public Exchange {
   std::vector<MPI_Request> reqs_;
 };
 
-class MpiDirectTransport : public Transport {
+class MpiDirectTransport : public MpiTransport {
  public:
-  explicit MpiDirectTransport(MPI_Comm c) : Transport(c) {}
+  explicit MpiDirectTransport(MPI_Comm c) : MpiTransport(c) {}
   Kind kind() const override { return Kind::MpiDirect; }
   const char* name() const override { return "mpi-direct"; }
   std::unique_ptr<Exchange> plan(const std::vector<Msg>& r, const std::vector<Msg>& s) override {
@@ -180,71 +198,6 @@ class MpiDirectTransport : public Transport {
     const bool inplace = send == static_cast<const char*>(recv) + rank_ * bpr;
     GMT_MPI_CHECK(MPI_Allgather(inplace ? MPI_IN_PLACE : send, inplace ? 0 : n, t, recv, n, t, comm_));
   }
-};
-
-// ---------------------------------------------------------------------- rccl
-class RcclExchange : public Exchange {
- public:
-  RcclExchange(gmt_ccl_comm_t cc, std::vector<Msg> r, std::vector<Msg> s)
-      : cc_(cc), recvs_(std::move(r)), sends_(std::move(s)) {
-    // Within one group, messages between a pair of ranks are matched in
-    // issue order: sort both sides by (peer, tag) so the k-th send to B is
-    // B's k-th receive from us.
-    auto key = [](const Msg& a, const Msg& b) {
-      return a.peer != b.peer ? a.peer < b.peer : a.tag < b.tag;
-    };
-    std::sort(recvs_.begin(), recvs_.end(), key);
-    std::sort(sends_.begin(), sends_.end(), key);
-  }
-  void start(gmt_stream_t s) override {
-    GMT_CCL_CHECK("group start", gmt_ccl_group_start());
-    for (auto& m : recvs_) GMT_CCL_CHECK("recv", gmt_ccl_recv(m.buf, m.bytes, m.peer, cc_, s));
-    for (auto& m : sends_) GMT_CCL_CHECK("send", gmt_ccl_send(m.buf, m.bytes, m.peer, cc_, s));
-    GMT_CCL_CHECK("group end", gmt_ccl_group_end());
-  }
-  void wait(gmt_stream_t) override {}  // stream-ordered on s already
-
- private:
-  gmt_ccl_comm_t cc_;
-  std::vector<Msg> recvs_, sends_;
-};
-
-class RcclTransport : public Transport {
- public:
-  RcclTransport(MPI_Comm c, const RankBinding& b) : Transport(c) {
-    if (!gmt_ccl_available()) {
-      std::printf("ERROR: transport rccl requested but this build has no RCCL (%s backend)\n",
-                  gmt_rt_backend_name());
-      abort_job(EXIT_FAILURE);
-    }
-    int worst = b.ranks_per_device;
-    MPI_Allreduce(MPI_IN_PLACE, &worst, 1, MPI_INT, MPI_MAX, c);
-    if (worst > 1) {
-      std::printf("ERROR: transport rccl needs one rank per GPU (%d ranks share a GPU); "
-                  "use --transport=ipc or mpi-host\n", worst);
-      abort_job(EXIT_FAILURE);
-    }
-    gmt_ccl_id id;
-    std::memset(&id, 0, sizeof(id));
-    if (rank_ == 0) GMT_CCL_CHECK("unique id", gmt_ccl_get_unique_id(&id));
-    GMT_MPI_CHECK(MPI_Bcast(&id, sizeof(id), MPI_BYTE, 0, c));
-    GMT_CCL_CHECK("comm init", gmt_ccl_comm_init(&cc_, size_, &id, rank_));
-  }
-  ~RcclTransport() override { gmt_ccl_comm_destroy(cc_); }
-  Kind kind() const override { return Kind::Rccl; }
-  const char* name() const override { return "rccl"; }
-  std::unique_ptr<Exchange> plan(const std::vector<Msg>& r, const std::vector<Msg>& s) override {
-    return std::make_unique<RcclExchange>(cc_, r, s);
-  }
-  void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override {
-    GMT_CCL_CHECK("allreduce", gmt_ccl_allreduce_sum_f64(buf, buf, n, cc_, s));
-  }
-  void allgather(const void* send, void* recv, size_t bpr, gmt_stream_t s) override {
-    GMT_CCL_CHECK("allgather", gmt_ccl_allgather(send, recv, bpr, cc_, s));
-  }
-
- private:
-  gmt_ccl_comm_t cc_ = nullptr;
 };
 
 // ----------------------------------------------------------------------- ipc
@@ -377,9 +330,9 @@ class IpcExchange : public Exchange {
   char token_ = 0;
 };
 
-class IpcTransport : public Transport {
+class IpcTransport : public MpiTransport {
  public:
-  explicit IpcTransport(MPI_Comm c) : Transport(c) {
+  explicit IpcTransport(MPI_Comm c) : MpiTransport(c) {
     GMT_CHECK("ipc copy stream", gmt_rt_stream_create(&cs_, 1));
   }
   ~IpcTransport() override { gmt_rt_stream_destroy(cs_); }
@@ -408,18 +361,9 @@ Kind parse_kind(const std::string& s) {
   if (s == "mpi-direct" || s == "direct" || s == "mpi") return Kind::MpiDirect;
   if (s == "rccl" || s == "nccl") return Kind::Rccl;
   if (s == "ipc" || s == "hip-ipc") return Kind::Ipc;
+  if (s == "local") return Kind::Local;
   std::printf("ERROR: unknown transport '%s' (auto|mpi-host|mpi-direct|rccl|ipc)\n", s.c_str());
   abort_job(EXIT_FAILURE);
-}
-
-const char* kind_name(Kind k) {
-  switch (k) {
-    case Kind::MpiHost: return "mpi-host";
-    case Kind::MpiDirect: return "mpi-direct";
-    case Kind::Rccl: return "rccl";
-    case Kind::Ipc: return "ipc";
-    default: return "auto";
-  }
 }
 
 bool mpi_gpu_aware() {
@@ -442,8 +386,25 @@ std::unique_ptr<Transport> make_transport(Kind k, MPI_Comm comm, const RankBindi
   switch (resolve(k, b)) {
     case Kind::MpiHost: return std::make_unique<MpiHostTransport>(comm);
     case Kind::MpiDirect: return std::make_unique<MpiDirectTransport>(comm);
-    case Kind::Rccl: return std::make_unique<RcclTransport>(comm, b);
+    case Kind::Rccl: {
+      int worst = b.ranks_per_device;
+      MPI_Allreduce(MPI_IN_PLACE, &worst, 1, MPI_INT, MPI_MAX, comm);
+      if (worst > 1) {
+        std::printf("ERROR: transport rccl needs one rank per GPU (%d ranks share a GPU); "
+                    "use --transport=ipc or mpi-host\n", worst);
+        abort_job(EXIT_FAILURE);
+      }
+      int rank = 0, size = 1;
+      MPI_Comm_rank(comm, &rank);
+      MPI_Comm_size(comm, &size);
+      gmt_ccl_id id;
+      std::memset(&id, 0, sizeof(id));
+      if (rank == 0) GMT_CCL_CHECK("unique id", gmt_ccl_get_unique_id(&id));
+      GMT_MPI_CHECK(MPI_Bcast(&id, sizeof(id), MPI_BYTE, 0, comm));
+      return make_rccl_transport(rank, size, id);
+    }
     case Kind::Ipc: return std::make_unique<IpcTransport>(comm);
+    case Kind::Local: return make_local_transport();
     default: break;
   }
   abort_job(EXIT_FAILURE);

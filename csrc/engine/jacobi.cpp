@@ -1,0 +1,196 @@
+// Native distributed Jacobi engine (gmt/jacobi.hpp).
+#include "gmt/jacobi.hpp"
+
+#include <cmath>
+#include <cstdio>
+
+namespace gmt {
+
+namespace {
+constexpr double kC0 = 0.25;  // un = 1/4 (W + E + S + N): Laplace, no source term
+
+int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+}  // namespace
+
+void choose_dims(int world, int64_t ny, int64_t nx, int* py, int* px) {
+  double best = -1.0;
+  for (int x = 1; x <= world; ++x) {
+    if (world % x) continue;
+    const int y = world / x;
+    const double ly = static_cast<double>(ny) / y, lx = static_cast<double>(nx) / x;
+    const double cost = (y > 1 ? 2 * lx : 0.0) + (x > 1 ? 1.5 * 2 * ly : 0.0);
+    if (best < 0 || cost < best - 1e-9 || (std::fabs(cost - best) <= 1e-9 && y > *py)) {
+      best = cost;
+      *py = y;
+      *px = x;
+    }
+  }
+}
+
+JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), cfg_(c) {
+  const int rank = t.rank(), world = t.size();
+  if (c.py * c.px != world) {
+    std::printf("JacobiSolver: process grid %dx%d != world size %d\n", c.py, c.px, world);
+    abort_job(EXIT_FAILURE);
+  }
+  const int cy = rank / c.px, cx = rank % c.px;
+  block_split(c.ny_global, c.py, cy, &oy_, &ny_);
+  block_split(c.nx_global, c.px, cx, &ox_, &nx_);
+  if (nx_ < 1 || ny_ < 1) {
+    std::printf("JacobiSolver: empty local domain (%lldx%lld over %dx%d)\n",
+                static_cast<long long>(c.ny_global), static_cast<long long>(c.nx_global), c.py, c.px);
+    abort_job(EXIT_FAILURE);
+  }
+  auto at = [&](int y, int x) { return y * c.px + x; };
+  nb_.west = cx > 0 ? at(cy, cx - 1) : (c.periodic ? at(cy, c.px - 1) : -1);
+  nb_.east = cx < c.px - 1 ? at(cy, cx + 1) : (c.periodic ? at(cy, 0) : -1);
+  nb_.south = cy > 0 ? at(cy - 1, cx) : (c.periodic ? at(c.py - 1, cx) : -1);
+  nb_.north = cy < c.py - 1 ? at(cy + 1, cx) : (c.periodic ? at(0, cx) : -1);
+
+  ld_ = round_up(xo_ + nx_ + 1, 64);
+  const size_t elems = static_cast<size_t>(ld_) * (ny_ + 2);
+  GMT_CHECK("stream", gmt_rt_stream_create(&s_, 0));
+  GMT_CHECK("comm stream", gmt_rt_stream_create(&cs_, 1));
+  GMT_CHECK("event", gmt_rt_event_create(&ev_start_, 0));
+  GMT_CHECK("event", gmt_rt_event_create(&ev_halo_, 0));
+  if (c.variant) gmt_jacobi5_set_variant(c.variant);
+
+  // deterministic, decomposition-independent initial field and Dirichlet
+  // ring: u(x, y) = x^3 + y^2 at global ghost-inclusive coordinates * h
+  const double h = 1.0 / (static_cast<double>(c.ny_global > c.nx_global ? c.ny_global : c.nx_global) + 1);
+  for (int b = 0; b < 2; ++b) {
+    buf_[b] = Buffer<double>(elems, GMT_SPACE_DEVICE);
+    GMT_CHECK("memset", gmt_rt_memset_async(buf_[b].data(), 0, buf_[b].bytes(), s_));
+    GMT_CHECK("fill", gmt_fill_poly(0, nx_ + 2, ny_ + 2, (ox_ - 1) * h, h, (oy_ - 1) * h, h,
+                                    buf_[b].data() + (xo_ - 1), ld_, s_));
+  }
+  GMT_CHECK("init sync", gmt_rt_stream_synchronize(s_));
+  resid_ws_ = Buffer<double>(gmt_jacobi_resid_workspace(nx_, ny_) + 1, GMT_SPACE_DEVICE);
+  for (int b = 0; b < 2; ++b) {
+    Span2D<double> f(buf_[b].data() + (xo_ - 1), nx_ + 2, ny_ + 2, ld_);
+    halo_[b] = std::make_unique<Halo2D>(t_, f, 1, 1, nb_, false, GMT_SPACE_DEVICE);
+  }
+  if (c.graph) capture_graphs();
+}
+
+JacobiSolver::~JacobiSolver() {
+  if (s_) gmt_rt_stream_synchronize(s_);
+  if (cs_) gmt_rt_stream_synchronize(cs_);
+  for (auto& g : graph_) gmt_rt_graph_destroy(g);
+  gmt_rt_event_destroy(ev_start_);
+  gmt_rt_event_destroy(ev_halo_);
+  halo_[0].reset();
+  halo_[1].reset();
+  gmt_rt_stream_destroy(cs_);
+  gmt_rt_stream_destroy(s_);
+}
+
+void JacobiSolver::sweep_full(int parity, double* resid) {
+  const double* u = buf_[parity].data();
+  double* un = buf_[parity ^ 1].data();
+  GMT_CHECK("jacobi sweep", gmt_jacobi5(xo_, nx_, 1, ny_, u, un, ld_, nullptr, 0, kC0, 0.0, resid, s_));
+}
+
+void JacobiSolver::enqueue_step(int parity) {
+  Halo2D& h = *halo_[parity];
+  if (!h.active()) {
+    sweep_full(parity, nullptr);
+    return;
+  }
+  if (!cfg_.overlap || nx_ < 6 || ny_ < 3) {
+    h.start(s_);
+    h.finish(s_);
+    sweep_full(parity, nullptr);
+    return;
+  }
+  const double* u = buf_[parity].data();
+  double* un = buf_[parity ^ 1].data();
+  // core: every cell whose 5-point stencil stays inside the interior; it
+  // starts at an even column so the sweep keeps its 16-B vector path
+  GMT_CHECK("event", gmt_rt_event_record(ev_start_, s_));
+  GMT_CHECK("core sweep", gmt_jacobi5(xo_ + 2, nx_ - 4, 2, ny_ - 2, u, un, ld_, nullptr, 0, kC0,
+                                      0.0, nullptr, s_));
+  // halo on the high-priority stream, concurrent with the core sweep
+  GMT_CHECK("wait", gmt_rt_stream_wait_event(cs_, ev_start_));
+  h.start(cs_);
+  h.finish(cs_);
+  GMT_CHECK("event", gmt_rt_event_record(ev_halo_, cs_));
+  GMT_CHECK("wait", gmt_rt_stream_wait_event(s_, ev_halo_));
+  // boundary frame: first/last row, first/last two columns
+  const int64_t rects[16] = {xo_,           nx_, 1, 1,       xo_, nx_, ny_, 1,
+                             xo_,           2,   2, ny_ - 2, xo_ + nx_ - 2, 2, 2, ny_ - 2};
+  GMT_CHECK("frame sweep", gmt_jacobi5_rects(4, rects, u, un, ld_, nullptr, 0, kC0, 0.0, s_));
+}
+
+void JacobiSolver::capture_graphs() {
+  for (int b = 0; b < 2; ++b)
+    if (halo_[b]->active() && !halo_[b]->capturable()) {
+      std::printf("# jacobi: transport %s is not stream-ordered; running without hipGraphs\n",
+                  t_.name());
+      return;
+    }
+  // the first send/recv to each peer sets up connections: do that eagerly
+  for (int b = 0; b < 2; ++b) {
+    halo_[b]->start(cs_);
+    halo_[b]->finish(cs_);
+  }
+  GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));
+  for (int p = 0; p < 2; ++p) {
+    int e = gmt_rt_stream_begin_capture(s_);
+    if (e == 0) {
+      enqueue_step(p);
+      e = gmt_rt_stream_end_capture(s_, &graph_[p]);
+    }
+    if (e != 0) {
+      std::printf("# jacobi: hipGraph capture unavailable (%s); running eagerly\n",
+                  gmt_rt_error_string(e));
+      for (auto& g : graph_) {
+        gmt_rt_graph_destroy(g);
+        g = nullptr;
+      }
+      return;
+    }
+  }
+}
+
+void JacobiSolver::step() {
+  if (graph_[parity_])
+    GMT_CHECK("graph launch", gmt_rt_graph_launch(graph_[parity_], s_));
+  else
+    enqueue_step(parity_);
+  parity_ ^= 1;
+}
+
+void JacobiSolver::synchronize() {
+  GMT_CHECK("sync", gmt_rt_stream_synchronize(s_));
+  GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));
+}
+
+double JacobiSolver::residual() {
+  Halo2D& h = *halo_[parity_];
+  h.start(s_);
+  h.finish(s_);
+  sweep_full(parity_, resid_ws_.data());
+  t_.allreduce_sum(resid_ws_.data(), 1, s_);
+  double r = 0.0;
+  GMT_CHECK("resid D2H", gmt_rt_memcpy_async(&r, resid_ws_.data(), sizeof(double), s_));
+  GMT_CHECK("resid sync", gmt_rt_stream_synchronize(s_));
+  parity_ ^= 1;
+  return std::sqrt(r);
+}
+
+void JacobiSolver::exchange_only() {
+  Halo2D& h = *halo_[parity_];
+  h.start(cs_);
+  h.finish(cs_);
+  GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));
+}
+
+void JacobiSolver::copy_interior(double* host) const {
+  const double* src = buf_[parity_].data() + xo_ + ld_;
+  GMT_CHECK("interior D2H", gmt_rt_memcpy2d_async(host, nx_ * sizeof(double), src,
+                                                  ld_ * sizeof(double), nx_ * sizeof(double), ny_, s_));
+  GMT_CHECK("interior sync", gmt_rt_stream_synchronize(s_));
+}
+
+}  // namespace gmt

@@ -12,8 +12,6 @@
 // nothing, cuda_error.h:7-8 vs :16).
 #pragma once
 
-#include <mpi.h>
-
 #include <cstdio>
 #include <cstdlib>
 
@@ -23,13 +21,18 @@
 
 namespace gmt {
 
+// Job-wide abort.  MPI programs install an MPI_Abort hook (gmt/mpi.hpp) so a
+// failed check takes every rank down; the MPI-free engine library used from
+// Python exits the process (the launcher tears the job down).
+using AbortHook = void (*)(int);
+inline AbortHook& abort_hook() {
+  static AbortHook h = nullptr;
+  return h;
+}
 [[noreturn]] inline void abort_job(int code) {
-  int init = 0, fin = 0;
-  MPI_Initialized(&init);
-  MPI_Finalized(&fin);
   std::fflush(stdout);
   std::fflush(stderr);
-  if (init && !fin) MPI_Abort(MPI_COMM_WORLD, code);
+  if (abort_hook()) abort_hook()(code);
   std::exit(code);
 }
 
@@ -52,16 +55,6 @@ inline int check_ccl(const char* msg, int val, const char* file, int line) {
     abort_job(EXIT_FAILURE);
   }
   return val;
-}
-
-inline void check_mpi(const char* file, int line, int rval) {
-  if (rval != MPI_SUCCESS) {
-    char s[MPI_MAX_ERROR_STRING];
-    int len = 0;
-    MPI_Error_string(rval, s, &len);
-    std::printf("%s:%d error %d (%s)\n", file, line, rval, s);
-    abort_job(2);
-  }
 }
 
 inline const char* space_name(int space) {
@@ -120,6 +113,5 @@ inline void print_mem_info(const char* label, const void* ptr, size_t size) {
 #define GMT_WARN(msg, val) ((void)(val))
 #define GMT_CCL_CHECK(msg, val) ((void)(val))
 #endif
-#define GMT_MPI_CHECK(x) ::gmt::check_mpi(__FILE__, __LINE__, (x))
 #define GMT_PTRINFO(label, ptr) ::gmt::print_ptr_info((label), (ptr))
 #define GMT_MEMINFO(label, ptr, size) ::gmt::print_mem_info((label), (ptr), (size))

@@ -16,7 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 
-#include "gmt/check.hpp"
+#include "gmt/mpi.hpp"
 
 namespace gmt {
 
@@ -52,6 +52,7 @@ inline int get_node_count(MPI_Comm comm) {
 // Select and set this rank's device.  print: emit the reference's
 // "RANK[r/N] => DEVICE[d/D] mem=%zd" line (mpi_daxpy.cc:58-59).
 inline RankBinding set_rank_device(MPI_Comm comm, bool print) {
+  install_mpi_abort();
   RankBinding b;
   MPI_Comm_rank(comm, &b.rank);
   MPI_Comm_size(comm, &b.world_size);

@@ -1,0 +1,39 @@
+/*
+ * gmt/engine.h — C ABI of the native Jacobi engine (libgmt_engine.so).
+ *
+ * The Python package drives the flagship benchmark through this ABI
+ * (gpu_mpi_tests_amd/engine.py): torch.distributed does the rendezvous and
+ * broadcasts the RCCL unique id, then every step runs in C++ (hipGraph
+ * replay of halo exchange + sweeps) with no Python on the critical path.
+ * No MPI in this library.
+ */
+#ifndef GMT_ENGINE_H
+#define GMT_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum gmt_engine_transport { GMT_ENGINE_LOCAL = 0, GMT_ENGINE_RCCL = 1 };
+
+/* fills 128 bytes (an RCCL unique id); returns 0 or an error code */
+int gmt_engine_unique_id(void* out128);
+/* flags: bit0 periodic, bit1 overlap, bit2 graph.  ccl_id: 128 bytes (RCCL) or NULL (local) */
+void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank, int world,
+                               int transport, const void* ccl_id, int flags, int variant);
+void gmt_engine_jacobi_destroy(void* h);
+int gmt_engine_jacobi_run(void* h, int steps); /* enqueue `steps` steps */
+int gmt_engine_jacobi_sync(void* h);
+double gmt_engine_jacobi_residual(void* h);
+int gmt_engine_jacobi_exchange(void* h); /* one blocking halo exchange */
+/* out[10]: nx, ny, off_x, off_y, bytes_per_exchange, messages, graph, overlap, py, px */
+int gmt_engine_jacobi_info(void* h, int64_t* out);
+int gmt_engine_jacobi_copy_interior(void* h, double* host);
+const char* gmt_engine_backend(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GMT_ENGINE_H */

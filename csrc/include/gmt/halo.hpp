@@ -22,7 +22,7 @@
 #include <vector>
 
 #include "gmt/buffer.hpp"
-#include "gmt/comm.hpp"
+#include "gmt/transport.hpp"
 
 namespace gmt {
 
@@ -88,6 +88,8 @@ class Halo2D {
   }
 
   bool active() const { return ex_ != nullptr; }
+  // the whole exchange is stream-ordered (capturable into a hipGraph)
+  bool capturable() const { return !ex_ || ex_->graph_capturable(); }
   size_t bytes_sent() const { return bytes_; }
   size_t messages() const { return nmsg_; }
 

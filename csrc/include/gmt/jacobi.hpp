@@ -1,0 +1,101 @@
+// gmt/jacobi.hpp — distributed 2-D 5-point Jacobi solver (native engine).
+//
+// The BASELINE workload "mpi_stencil2d 32768² on 8 GPUs (2×4 decomp), halo
+// exchange/interior overlap" and its single-GPU 8192² point.  The reference
+// itself only times halo exchanges around a derivative stencil, serialised
+// against compute (mpi_stencil2d_gt.cc:511-535); this engine is the
+// MI355X-first version of that loop:
+//
+//   * 2-D Cartesian decomposition (py x px ranks), ghost width 1, fp64;
+//   * one step = halo exchange of u + one Jacobi sweep u -> un + swap;
+//   * overlap: the interior "core" sweep runs on the compute stream while
+//     the halo (fused pack kernel + RCCL/IPC/MPI transfer + unpack) runs on a
+//     high-priority comm stream; the 1-2 cell boundary frame is swept after
+//     the halo lands (gmt_jacobi5_rects);
+//   * graph: with a stream-ordered transport (rccl, local) both step parities
+//     are captured into hipGraphs and replayed — one host call per step, so
+//     small per-GPU domains (strong scaling at 8 GPUs) are not launch-bound.
+//
+// Storage is column-major (x contiguous) with the interior origin at x = 8
+// so every interior row starts 64-B aligned and the sweep kernels take their
+// 16-B vector path; the row pitch is padded to 64 doubles.
+#pragma once
+
+#include <memory>
+
+#include "gmt/buffer.hpp"
+#include "gmt/halo.hpp"
+#include "gmt/transport.hpp"
+
+namespace gmt {
+
+struct JacobiConfig {
+  int64_t ny_global = 8192, nx_global = 8192;  // global interior extent
+  int py = 1, px = 1;                            // process grid (rank = cy*px + cx)
+  bool periodic = false;                         // else Dirichlet (fixed ghost ring)
+  bool overlap = true;
+  bool graph = false;
+  int variant = 0;                               // gmt_jacobi5_set_variant
+};
+
+class JacobiSolver {
+ public:
+  JacobiSolver(comm::Transport& t, const JacobiConfig& c);
+  ~JacobiSolver();
+  JacobiSolver(const JacobiSolver&) = delete;
+  JacobiSolver& operator=(const JacobiSolver&) = delete;
+
+  void step();  // asynchronous (compute stream)
+  void run(int k) {
+    for (int i = 0; i < k; ++i) step();
+  }
+  void synchronize();
+  // sqrt(global sum (u_{k+1} - u_k)^2) of one extra sweep (advances the solution)
+  double residual();
+  // one blocking halo exchange of the current field (latency measurements)
+  void exchange_only();
+  // local interior, row-major [ny][nx] (host memory)
+  void copy_interior(double* host) const;
+
+  int64_t nx() const { return nx_; }
+  int64_t ny() const { return ny_; }
+  int64_t off_x() const { return ox_; }
+  int64_t off_y() const { return oy_; }
+  size_t bytes_per_exchange() const { return halo_[0] ? halo_[0]->bytes_sent() : 0; }
+  size_t messages() const { return halo_[0] ? halo_[0]->messages() : 0; }
+  bool graph_active() const { return graph_[0] != nullptr; }
+  bool overlap_active() const { return cfg_.overlap && halo_[0] && halo_[0]->active(); }
+  const Neighbors& neighbors() const { return nb_; }
+  gmt_stream_t stream() const { return s_; }
+
+ private:
+  void enqueue_step(int parity);
+  void sweep_full(int parity, double* resid);
+  void capture_graphs();
+
+  comm::Transport& t_;
+  JacobiConfig cfg_;
+  int64_t nx_ = 0, ny_ = 0, ox_ = 0, oy_ = 0;  // local interior + global offset
+  int64_t xo_ = 8, ld_ = 0;                    // interior origin column, row pitch
+  Neighbors nb_;
+  Buffer<double> buf_[2];
+  std::unique_ptr<Halo2D> halo_[2];
+  Buffer<double> resid_ws_;
+  gmt_stream_t s_ = nullptr, cs_ = nullptr;
+  gmt_event_t ev_start_ = nullptr, ev_halo_ = nullptr;
+  gmt_graph_t graph_[2] = {nullptr, nullptr};
+  int parity_ = 0;  // buf_[parity_] holds the current u
+};
+
+// Balanced block split of n over p parts: offset and length of part i.
+inline void block_split(int64_t n, int p, int i, int64_t* off, int64_t* len) {
+  const int64_t base = n / p, rem = n % p;
+  *off = i * base + (i < rem ? i : rem);
+  *len = base + (i < rem ? 1 : 0);
+}
+
+// Process grid minimising the halo bytes per rank; strided x faces (which
+// need a pack kernel) are weighted 1.5x a contiguous y face.
+void choose_dims(int world, int64_t ny, int64_t nx, int* py, int* px);
+
+}  // namespace gmt

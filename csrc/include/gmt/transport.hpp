@@ -1,0 +1,96 @@
+// gmt/transport.hpp — pluggable device-data transports.
+//
+// The reference has exactly one transport: GPU-aware MPI fed device,
+// managed or pinned pointers (mpi_stencil2d_gt.cc:179-225, :615;
+// mpi_daxpy_nvtx.cc:285-288), with host staging as an in-benchmark option
+// (mpi_stencil2d_gt.cc:147-176).  On an MI355X node MPI is the control plane
+// and the data plane is one of:
+//
+//   mpi-host   pack -> D2H into pinned staging -> MPI -> H2D -> unpack
+//              (reference stage_host / buf:1; works everywhere)
+//   mpi-direct device/managed pointers straight to MPI — only when MPI can
+//              read them: a GPU-aware MPI (GMT_MPI_GPU_AWARE=1), managed or
+//              host memory, or the host backend
+//   rccl       ncclSend/ncclRecv grouped per exchange on the caller's stream,
+//              ncclAllReduce / ncclAllGather for collectives: xGMI links,
+//              stream-ordered, one rank per GPU
+//   ipc        HIP IPC: each rank opens its neighbours' receive buffers once
+//              and writes its halo straight into them (xGMI peer write, or a
+//              same-device copy when ranks share one GPU); MPI carries only
+//              zero-byte ready/done tokens.  The one device-direct path that
+//              works with several ranks per GPU.
+//   local      single process: messages to self become device copies
+//              (periodic boundaries on one GPU; the Python engine's CPU tests)
+//
+// Exchanges are PERSISTENT plans (like MPI_Send_init/MPI_Recv_init): the
+// buffers are registered once, so staging memory, RCCL peers and IPC
+// mappings are set up outside the timed loop — the reference re-allocates
+// its buffers on every call (mpi_stencil2d_gt.cc:141-156).
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "gmt/check.hpp"
+
+namespace gmt {
+namespace comm {
+
+struct Msg {
+  void* buf;     // device (or managed/host) memory
+  size_t bytes;
+  int peer;      // rank in the transport's communicator
+  int tag;       // matches a send on the peer with the same tag
+};
+
+class Exchange {
+ public:
+  virtual ~Exchange() = default;
+  // Send buffers hold valid data in stream order on `s`.  Starts the transfer.
+  virtual void start(gmt_stream_t s) = 0;
+  // On return the receive buffers are valid in stream order on `s`.
+  virtual void wait(gmt_stream_t s) = 0;
+  // Fully stream-ordered (no host blocking in start/wait): may be captured
+  // into a hipGraph.
+  virtual bool graph_capturable() const { return false; }
+  void run(gmt_stream_t s) {
+    start(s);
+    wait(s);
+  }
+};
+
+enum class Kind { Auto, MpiHost, MpiDirect, Rccl, Ipc, Local };
+
+class Transport {
+ public:
+  virtual ~Transport() = default;
+  virtual Kind kind() const = 0;
+  virtual const char* name() const = 0;
+  virtual std::unique_ptr<Exchange> plan(const std::vector<Msg>& recvs,
+                                         const std::vector<Msg>& sends) = 0;
+  // in-place sum over all ranks of a device/managed vector, stream-ordered on s
+  virtual void allreduce_sum(double* buf, size_t n, gmt_stream_t s) = 0;
+  // recv = concat over ranks of `bytes_per_rank` from each rank's send;
+  // in place when send == recv + rank*bytes_per_rank
+  virtual void allgather(const void* send, void* recv, size_t bytes_per_rank, gmt_stream_t s) = 0;
+  int rank() const { return rank_; }
+  int size() const { return size_; }
+
+ protected:
+  Transport(int rank, int size) : rank_(rank), size_(size) {}
+  int rank_ = 0, size_ = 1;
+};
+
+const char* kind_name(Kind k);
+
+// RCCL over xGMI, bootstrapped from an already-distributed unique id (the
+// MPI apps broadcast it with MPI_Bcast, the Python engine through
+// torch.distributed).  One rank per GPU.
+std::unique_ptr<Transport> make_rccl_transport(int rank, int size, const gmt_ccl_id& id);
+// Single-process transport: every message must be addressed to rank 0
+// (periodic self-exchange); a device-to-device copy per message.
+std::unique_ptr<Transport> make_local_transport();
+
+}  // namespace comm
+}  // namespace gmt
