@@ -6,12 +6,15 @@ halo-exchange latency".  The headline ``value`` is the whole-job stencil rate
 in MLUPS (million lattice-point updates per second, summed over all GPUs) on
 the BASELINE multi-GPU config "mpi_stencil2d 32768² ... (2×4 decomp), halo
 exchange/interior overlap".  The global domain is FIXED at 32768² for every N
-(strong scaling: N = 8 is exactly the named 2×4 config).  The same JSON line
-also carries the single-GPU DAXPY bandwidth (N = 2^28 fp64, BASELINE config
-"daxpy N=2^28 fp64 on one MI355X") and the measured halo-exchange latency.
+(strong scaling: N = 8 is exactly the named config).  The same JSON line also
+carries the single-GPU-per-rank DAXPY bandwidth (BASELINE config "daxpy
+N=2^28 fp64 on one MI355X") and the measured halo-exchange latency.
 
-One step = halo exchange (RCCL over xGMI, overlapped with the interior sweep
-on a second stream) + one full Jacobi sweep of the global domain.  Nothing is
+One step = halo exchange of u (RCCL over xGMI on a high-priority stream,
+overlapped with the interior sweep) + one full Jacobi sweep of the global
+domain + swap.  The step loop runs in the native engine (C++ + hipGraph
+replay, ``csrc/engine/jacobi.cpp``); ``--engine torch`` runs the same
+algorithm through torch.distributed P2P from Python instead.  Nothing is
 skipped inside the timed region.
 
 Launch (driver contract):
@@ -32,8 +35,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from gpu_mpi_tests_amd import ops  # noqa: E402
-from gpu_mpi_tests_amd.models.jacobi import Jacobi2D  # noqa: E402
 from gpu_mpi_tests_amd.parallel import dist as gdist  # noqa: E402
+from gpu_mpi_tests_amd.parallel.decomp import choose_dims  # noqa: E402
 
 
 def _sync(env):
@@ -41,38 +44,59 @@ def _sync(env):
         torch.cuda.synchronize(env.device)
 
 
-def bench_jacobi(env, n, steps, warmup, overlap, dims):
-    solver = Jacobi2D(n, n, env=env, dims=dims, overlap=overlap)
-    for _ in range(warmup):
-        solver.step()
+def _timed(env, fn_run, fn_sync, steps, warmup):
+    fn_run(warmup)
+    fn_sync()
     gdist.barrier(env)
     _sync(env)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        solver.step()
+    fn_run(steps)
+    fn_sync()
     _sync(env)
     gdist.barrier(env)
     dt = time.perf_counter() - t0
-    dt = gdist.allreduce_max(dt, env)
-    resid = solver.global_residual()  # one extra (untimed) step: sanity that values are finite
-    return solver, dt, resid
+    return gdist.allreduce_max(dt, env)
 
 
-def bench_halo(env, solver, iters):
-    """Halo-exchange latency: start()+finish() alone, mean over iters (max over ranks)."""
+def bench_native(env, n, steps, warmup, overlap, dims, graph, variant):
+    from gpu_mpi_tests_amd.engine import NativeJacobi
+
+    eng = NativeJacobi(n, n, env, dims=dims, overlap=overlap, graph=graph, variant=variant)
+    dt = _timed(env, eng.run, eng.synchronize, steps, warmup)
+    info = {"engine": "native", "graph": eng.graph, "overlap": eng.overlap,
+            "transport": eng.transport if env.world_size > 1 else "none",
+            "halo_bytes_per_rank": eng.halo_bytes, "dims": (eng.py, eng.px)}
+    return eng, dt, info
+
+
+def bench_torch(env, n, steps, warmup, overlap, dims):
+    from gpu_mpi_tests_amd.models.jacobi import Jacobi2D
+
+    solver = Jacobi2D(n, n, env=env, dims=dims, overlap=overlap)
+    dt = _timed(env, solver.run, lambda: _sync(env), steps, warmup)
     ex = solver.ex[id(solver.u)]
-    if not ex.active:
-        return None, 0
+    info = {"engine": "torch", "graph": False, "overlap": overlap,
+            "transport": env.backend if env.world_size > 1 else "none",
+            "halo_bytes_per_rank": ex.bytes_per_exchange() if ex.active else 0,
+            "dims": (solver.decomp.py, solver.decomp.px)}
+    return solver, dt, info
+
+
+def halo_latency(env, solver, iters):
+    """Blocking halo exchange of the current field: mean seconds (max over ranks)."""
+    if env.world_size == 1:
+        return None
+    exch = solver.exchange if hasattr(solver, "exchange") else solver.ex[id(solver.u)].exchange
     for _ in range(5):
-        ex.exchange()
-    gdist.barrier(env)
+        exch()
     _sync(env)
+    gdist.barrier(env)
     t0 = time.perf_counter()
     for _ in range(iters):
-        ex.exchange()
+        exch()
     _sync(env)
     dt = (time.perf_counter() - t0) / iters
-    return gdist.allreduce_max(dt, env), ex.bytes_per_exchange()
+    return gdist.allreduce_max(dt, env)
 
 
 def bench_daxpy(env, n, iters):
@@ -105,10 +129,12 @@ def bench_daxpy(env, n, iters):
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--size", type=int, default=32768, help="global domain is size x size (default 32768)")
+    ap.add_argument("--engine", choices=("native", "torch"), default="native")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--dims", type=str, default=None, help="process grid PYxPX, e.g. 4x2")
     ap.add_argument("--daxpy-n", type=int, default=1 << 28)
     ap.add_argument("--skip-extras", action="store_true", help="headline stencil only")
@@ -119,19 +145,26 @@ def main(argv=None):
     env = gdist.init(device=args.device)
     if args.gpus != env.world_size and env.rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
-    if env.is_gpu and args.variant:
-        ops.set_jacobi_variant(args.variant)
     dims = tuple(int(v) for v in args.dims.lower().split("x")) if args.dims else None
-
-    solver, dt, resid = bench_jacobi(env, args.size, args.steps, args.warmup, not args.no_overlap, dims)
-    points = solver.points
+    overlap = not args.no_overlap
+    if args.engine == "native":
+        solver, dt, info = bench_native(env, args.size, args.steps, args.warmup, overlap, dims,
+                                        not args.no_graph, args.variant)
+    else:
+        if env.is_gpu and args.variant:
+            ops.set_jacobi_variant(args.variant)
+        solver, dt, info = bench_torch(env, args.size, args.steps, args.warmup, overlap, dims)
+    points = args.size * args.size
     mlups = points * args.steps / dt / 1e6
     ms_per_step = dt / args.steps * 1e3
     extras = {}
     if not args.skip_extras:
-        hl, hbytes = bench_halo(env, solver, iters=max(20, args.steps))
+        hl = halo_latency(env, solver, iters=max(20, min(args.steps, 200)))
         extras["halo_exchange_us"] = None if hl is None else round(hl * 1e6, 2)
-        extras["halo_bytes_per_rank"] = hbytes
+        resid = solver.residual() if hasattr(solver, "residual") else solver.global_residual()
+        extras["residual_l2"] = resid
+        if hasattr(solver, "close"):
+            solver.close()
         del solver
         if env.is_gpu:
             torch.cuda.empty_cache()
@@ -140,10 +173,7 @@ def main(argv=None):
         extras["daxpy_GBps_per_gpu"] = round(gbps / env.world_size, 1)
         extras["daxpy_n"] = args.daxpy_n
         extras["daxpy_ms"] = round(ddt * 1e3, 4)
-    py, px = (1, 1)
-    if env.world_size > 1 or True:
-        from gpu_mpi_tests_amd.parallel.decomp import choose_dims
-        py, px = dims if dims else choose_dims(env.world_size, args.size, args.size)
+    py, px = info["dims"] if info.get("dims") else choose_dims(env.world_size, args.size, args.size)
     if env.rank == 0:
         rec = {
             "metric": "2D 5-pt Jacobi stencil MLUPS (fp64, halo exchange overlapped)",
@@ -157,17 +187,19 @@ def main(argv=None):
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp64",
-            "data": "synthetic (seeded uniform random interior, Dirichlet lid BC)",
+            "data": "synthetic (analytic x^3+y^2 initial field, Dirichlet boundary)",
             "config": {
                 "model": f"mpi_stencil2d jacobi5 {args.size}x{args.size} fp64",
                 "global_batch": points,
                 "seq_len": None,
-                "parallelism": f"spatial2d px{px} x py{py} ({px}x{py} decomp), "
-                               f"{'overlap' if not args.no_overlap else 'serial'}",
-                "transport": env.backend if env.world_size > 1 else "none",
+                "parallelism": f"spatial2d py{py} x px{px}, "
+                               f"{'overlap' if info['overlap'] else 'serial'}",
+                "engine": info["engine"],
+                "hipgraph": info["graph"],
+                "transport": info["transport"],
+                "halo_bytes_per_rank": info["halo_bytes_per_rank"],
                 "device": str(env.device),
             },
-            "residual_l2": resid,
             **extras,
         }
         print(json.dumps(rec), flush=True)

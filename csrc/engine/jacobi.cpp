@@ -123,6 +123,7 @@ void JacobiSolver::enqueue_step(int parity) {
 }
 
 void JacobiSolver::capture_graphs() {
+  if (gmt_rt_backend() == GMT_BACKEND_HOST) return;  // no graphs on the CPU backend
   for (int b = 0; b < 2; ++b)
     if (halo_[b]->active() && !halo_[b]->capturable()) {
       std::printf("# jacobi: transport %s is not stream-ordered; running without hipGraphs\n",

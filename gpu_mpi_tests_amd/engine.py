@@ -1,0 +1,183 @@
+"""Python front end of the native Jacobi engine (``libgmt_engine.so``).
+
+The flagship benchmark's step loop runs in C++ (``csrc/engine/jacobi.cpp``):
+halo exchange over RCCL on a high-priority stream overlapped with the
+interior sweep, both step parities captured into hipGraphs.  Python only does
+the rendezvous: ``torch.distributed`` (one process per GPU) broadcasts the
+RCCL unique id, then each ``run(k)`` is a single ctypes call that enqueues k
+graph replays — no Python on the per-step critical path, which is what keeps
+small per-GPU domains (strong scaling to 8 GPUs) from going launch-bound.
+
+Library selection: device ``cuda`` loads ``gpu_mpi_tests_amd/_lib`` (HIP,
+gfx950); device ``cpu`` loads ``build/lib-host`` (the CPU backend, same ABI)
+so the engine is testable without a GPU.  Both export SONAME ``libgmt.so``,
+so one process can only hold one backend — mixing raises instead of silently
+binding the wrong one.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+from .parallel import dist as gdist
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_ROOT = os.path.dirname(_HERE)
+HIP_ENGINE = os.path.join(_HERE, "_lib", "libgmt_engine.so")
+HOST_ENGINE = os.path.join(_ROOT, "build", "lib-host", "libgmt_engine.so")
+
+LOCAL, RCCL = 0, 1
+_libs: dict[str, ctypes.CDLL] = {}
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def load(device: str = "cuda") -> ctypes.CDLL:
+    kind = "hip" if device.startswith("cuda") else "host"
+    if kind in _libs:
+        return _libs[kind]
+    other = "host" if kind == "hip" else "hip"
+    if other in _libs:
+        raise EngineError(f"the {other} engine backend is already loaded in this process; "
+                          f"run the {kind} engine in a separate process")
+    path = HIP_ENGINE if kind == "hip" else HOST_ENGINE
+    if not os.path.exists(path):
+        raise EngineError(f"{path} is missing: build it with `make lib host` "
+                          "(or __graft_entry__.build())")
+    if kind == "hip":
+        import torch  # noqa: F401  -- torch owns the HIP runtime first (see _native.py)
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    vp, i64, c_int = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+    lib.gmt_engine_unique_id.argtypes = [vp]
+    lib.gmt_engine_unique_id.restype = c_int
+    lib.gmt_engine_jacobi_create.argtypes = [i64, i64, c_int, c_int, c_int, c_int, c_int, vp, c_int,
+                                             c_int]
+    lib.gmt_engine_jacobi_create.restype = vp
+    lib.gmt_engine_jacobi_destroy.argtypes = [vp]
+    lib.gmt_engine_jacobi_destroy.restype = None
+    for name in ("gmt_engine_jacobi_sync", "gmt_engine_jacobi_exchange"):
+        getattr(lib, name).argtypes = [vp]
+        getattr(lib, name).restype = c_int
+    lib.gmt_engine_jacobi_run.argtypes = [vp, c_int]
+    lib.gmt_engine_jacobi_run.restype = c_int
+    lib.gmt_engine_jacobi_residual.argtypes = [vp]
+    lib.gmt_engine_jacobi_residual.restype = ctypes.c_double
+    lib.gmt_engine_jacobi_info.argtypes = [vp, ctypes.POINTER(i64)]
+    lib.gmt_engine_jacobi_info.restype = c_int
+    lib.gmt_engine_jacobi_copy_interior.argtypes = [vp, vp]
+    lib.gmt_engine_jacobi_copy_interior.restype = c_int
+    lib.gmt_engine_backend.restype = ctypes.c_char_p
+    got = lib.gmt_engine_backend().decode()
+    if got != kind:
+        raise EngineError(f"{path} bound to the {got} runtime, expected {kind} "
+                          "(another libgmt.so is already loaded in this process)")
+    _libs[kind] = lib
+    return lib
+
+
+def _broadcast_unique_id(lib, env) -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    if env.rank == 0:
+        err = lib.gmt_engine_unique_id(buf)
+        if err:
+            raise EngineError(f"RCCL unique id failed: {err}")
+    obj = [bytes(buf.raw) if env.rank == 0 else None]
+    torch.distributed.broadcast_object_list(obj, src=0, group=env.host_group)
+    return obj[0]
+
+
+class NativeJacobi:
+    """Distributed 2-D Jacobi (fp64) on the native engine; one rank per GPU."""
+
+    def __init__(self, ny: int, nx: int, env: "gdist.DistEnv | None" = None,
+                 dims: tuple[int, int] | None = None, periodic: bool = False,
+                 overlap: bool = True, graph: bool = True, variant: int = 0):
+        from .parallel.decomp import choose_dims
+
+        self.env = env or gdist.get()
+        e = self.env
+        self.device = "cuda" if e.is_gpu else "cpu"
+        self.lib = load(self.device)
+        py, px = dims if dims else choose_dims(e.world_size, ny, nx)
+        if py * px != e.world_size:
+            raise ValueError(f"process grid {py}x{px} != world size {e.world_size}")
+        self.ny_g, self.nx_g, self.py, self.px = ny, nx, py, px
+        if e.world_size == 1:
+            transport, cid = LOCAL, None
+        else:
+            if not e.is_gpu:
+                raise EngineError("multi-rank native engine needs GPUs (RCCL); "
+                                  "use the mpi_jacobi2d app or the torch engine on CPU")
+            transport = RCCL
+            cid = ctypes.create_string_buffer(_broadcast_unique_id(self.lib, e), 128)
+        flags = (1 if periodic else 0) | (2 if overlap else 0) | (4 if graph else 0)
+        self.h = self.lib.gmt_engine_jacobi_create(ny, nx, py, px, e.rank, e.world_size, transport,
+                                                   cid, flags, variant)
+        if not self.h:
+            raise EngineError("gmt_engine_jacobi_create failed")
+        info = (ctypes.c_int64 * 10)()
+        self.lib.gmt_engine_jacobi_info(self.h, info)
+        (self.nx, self.ny, self.off_x, self.off_y, self.halo_bytes, self.halo_msgs,
+         graph_on, overlap_on, _, _) = list(info)
+        self.graph = bool(graph_on)
+        self.overlap = bool(overlap_on)
+        self.transport = "rccl" if transport == RCCL else "local"
+
+    # ------------------------------------------------------------------
+    def run(self, steps: int) -> None:
+        self.lib.gmt_engine_jacobi_run(self.h, int(steps))
+
+    def step(self) -> None:
+        self.run(1)
+
+    def synchronize(self) -> None:
+        self.lib.gmt_engine_jacobi_sync(self.h)
+
+    def exchange(self) -> None:
+        self.lib.gmt_engine_jacobi_exchange(self.h)
+
+    def residual(self) -> float:
+        return float(self.lib.gmt_engine_jacobi_residual(self.h))
+
+    def interior(self) -> np.ndarray:
+        out = np.empty((self.ny, self.nx), dtype=np.float64)
+        self.lib.gmt_engine_jacobi_copy_interior(self.h, out.ctypes.data)
+        return out
+
+    @property
+    def points(self) -> int:
+        return self.ny_g * self.nx_g
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.gmt_engine_jacobi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def serial_jacobi(ny: int, nx: int, steps: int, periodic: bool = False) -> np.ndarray:
+    """NumPy reference of exactly the engine's problem (init, boundary, update)."""
+    h = 1.0 / (max(ny, nx) + 1)
+    x = (np.arange(nx + 2) - 1) * h
+    y = (np.arange(ny + 2) - 1) * h
+    u = (x[None, :] ** 3) + (y[:, None] ** 2)
+    un = u.copy()
+    for _ in range(steps):
+        if periodic:
+            u[1:-1, 0] = u[1:-1, -2]
+            u[1:-1, -1] = u[1:-1, 1]
+            u[0, 1:-1] = u[-2, 1:-1]
+            u[-1, 1:-1] = u[1, 1:-1]
+        un[1:-1, 1:-1] = 0.25 * ((u[1:-1, :-2] + u[1:-1, 2:]) + (u[:-2, 1:-1] + u[2:, 1:-1]))
+        u, un = un, u
+    return u[1:-1, 1:-1].copy()
