@@ -50,10 +50,10 @@ APP_HDRS    := $(wildcard csrc/include/gmt/*.hpp csrc/include/gmt/*.h csrc/apps/
 # reference binary names (Makefile:2, CMakeLists.txt:22-82) + MI355X additions
 APPS := daxpy daxpy_nvtx mpi_daxpy mpi_daxpy_nvtx_managed mpi_daxpy_nvtx_unmanaged \
         mpienv mpigatherinplace mpi_daxpy_gt mpi_stencil_gt mpi_stencil2d_gt \
-        mpi_stencil2d_sycl mpi_stencil2d_sycl_oo mpi_jacobi2d mpi_halo_bench
+        mpi_stencil2d_sycl mpi_stencil2d_sycl_oo mpi_jacobi2d mpi_halo_bench gmt_kernel_bench
 
-.PHONY: all lib host apps clean
-all: lib host apps
+.PHONY: all lib host apps host-apps sweep clean
+all: lib host apps sweep
 
 lib: $(LIB) $(LIB_CCL) $(LIB_ENG)
 host: $(LIBH) $(LIBH_CCL) $(LIBH_ENG)
@@ -118,6 +118,9 @@ $(OBJ)/apps/mpi_daxpy_nvtx_unmanaged.o: csrc/apps/mpi_daxpy_nvtx.cpp $(APP_HDRS)
 
 apps: $(addprefix $(BIN)/,$(APPS)) $(addprefix $(BINH)/,$(APPS))
 
+# CPU-only subset (no hipcc needed): host backend + build/bin-host apps
+host-apps: host $(addprefix $(BINH)/,$(APPS))
+
 $(BIN)/%: $(OBJ)/apps/%.o $(COMM_OBJS) $(LIB) $(LIB_CCL)
 	@mkdir -p $(BIN)
 	$(CXX) -o $@ $< $(COMM_OBJS) -L$(LIBDIR) -lgmt -lgmt_ccl \
@@ -127,6 +130,12 @@ $(BINH)/%: $(OBJ)/apps/%.o $(COMM_OBJS) $(LIBH) $(LIBH_CCL)
 	@mkdir -p $(BINH)
 	$(CXX) -o $@ $< $(COMM_OBJS) -L$(LIBH_DIR) -lgmt -lgmt_ccl \
 	  -Wl,-rpath,'$$ORIGIN/../lib-host' $(MPI_LIBS)
+
+# tuning harness (standalone, not part of the libraries)
+sweep: $(BUILD)/bench/stream_sweep
+$(BUILD)/bench/stream_sweep: csrc/bench/stream_sweep.hip
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
 .SECONDARY:
 

@@ -1,0 +1,119 @@
+// gmt_kernel_bench — A/B timing of every hand-written kernel variant.
+//
+// Not in the reference (it has no kernels of its own).  Times
+// the gfx950 kernels with hipEvents, median of --iters launches, and prints
+// the effective HBM bandwidth from the kernel's compulsory bytes:
+//   daxpy      24 B/elem      (variants 1-5)
+//   jacobi5    16 B/point     (variants 1-8)
+//   stencil5   16 B/point     (dim 0 / dim 1, the reference's derivative)
+//   copy2d     16 B/elem      (halo pack of a dim-0 face: strided 16-B reads)
+// CLI: gmt_kernel_bench [--daxpy-n=N] [--jacobi-n=N] [--iters=K] [--json=FILE]
+//      [--only=daxpy,jacobi,stencil,pack]
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+
+#include "gmt/buffer.hpp"
+#include "gmt/util.hpp"
+
+using namespace gmt;
+
+static double time_ms(gmt_stream_t s, int iters, const std::function<void()>& f) {
+  gmt_event_t e0, e1;
+  GMT_CHECK("event", gmt_rt_event_create(&e0, 1));
+  GMT_CHECK("event", gmt_rt_event_create(&e1, 1));
+  for (int w = 0; w < 3; ++w) f();
+  Stats st;
+  for (int k = 0; k < iters; ++k) {
+    GMT_CHECK("rec", gmt_rt_event_record(e0, s));
+    f();
+    GMT_CHECK("rec", gmt_rt_event_record(e1, s));
+    GMT_CHECK("sync", gmt_rt_event_synchronize(e1));
+    float ms = 0;
+    GMT_CHECK("elapsed", gmt_rt_event_elapsed_ms(&ms, e0, e1));
+    st.add(ms);
+  }
+  gmt_rt_event_destroy(e0);
+  gmt_rt_event_destroy(e1);
+  return st.median();
+}
+
+int main(int argc, char** argv) {
+  Cli cli(argc, argv);
+  const int iters = static_cast<int>(cli.geti("iters", 20));
+  const std::string only = cli.get("only", "daxpy,jacobi,stencil,pack");
+  const std::string json = cli.get("json", "");
+  gmt_stream_t s = nullptr;
+  GMT_CHECK("stream", gmt_rt_stream_create(&s, 0));
+  auto report = [&](const char* kernel, int variant, const char* shape, double ms, double bytes) {
+    const double gbps = bytes / (ms * 1e-3) / 1e9;
+    std::printf("%-10s v%-2d %-22s %9.4f ms  %8.1f GB/s\n", kernel, variant, shape, ms, gbps);
+    JsonRecord j;
+    j.add("app", "gmt_kernel_bench").add("kernel", kernel).add("variant", variant).add("shape", shape)
+        .add("ms", ms).add("GBps", gbps).add("backend", gmt_rt_backend_name());
+    j.append_to(json);
+  };
+  std::printf("# gmt_kernel_bench backend=%s iters=%d (median)\n", gmt_rt_backend_name(), iters);
+
+  if (only.find("daxpy") != std::string::npos) {
+    const size_t n = static_cast<size_t>(cli.geti("daxpy-n", 1LL << 28));
+    Buffer<double> x(n, GMT_SPACE_DEVICE), y(n, GMT_SPACE_DEVICE);
+    GMT_CHECK("fill", gmt_fill_poly(1, n, 1, 0.0, 1e-9, 0.0, 0.0, x.data(), n, s));
+    GMT_CHECK("fill", gmt_fill_poly(1, n, 1, 1.0, 1e-9, 0.0, 0.0, y.data(), n, s));
+    char shape[64];
+    std::snprintf(shape, sizeof(shape), "n=%zu", n);
+    for (int v = 1; v <= 5; ++v) {
+      gmt_daxpy_set_variant(v);
+      const double ms = time_ms(s, iters, [&] { GMT_CHECK("daxpy", gmt_daxpy(n, 1e-3, x.data(), y.data(), s)); });
+      report("daxpy", v, shape, ms, 24.0 * n);
+    }
+    gmt_daxpy_set_variant(0);
+    const double ms = time_ms(s, iters, [&] { GMT_CHECK("daxpy", gmt_blas_daxpy(n, 1e-3, x.data(), y.data(), s)); });
+    report("rocblas", 0, shape, ms, 24.0 * n);
+  }
+  if (only.find("jacobi") != std::string::npos) {
+    const int64_t n = cli.geti("jacobi-n", 32768);
+    const int64_t xo = 8, ld = ((xo + n + 1 + 63) / 64) * 64;
+    Buffer<double> u(static_cast<size_t>(ld) * (n + 2), GMT_SPACE_DEVICE), un(u.size(), GMT_SPACE_DEVICE);
+    GMT_CHECK("fill", gmt_fill_poly(0, ld, n + 2, 0.0, 1e-5, 0.0, 1e-5, u.data(), ld, s));
+    GMT_CHECK("fill", gmt_fill_poly(0, ld, n + 2, 0.0, 1e-5, 0.0, 1e-5, un.data(), ld, s));
+    char shape[64];
+    std::snprintf(shape, sizeof(shape), "%lldx%lld", (long long)n, (long long)n);
+    for (int v = 1; v <= 8; ++v) {
+      if (v == 3 && n > 16384) continue;  // scalar reference kernel: too slow to matter
+      gmt_jacobi5_set_variant(v);
+      const double ms = time_ms(s, iters, [&] {
+        GMT_CHECK("jacobi", gmt_jacobi5(xo, n, 1, n, u.data(), un.data(), ld, nullptr, 0, 0.25, 0.0, nullptr, s));
+      });
+      report("jacobi5", v, shape, ms, 16.0 * n * n);
+    }
+    gmt_jacobi5_set_variant(0);
+  }
+  if (only.find("stencil") != std::string::npos) {
+    // the reference's default deriv shapes: 1028 x 524288 (dim 0), 524288 x 1028 (dim 1)
+    const int64_t a = 1024, b = 512 * 1024;
+    Buffer<double> in(static_cast<size_t>(a + 4) * b, GMT_SPACE_DEVICE), out(static_cast<size_t>(a) * b, GMT_SPACE_DEVICE);
+    GMT_CHECK("fill", gmt_fill_poly(0, a + 4, b, 0.0, 1e-3, 0.0, 1e-3, in.data(), a + 4, s));
+    const double c[5] = {1.0 / 12, -2.0 / 3, 0.0, 2.0 / 3, -1.0 / 12};
+    double ms = time_ms(s, iters, [&] {
+      GMT_CHECK("d0", gmt_stencil5_2d(0, a, b, c, 128.0, in.data(), a + 4, out.data(), a, s));
+    });
+    report("stencil5", 0, "dim0 1024x524288", ms, 16.0 * a * b);
+    ms = time_ms(s, iters, [&] {
+      GMT_CHECK("d1", gmt_stencil5_2d(1, b, a, c, 128.0, in.data(), b, out.data(), b, s));
+    });
+    report("stencil5", 1, "dim1 524288x1024", ms, 16.0 * a * b);
+  }
+  if (only.find("pack") != std::string::npos) {
+    // dim-0 halo faces of the reference's field: 2 rows x 524288 columns, pitch 1028
+    const int64_t ld = 1028, ny = 512 * 1024;
+    Buffer<double> z(static_cast<size_t>(ld) * ny, GMT_SPACE_DEVICE), b0(2 * ny, GMT_SPACE_DEVICE),
+        b1(2 * ny, GMT_SPACE_DEVICE);
+    gmt_copy2d_desc d[2] = {{z.data() + 2, b0.data(), ld, 2, 2, ny}, {z.data() + 1024, b1.data(), ld, 2, 2, ny}};
+    const double ms = time_ms(s, iters, [&] { GMT_CHECK("pack", gmt_copy2d_batched(2, d, 8, s)); });
+    report("pack", 0, "2 faces 2x524288", ms, 2.0 * 2 * 16.0 * ny);
+  }
+  gmt_rt_stream_destroy(s);
+  return 0;
+}

@@ -16,6 +16,7 @@
 
 namespace {
 int g_variant = 0;
+int g_daxpy_variant = 0;
 }
 
 extern "C" {
@@ -24,6 +25,9 @@ int gmt_daxpy(int64_t n, double a, const double* x, double* y, void*) {
   for (int64_t i = 0; i < n; ++i) y[i] = a * x[i] + y[i];
   return 0;
 }
+
+void gmt_daxpy_set_variant(int v) { g_daxpy_variant = v; }
+int gmt_daxpy_get_variant(void) { return g_daxpy_variant; }
 
 int gmt_stencil5_1d(int64_t n_out, const double* c, double scale, const double* in, double* out,
                     void*) {

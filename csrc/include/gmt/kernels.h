@@ -24,6 +24,9 @@ extern "C" {
 
 /* ---- K1/K2: y <- a*x + y (fp64).  reference: daxpy.cu:73, mpi_daxpy_gt.cc:81 */
 int gmt_daxpy(int64_t n, double a, const double* x, double* y, void* stream);
+/* DAXPY kernel variant for A/B measurement (0 = default; see daxpy.hip) */
+void gmt_daxpy_set_variant(int variant);
+int gmt_daxpy_get_variant(void);
 
 /* ---- K3: 1-D 5-tap stencil, out[i] = scale * sum_k c[k]*in[i+k], k=0..4.
  *      `in` has n_out+4 elements.  reference: mpi_stencil_gt.cc:54-59 */
@@ -95,7 +98,9 @@ int gmt_jacobi5_rects(int n_rect, const int64_t* rects, const double* u, double*
                       int64_t ld, const double* f, int64_t ldf, double c0, double c1,
                       void* stream);
 /* Kernel variant selection for A/B measurement: 0 = auto, 1 = register
- * sliding window (vector x2), 2 = LDS-tiled, 3 = scalar reference kernel. */
+ * sliding window (vector x2, W/E from L1), 2 = LDS-tiled, 3 = scalar
+ * reference kernel, 4-8 = register window with lane-exchanged W/E
+ * neighbours (DPP / shfl, 32-128 rows per tile, see jacobi5.hip). */
 void gmt_jacobi5_set_variant(int variant);
 int gmt_jacobi5_get_variant(void);
 

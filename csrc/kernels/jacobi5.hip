@@ -89,6 +89,78 @@ __global__ __launch_bounds__(kBlock) void jacobi5_reg(int64_t x0, int64_t nx, in
   }
 }
 
+
+// Variants 4-8 — register sliding window where the W/E neighbours come from
+// the adjacent LANES instead of a second and third (L1-served) global load:
+// lane t holds columns 2t, 2t+1, so west of 2t is lane t-1's .y and east of
+// 2t+1 is lane t+1's .x.  XCHG = 1 uses DPP wave_shr/wave_shl (a VALU
+// modifier, no LDS traffic), XCHG = 2 uses __shfl (ds_bpermute), XCHG = 0
+// keeps the L1 loads.  Only the two wave-edge lanes load a neighbour from
+// memory.  R rows per tile; NTS = nontemporal stores of un (streamed out,
+// not re-read before the next step).  Requires an even region width.
+__device__ __forceinline__ double dpp_from_lower(double v) {  // lane i <- lane i-1
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_from_upper(double v) {  // lane i <- lane i+1
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+template <int R, int XCHG, bool NTS>
+__global__ __launch_bounds__(kBlock) void jacobi5_lane(int64_t x0, int64_t nx, int64_t y0,
+                                                       int64_t ny, const double* __restrict__ u,
+                                                       double* __restrict__ un, int64_t ld,
+                                                       int64_t nbx, int64_t nblocks) {
+  const int64_t t = xcd_swizzle(blockIdx.x, nblocks);
+  const int64_t bx = t % nbx, by = t / nbx;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t xr = (bx * kBlock + threadIdx.x) * 2;  // relative column (nx is even)
+  const bool active = xr < nx;
+  const bool edge_lo = lane == 0;
+  const bool edge_hi = lane == kWave - 1 || xr + 2 >= nx;
+  const int64_t yr0 = by * R;
+  const int64_t rows = (ny - yr0) < R ? (ny - yr0) : R;
+  const int64_t x = x0 + (active ? xr : 0);
+  const double* p = u + (y0 + yr0 - 1) * ld + x;  // row above the first output row
+  double* q = un + (y0 + yr0) * ld + x;
+  d2 n = active ? ld2(p) : d2{0.0, 0.0};
+  d2 c = active ? ld2(p + ld) : d2{0.0, 0.0};
+  auto body = [&](int64_t r) {
+    const double* pc = p + (r + 1) * ld;
+    const d2 s = active ? ld2(pc + ld) : d2{0.0, 0.0};
+    double w, e;
+    if (XCHG == 0) {
+      w = active ? pc[-1] : 0.0;
+      e = active ? pc[2] : 0.0;
+    } else {
+      w = XCHG == 1 ? dpp_from_lower(c.y) : __shfl_up(c.y, 1, kWave);
+      e = XCHG == 1 ? dpp_from_upper(c.x) : __shfl_down(c.x, 1, kWave);
+      if (active && edge_lo) w = pc[-1];
+      if (active && edge_hi) e = pc[2];
+    }
+    if (active) {
+      d2 o;
+      o.x = 0.25 * ((w + c.y) + (n.x + s.x));
+      o.y = 0.25 * ((c.x + e) + (n.y + s.y));
+      if (NTS)
+        st2_nt(q + r * ld, o);
+      else
+        st2(q + r * ld, o);
+    }
+    n = c;
+    c = s;
+  };
+  if (rows == R) {
+#pragma unroll 4
+    for (int r = 0; r < R; ++r) body(r);
+  } else {
+    for (int64_t r = 0; r < rows; ++r) body(r);
+  }
+}
+
 // LDS-tiled variant: stage (LR+2) rows x (JTX+2) columns of u, then compute.
 constexpr int LR = 16;
 template <bool HAS_F, bool RESID>
@@ -260,6 +332,21 @@ extern "C" int gmt_jacobi5(int64_t x0, int64_t nx, int64_t y0, int64_t ny, const
   if (!vec_ok) v = 3;
   double* partial = want_r ? resid + 1 : nullptr;
   int64_t nb;
+  if (v >= 4 && v <= 8 && !has_f && !want_r && nx % 2 == 0 && c0 == 0.25) {
+    const int rr = (v == 6 || v == 7) ? 64 : (v == 8 ? 128 : 32);
+    const int64_t nbx = (nx + JTX - 1) / JTX;
+    nb = nbx * ((ny + rr - 1) / rr);
+    const unsigned g = grid_1d(nb);
+    switch (v) {
+      case 4: jacobi5_lane<32, 1, false><<<g, kBlock, 0, s>>>(x0, nx, y0, ny, u, un, ld, nbx, nb); break;
+      case 5: jacobi5_lane<32, 2, false><<<g, kBlock, 0, s>>>(x0, nx, y0, ny, u, un, ld, nbx, nb); break;
+      case 6: jacobi5_lane<64, 1, true><<<g, kBlock, 0, s>>>(x0, nx, y0, ny, u, un, ld, nbx, nb); break;
+      case 7: jacobi5_lane<64, 0, true><<<g, kBlock, 0, s>>>(x0, nx, y0, ny, u, un, ld, nbx, nb); break;
+      default: jacobi5_lane<128, 1, true><<<g, kBlock, 0, s>>>(x0, nx, y0, ny, u, un, ld, nbx, nb); break;
+    }
+    GMT_RET_LAUNCH();
+  }
+  if (v >= 4) v = 1;
   if (v == 3) {
     const int64_t rect[4] = {x0, nx, y0, ny};
     Rects rs = make_rects(1, rect);

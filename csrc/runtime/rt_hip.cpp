@@ -39,6 +39,12 @@ int gmt_rt_device_info(int dev, gmt_device_info* out) {
   hipError_t e = hipGetDeviceProperties(&p, dev);
   if (e != hipSuccess) return static_cast<int>(e);
   std::snprintf(out->name, sizeof(out->name), "%s", p.name);
+  if (out->name[0] == '\0') {  // some ROCm builds leave the marketing name empty
+    char nm[256] = {0};
+    if (hipDeviceGetName(nm, sizeof(nm), dev) != hipSuccess || nm[0] == '\0')
+      std::snprintf(nm, sizeof(nm), "AMD GPU %.40s", p.gcnArchName);
+    std::snprintf(out->name, sizeof(out->name), "%s", nm);
+  }
   std::snprintf(out->arch, sizeof(out->arch), "%.63s", p.gcnArchName);
   out->total_mem = p.totalGlobalMem;
   out->vendor_id = 0x1002u;  // AMD PCI vendor id

@@ -62,6 +62,8 @@ _SIGS = {
         [c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_dbl, c_dbl, c_vp],
     ),
     "gmt_jacobi5_set_variant": (None, [c_int]),
+    "gmt_daxpy_set_variant": (None, [c_int]),
+    "gmt_daxpy_get_variant": (c_int, []),
     "gmt_jacobi5_get_variant": (c_int, []),
     "gmt_error_string": (ctypes.c_char_p, [c_int]),
     "gmt_device_synchronize": (c_int, []),

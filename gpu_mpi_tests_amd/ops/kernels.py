@@ -256,5 +256,6 @@ def jacobi5_rects(u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, 
 
 
 def set_jacobi_variant(v: int) -> None:
-    """0 auto, 1 register sliding window, 2 LDS-tiled, 3 scalar (A/B measurement)."""
+    """0 auto, 1 register window (W/E from L1), 2 LDS-tiled, 3 scalar, 4-8 lane-exchange
+    register windows (DPP / shfl, 32-128 rows per tile) — A/B measurement."""
     _native.lib().gmt_jacobi5_set_variant(int(v))

@@ -1,0 +1,59 @@
+"""Native Jacobi engine through its C ABI (libgmt_engine.so), CPU backend.
+
+Each case runs in a fresh interpreter: the HIP and host engine libraries share
+the libgmt.so SONAME, so one process may only ever bind one backend.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from native_util import ROOT, ensure_host_build
+
+CODE = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+import numpy as np
+from gpu_mpi_tests_amd import engine
+from gpu_mpi_tests_amd.parallel import dist as gd
+env = gd.init(device="cpu")
+ny, nx, steps, periodic, overlap = {ny}, {nx}, {steps}, {periodic}, {overlap}
+e = engine.NativeJacobi(ny, nx, env, periodic=periodic, overlap=overlap, graph=True)
+e.run(steps); e.synchronize()
+got = e.interior()
+ref = engine.serial_jacobi(ny, nx, steps, periodic)
+res = e.residual()
+print(json.dumps(dict(diff=float(np.abs(got - ref).max()), shape=list(got.shape),
+                      transport=e.transport, overlap=e.overlap, graph=e.graph,
+                      halo=e.halo_bytes, resid=res)))
+e.close()
+"""
+
+
+def _run(**kw):
+    ensure_host_build()
+    code = CODE.format(root=ROOT, **kw)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES=""))
+    assert p.returncode == 0, p.stdout + p.stderr
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("ny,nx,steps", [(1, 1, 3), (5, 7, 4), (37, 53, 9), (64, 200, 12)])
+@pytest.mark.parametrize("periodic", [False, True])
+def test_native_engine_matches_numpy(ny, nx, steps, periodic):
+    r = _run(ny=ny, nx=nx, steps=steps, periodic=periodic, overlap=True)
+    assert r["shape"] == [ny, nx]
+    assert r["diff"] < 1e-13
+    assert r["transport"] == "local"
+    assert r["graph"] is False  # no hipGraphs on the CPU backend
+    # a single rank only exchanges (with itself) when the domain wraps around
+    assert (r["halo"] > 0) == periodic
+    assert r["resid"] >= 0.0
+
+
+def test_native_engine_serial_mode():
+    r = _run(ny=40, nx=41, steps=6, periodic=True, overlap=False)
+    assert r["diff"] < 1e-13 and r["overlap"] is False

@@ -167,6 +167,39 @@ def test_jacobi5(variant, ny, nx):
         ops.set_jacobi_variant(0)
 
 
+@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8])
+@pytest.mark.parametrize("ny,nx", [(1, 2), (3, 6), (33, 514), (64, 1024), (130, 1030), (257, 4096)])
+def test_jacobi5_lane_variants(variant, ny, nx):
+    """DPP / shfl lane-exchange kernels (Laplace form, even widths): bitwise equal
+    to the fp64 reference, including wave-edge lanes and partial tiles."""
+    ops.set_jacobi_variant(variant)
+    try:
+        u = _rand(ny + 2, nx + 16, seed=21)
+        un = torch.zeros_like(u)
+        un_ref = torch.zeros(u.shape, dtype=torch.float64)
+        ops.jacobi5(u, un, (8, nx, 1, ny))
+        ref.jacobi5(u.cpu(), un_ref, 8, nx, 1, ny, None, 0.25, 0.0)
+        torch.cuda.synchronize()
+        assert torch.equal(un.cpu(), un_ref)
+    finally:
+        ops.set_jacobi_variant(0)
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("n", [1, 5, 4097, 1 << 20, (1 << 20) + 3])
+def test_daxpy_variants(variant, n):
+    lib = _native.lib()
+    lib.gmt_daxpy_set_variant(variant)
+    try:
+        x, y = _rand(n, seed=31), _rand(n, seed=32)
+        exp = 2.0 * x + y
+        ops.daxpy(2.0, x, y)
+        torch.cuda.synchronize()
+        assert torch.equal(y, exp)
+    finally:
+        lib.gmt_daxpy_set_variant(0)
+
+
 def test_jacobi5_odd_origin_scalar_path():
     u = _rand(20, 40, seed=14)
     un, un_ref = torch.zeros_like(u), torch.zeros(20, 40, dtype=torch.float64)

@@ -1,0 +1,221 @@
+"""Golden-output and distributed-correctness tests of the native apps.
+
+The apps run on the CPU backend (build/bin-host: the same sources linked
+against the host runtime, the analogue of the reference's gtensor `host`
+build, /root/reference/CMakeLists.txt:59-69) under MPICH with 1-4 ranks.
+Report-line formats follow the reference binaries; the
+values are the reference's closed forms: DAXPY sums, the
+analytic derivative of x^3 + y^2 (err_norm at round-off), and for the Jacobi
+engine a bit-level comparison with a serial run of the whole problem.
+"""
+import re
+
+import pytest
+
+from native_util import have_mpi, run_app
+
+pytestmark = pytest.mark.skipif(not have_mpi(), reason="mpirun not available")
+
+
+def test_daxpy_reference_sum():
+    out = run_app("daxpy").stdout.splitlines()
+    assert len(out) == 1025
+    assert out[0] == "1.000000" and out[1023] == "1024.000000"
+    assert out[-1] == "SUM = 524800.000000"  # daxpy.cu:87, n(n+1)/2
+
+
+def test_daxpy_large_host_path_and_rate():
+    # BASELINE config "daxpy N=1M fp64 on CPU host path (plumbing)"
+    out = run_app("daxpy", "--n=1048576", "--iters=3").stdout
+    assert "SUM = 549756338176.000000" in out
+    assert re.search(r"# DAXPY n=1048576 impl=gmt backend=host: median [\d.]+ ms", out)
+
+
+def test_daxpy_nvtx_same_output():
+    out = run_app("daxpy_nvtx").stdout.splitlines()
+    assert out[-1] == "SUM = 524800.000000"
+
+
+def test_mpi_daxpy_managed_probe():
+    out = run_app("mpi_daxpy", np=2).stdout
+    assert "MEMORY_PER_CORE is not set" in out
+    assert re.search(r"RANK\[1/2\] => DEVICE\[1/1\] mem=\d+", out)
+    assert re.search(r"RANK\[2/2\] => DEVICE\[1/1\] mem=\d+", out)
+    for r in range(2):
+        assert f"{r}/2 SUM = 524800.000000" in out
+    assert "HIP PreferredLocation of 'm_x' is CPU (-1)" in out
+    assert "HIP PreferredLocation of 'd_x' is UNMANAGED" in out
+    assert "HIP PreferredLocation of 'x' is NOT HIP" in out
+
+
+def test_mpi_daxpy_memory_per_core_env():
+    out = run_app("mpi_daxpy", np=1, env={"MEMORY_PER_CORE": "4096"}).stdout
+    assert "MEMORY_PER_CORE=4096" in out
+
+
+def test_mpi_daxpy_gt_every_rank():
+    out = run_app("mpi_daxpy_gt", np=3).stdout
+    for r in range(3):
+        assert f"{r}/3 [0:0x00000000] SUM = 524800.000000" in out
+
+
+@pytest.mark.parametrize("variant", ["mpi_daxpy_nvtx_managed", "mpi_daxpy_nvtx_unmanaged"])
+@pytest.mark.parametrize("np_", [1, 2, 3])
+def test_mpi_daxpy_nvtx_sums_and_times(variant, np_):
+    per_node = 1200
+    out = run_app(variant, f"--n-per-node={per_node}", "--iters=2", np=np_).stdout
+    n = per_node // np_
+    assert f"1 nodes, {np_} ranks, {n} elements each, total {per_node}" in out
+    for r in range(np_):
+        assert f"{r}/{np_} SUM = {(n + 1) / 2:f}" in out          # mpi_daxpy_nvtx.cc:268
+        assert f"{r}/{np_} ALLSUM = {np_ * (n + 1) / 2:f}" in out  # :310
+        for what in ("total  ", "kernel ", "barrier", "gather "):
+            assert re.search(rf"{r}/{np_} TIME {what}: \d+\.\d{{3}}", out), what
+
+
+def test_mpienv_fortran_layout():
+    out = run_app("mpienv", np=2, env={"MEMORY_PER_CORE": "2048"}).stdout
+    assert " rank            0  MEMORY_PER_CORE=        2048" in out
+    assert " rank            1  MEMORY_PER_CORE=        2048" in out
+    # Fortran (i6) read of a 5-char buffer: blank -> 0, longer values truncated
+    out = run_app("mpienv", np=1, env={"MEMORY_PER_CORE": ""}).stdout
+    assert "MEMORY_PER_CORE=           0" in out
+    out = run_app("mpienv", np=1, env={"MEMORY_PER_CORE": "1234567"}).stdout
+    assert "MEMORY_PER_CORE=       12345" in out
+
+
+@pytest.mark.parametrize("np_", [1, 2, 3])
+def test_mpigatherinplace_integer_division(np_):
+    n = 1000
+    out = run_app("mpigatherinplace", f"--n={n}", np=np_).stdout
+    # allx(rank*N+i) = rank*i/N, integer division, i = 1..N (mpigatherinplace.f90:35)
+    lsums = [sum((r * i) // n for i in range(1, n + 1)) for r in range(np_)]
+    for r in range(np_):
+        m = re.search(rf"^\s+{r} /\s+{np_}\s+(\S+)\s+(\S+)$", out, re.M)
+        assert m, out
+        assert float(m.group(1)) == lsums[r]
+        assert float(m.group(2)) == sum(lsums)
+
+
+@pytest.mark.parametrize("np_", [1, 2, 4])
+def test_mpi_stencil_gt_1d(np_):
+    out = run_app("mpi_stencil_gt", "1", "--iters=5", np=np_).stdout
+    assert f"n procs  = {np_}" in out and "n_global = 1048576" in out
+    assert f"n_local  = {1048576 // np_}" in out
+    errs = [float(v) for v in re.findall(r"err_norm = ([\d.]+)", out)]
+    assert len(errs) == np_ and max(errs) < 1e-4  # exact for x^3 up to round-off
+    assert len(re.findall(rf"\d/{np_} exchange time \d+\.\d{{8}}", out)) == np_
+    if np_ > 1:
+        assert "16-byte halo exchange transport=mpi-direct" in out
+
+
+def test_mpi_stencil_gt_divisibility_error():
+    p = run_app("mpi_stencil_gt", "--n=1000", np=3, check=False)
+    assert p.returncode != 0
+    assert "must be divisor of domain size" in p.stdout
+
+
+_TEST_RE = re.compile(r"^TEST dim:(\d), (device |managed), buf:(\d); ([\d.]+), err=([\d.]+)$", re.M)
+_SUM_RE = re.compile(r"^TEST dim:(\d), (device |managed), buf:0; allreduce=([\d.]+)$", re.M)
+
+
+@pytest.mark.parametrize("np_", [1, 2, 3])
+def test_mpi_stencil2d_gt_all_variants(np_):
+    out = run_app("mpi_stencil2d_gt", "48", "6", "--n-other=300", np=np_).stdout
+    assert f"n procs        = {np_}" in out
+    assert f"n_global_deriv = {48 * np_}" in out and "n_global_other = 300" in out
+    tests = _TEST_RE.findall(out)
+    # 8 test_deriv lines in the reference order (mpi_stencil2d_gt.cc:692-716)
+    assert [(d, m, b) for d, m, b, _, _ in tests] == [
+        ("0", "device ", "1"), ("0", "device ", "0"), ("0", "managed", "1"), ("0", "managed", "0"),
+        ("1", "device ", "1"), ("1", "device ", "0"), ("1", "managed", "1"), ("1", "managed", "0")]
+    for *_, err in tests:
+        assert float(err) < 1e-5
+    sums = _SUM_RE.findall(out)
+    assert [(d, m) for d, m, _ in sums] == [("0", "device "), ("0", "managed"),
+                                            ("1", "device "), ("1", "managed")]
+    assert "WARNING" not in out  # all-reduce values checked against PI*n_other
+
+
+@pytest.mark.parametrize("transport", ["mpi-host", "mpi-direct", "ipc"])
+def test_mpi_stencil2d_gt_transport_parity(transport):
+    out = run_app("mpi_stencil2d_gt", "40", "4", "--n-other=256", "--no-managed",
+                  f"--transport={transport}", "--host-init", "--host-verify", np=3).stdout
+    tests = _TEST_RE.findall(out)
+    assert len(tests) == 4
+    for *_, err in tests:
+        assert float(err) < 1e-5
+
+
+def test_mpi_stencil2d_gt_json(tmp_path):
+    j = tmp_path / "r.jsonl"
+    run_app("mpi_stencil2d_gt", "32", "3", "--n-other=128", "--no-managed", f"--json={j}", np=2)
+    import json
+    recs = [json.loads(line) for line in j.read_text().splitlines()]
+    assert len(recs) == 6
+    assert {r["test"] for r in recs} == {"deriv", "sum"}
+    assert all(r["ranks"] == 2 for r in recs)
+
+
+@pytest.mark.parametrize("stage", ["0", "1"])
+def test_mpi_stencil2d_sycl(stage):
+    out = run_app("mpi_stencil2d_sycl", "32", stage, "5", "--ny=200", np=2).stdout
+    assert "nx_global  = 64" in out and f"stage_host = {stage}" in out
+    assert re.search(r"dev bytes  = [\d.]+ MB", out)
+    assert len(re.findall(r"\d/2 exchange time \d+\.\d{8} ms", out)) == 2
+    errs = [float(v) for v in re.findall(r"err_norm = ([\d.]+)", out)]
+    assert len(errs) == 2 and max(errs) < 1e-6
+
+
+def test_mpi_stencil2d_sycl_oo_strong_scaling_and_debug():
+    out = run_app("mpi_stencil2d_sycl_oo", "1", "0", "5", np=2).stdout
+    assert "n_global   = 1024" in out and "n_local    = 512" in out
+    assert len(re.findall(r"^\d: exchange time \d+\.\d{8} ms$", out, re.M)) == 2
+    # DEBUG build: domain/1024, one iteration, rank-serialised halo dumps
+    out = run_app("mpi_stencil2d_sycl_oo", "8", "0", "5", "--debug", np=2).stdout
+    assert "n_global   = 8" in out and "n_iter     = 1" in out
+    ghost = dict(re.findall(r"^(\d: ghost \[\d, :\]) (.*)$", out, re.M))
+    send = dict(re.findall(r"^(\d: send \[\d, :\]) (.*)$", out, re.M))
+    # rank 0's upper ghost rows = rank 1's first interior rows and vice versa
+    assert ghost["0: ghost [6, :]"] == send["1: send [2, :]"]
+    assert ghost["1: ghost [1, :]"] == send["0: send [5, :]"]
+
+
+@pytest.mark.parametrize("args,np_", [
+    (["64", "10"], 1),
+    (["64", "10", "--periodic"], 1),
+    (["50", "9"], 2),
+    (["50", "9", "--transport=ipc"], 2),
+    (["50", "9", "--transport=mpi-host", "--no-overlap"], 2),
+    (["41", "7", "--dims=2x2", "--transport=ipc"], 4),
+    (["41", "7", "--dims=2x2", "--periodic"], 4),
+    (["41", "7", "--dims=1x3", "--transport=mpi-host"], 3),
+    (["21", "5", "--weak", "--periodic", "--transport=ipc"], 3),
+])
+def test_mpi_jacobi2d_matches_serial(args, np_):
+    out = run_app("mpi_jacobi2d", *args, "--check", "--warmup=2", "--halo-iters=3", np=np_).stdout
+    m = re.search(r"check     : max\|diff\| vs serial = (\S+) OK", out)
+    assert m, out
+    assert re.search(r"MLUPS     : [\d.]+", out)
+
+
+@pytest.mark.parametrize("transport,np_", [("ipc", 2), ("mpi-host", 2), ("mpi-direct", 3), ("local", 1)])
+def test_mpi_halo_bench_data(transport, np_):
+    out = run_app("mpi_halo_bench", "8", "65536", "3", f"--transport={transport}", np=np_).stdout
+    rows = re.findall(r"^\s+(\d+)\s+2\s+[\d.]+\s+[\d.]+\s+[\d.]+$", out, re.M)
+    assert [int(r) for r in rows] == [8 << k for k in range(14)]
+    assert "MISMATCH" not in out
+
+
+def test_transport_errors_are_loud():
+    p = run_app("mpi_jacobi2d", "32", "2", "--transport=rccl", np=1, check=False)
+    assert p.returncode != 0 and "no RCCL" in p.stdout
+    p = run_app("mpi_jacobi2d", "32", "2", "--transport=bogus", np=1, check=False)
+    assert p.returncode != 0 and "unknown transport" in p.stdout
+
+
+def test_kernel_bench_host():
+    out = run_app("gmt_kernel_bench", "--daxpy-n=4096", "--jacobi-n=64", "--iters=2",
+                  "--only=daxpy,jacobi").stdout
+    assert len(re.findall(r"^daxpy\s+v\d", out, re.M)) == 5
+    assert len(re.findall(r"^jacobi5\s+v\d", out, re.M)) == 8
