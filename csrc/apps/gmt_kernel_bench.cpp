@@ -63,7 +63,7 @@ int main(int argc, char** argv) {
     GMT_CHECK("fill", gmt_fill_poly(1, n, 1, 1.0, 1e-9, 0.0, 0.0, y.data(), n, s));
     char shape[64];
     std::snprintf(shape, sizeof(shape), "n=%zu", n);
-    for (int v = 1; v <= 5; ++v) {
+    for (int v = 1; v <= 6; ++v) {
       gmt_daxpy_set_variant(v);
       const double ms = time_ms(s, iters, [&] { GMT_CHECK("daxpy", gmt_daxpy(n, 1e-3, x.data(), y.data(), s)); });
       report("daxpy", v, shape, ms, 24.0 * n);
@@ -80,7 +80,7 @@ int main(int argc, char** argv) {
     GMT_CHECK("fill", gmt_fill_poly(0, ld, n + 2, 0.0, 1e-5, 0.0, 1e-5, un.data(), ld, s));
     char shape[64];
     std::snprintf(shape, sizeof(shape), "%lldx%lld", (long long)n, (long long)n);
-    for (int v = 1; v <= 8; ++v) {
+    for (int v = 1; v <= 9; ++v) {
       if (v == 3 && n > 16384) continue;  // scalar reference kernel: too slow to matter
       gmt_jacobi5_set_variant(v);
       const double ms = time_ms(s, iters, [&] {

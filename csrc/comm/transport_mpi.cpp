@@ -6,6 +6,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <tuple>
 
 #include "gmt/buffer.hpp"
 #include "gmt/comm.hpp"
@@ -302,8 +303,7 @@ class IpcExchange : public Exchange {
       }
     waitall(ready, "ipc ready");
     // (3) write straight into the neighbours' receive buffers (xGMI / same GPU)
-    for (size_t i = 0; i < sends_.size(); ++i)
-      GMT_CHECK("ipc copy", gmt_rt_memcpy_async(remote_[i], sends_[i].buf, sends_[i].bytes, cs_));
+    copy_out();
     GMT_CHECK("ipc copy sync", gmt_rt_stream_synchronize(cs_));
     // (4) tell the receivers their data has landed
     for (auto& m : sends_)
@@ -320,6 +320,33 @@ class IpcExchange : public Exchange {
   void wait(gmt_stream_t) override { waitall(done_, "ipc done"); }
 
  private:
+  // All sends in one launch of the fused copy kernel (remote stores over
+  // xGMI, or same-device stores): no SDMA-engine setup latency, which on
+  // MI355X dominates for halo-sized messages.  GMT_IPC_COPY=sdma restores
+  // hipMemcpyAsync.
+  void copy_out() {
+    static const bool sdma = [] {
+      const char* e = std::getenv("GMT_IPC_COPY");
+      return e && std::string(e) == "sdma";
+    }();
+    gmt_copy2d_desc d[GMT_MAX_COPY2D];
+    int n = 0;
+    for (size_t i = 0; i < sends_.size(); ++i) {
+      const size_t b = sends_[i].bytes;
+      if (sdma || b % 8 != 0) {
+        GMT_CHECK("ipc copy", gmt_rt_memcpy_async(remote_[i], sends_[i].buf, b, cs_));
+        continue;
+      }
+      const int64_t w = static_cast<int64_t>(b / 8);
+      d[n++] = {sends_[i].buf, remote_[i], w, w, w, 1};
+      if (n == GMT_MAX_COPY2D) {
+        GMT_CHECK("ipc copy kernel", gmt_copy2d_batched(n, d, 8, cs_));
+        n = 0;
+      }
+    }
+    if (n) GMT_CHECK("ipc copy kernel", gmt_copy2d_batched(n, d, 8, cs_));
+  }
+
   MPI_Comm c_;
   int rank_;
   IpcCache* cache_;
@@ -335,7 +362,10 @@ class IpcTransport : public MpiTransport {
   explicit IpcTransport(MPI_Comm c) : MpiTransport(c) {
     GMT_CHECK("ipc copy stream", gmt_rt_stream_create(&cs_, 1));
   }
-  ~IpcTransport() override { gmt_rt_stream_destroy(cs_); }
+  ~IpcTransport() override {
+    gathers_.clear();
+    gmt_rt_stream_destroy(cs_);
+  }
   Kind kind() const override { return Kind::Ipc; }
   const char* name() const override { return "ipc"; }
   std::unique_ptr<Exchange> plan(const std::vector<Msg>& r, const std::vector<Msg>& s) override {
@@ -344,13 +374,33 @@ class IpcTransport : public MpiTransport {
   void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override {
     staged_allreduce(comm_, buf, n, s);
   }
+  // All-gather as one persistent IPC exchange: every rank writes its block
+  // straight into every peer's receive buffer.  Plans are cached per
+  // (send, recv, size) so the handle exchange happens once per buffer set.
   void allgather(const void* send, void* recv, size_t bpr, gmt_stream_t s) override {
-    staged_allgather(comm_, rank_, size_, send, recv, bpr, s);
+    char* r = static_cast<char*>(recv);
+    if (send != r + rank_ * bpr)
+      GMT_CHECK("gather self", gmt_rt_memcpy_async(r + rank_ * bpr, send, bpr, s));
+    if (size_ == 1) return;
+    const auto key = std::make_tuple(send, recv, bpr);
+    auto it = gathers_.find(key);
+    if (it == gathers_.end()) {
+      std::vector<Msg> recvs, sends;
+      for (int p = 0; p < size_; ++p) {
+        if (p == rank_) continue;
+        recvs.push_back({r + p * bpr, bpr, p, kGatherTag});
+        sends.push_back({const_cast<void*>(send), bpr, p, kGatherTag});
+      }
+      it = gathers_.emplace(key, plan(recvs, sends)).first;
+    }
+    it->second->run(s);
   }
 
  private:
+  static constexpr int kGatherTag = 777;
   gmt_stream_t cs_ = nullptr;
   IpcCache cache_;
+  std::map<std::tuple<const void*, void*, size_t>, std::unique_ptr<Exchange>> gathers_;
 };
 
 }  // namespace

@@ -14,6 +14,11 @@
 //      nontemporal stores of y
 //   4  one block per 256*U*2 elements, U = 4, plain loads, nontemporal stores
 //   5  one block per 256*U*2 elements, U = 8, plain loads, nontemporal stores
+//   6  (default) 128-thread blocks, ONE 16-B chunk of x and y per lane,
+//      nontemporal loads AND stores: every byte is touched once, so nothing
+//      is worth keeping in L2/MALL.  Measured 0.974 ms at n = 2^28 = 6.62 TB/s
+//      effective vs 1.076 ms (5.99 TB/s) for rocblas_daxpy and 1.12 ms for v1
+//      (profiles/r01_sweep2.md).  rocBLAS moves one double per lane.
 #include "common.hpp"
 #include "gmt/kernels.h"
 
@@ -49,6 +54,13 @@ __global__ __launch_bounds__(kBlock) void daxpy_tile(int64_t n2, double a,
       if (i < n2) st2(y + 2 * i, a * ld2(x + 2 * i) + ld2(y + 2 * i));
     }
   }
+}
+
+template <int B>
+__global__ __launch_bounds__(B) void daxpy_stream(int64_t n2, double a, const double* __restrict__ x,
+                                                  double* __restrict__ y) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * B + threadIdx.x;
+  if (i < n2) st2_nt(y + 2 * i, a * ld2_nt(x + 2 * i) + ld2_nt(y + 2 * i));
 }
 
 template <int U>
@@ -115,8 +127,12 @@ extern "C" int gmt_daxpy(int64_t n, double a, const double* x, double* y, void* 
           break;
         }
         case 5: launch_tile<8, false, true>(n2, a, x, y, s); break;
-        case 4:
-        default: launch_tile<4, false, true>(n2, a, x, y, s); break;
+        case 4: launch_tile<4, false, true>(n2, a, x, y, s); break;
+        default: {
+          constexpr int B = 128;
+          daxpy_stream<B><<<grid_1d((n2 + B - 1) / B), B, 0, s>>>(n2, a, x, y);
+          break;
+        }
       }
     }
     if (n & 1) daxpy_scalar_kernel<<<1, kBlock, 0, s>>>(1, a, x + n - 1, y + n - 1);

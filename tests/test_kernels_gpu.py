@@ -148,7 +148,7 @@ def test_fill_poly(mode):
     torch.testing.assert_close(z, exp, rtol=1e-14, atol=1e-14)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant", [1, 2, 3, 9])
 @pytest.mark.parametrize("ny,nx", [(1, 2), (3, 7), (33, 513), (64, 1024), (100, 1030)])
 def test_jacobi5(variant, ny, nx):
     ops.set_jacobi_variant(variant)
@@ -167,7 +167,7 @@ def test_jacobi5(variant, ny, nx):
         ops.set_jacobi_variant(0)
 
 
-@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("ny,nx", [(1, 2), (3, 6), (33, 514), (64, 1024), (130, 1030), (257, 4096)])
 def test_jacobi5_lane_variants(variant, ny, nx):
     """DPP / shfl lane-exchange kernels (Laplace form, even widths): bitwise equal
@@ -185,7 +185,7 @@ def test_jacobi5_lane_variants(variant, ny, nx):
         ops.set_jacobi_variant(0)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("n", [1, 5, 4097, 1 << 20, (1 << 20) + 3])
 def test_daxpy_variants(variant, n):
     lib = _native.lib()
@@ -198,6 +198,25 @@ def test_daxpy_variants(variant, n):
         assert torch.equal(y, exp)
     finally:
         lib.gmt_daxpy_set_variant(0)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 9])
+def test_jacobi5_large_residual_two_level_reduction(variant):
+    """>1024 per-block partials: the deterministic two-level reduction."""
+    ops.set_jacobi_variant(variant)
+    try:
+        ny, nx = 2000, 4000
+        u = _rand(ny + 2, nx + 16, seed=41)
+        un = torch.zeros_like(u)
+        r = ops.jacobi5(u, un, (8, nx, 1, ny), resid=True)
+        un_ref = torch.zeros(u.shape, dtype=torch.float64)
+        r_ref = ref.jacobi5(u.cpu(), un_ref, 8, nx, 1, ny, None, 0.25, 0.0)
+        torch.testing.assert_close(un.cpu(), un_ref, rtol=1e-14, atol=1e-14)
+        assert abs(float(r) - float(r_ref)) <= 1e-10 * float(r_ref)
+        r2 = ops.jacobi5(u, un, (8, nx, 1, ny), resid=True)
+        assert float(r2) == float(r)  # deterministic order
+    finally:
+        ops.set_jacobi_variant(0)
 
 
 def test_jacobi5_odd_origin_scalar_path():
