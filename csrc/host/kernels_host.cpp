@@ -27,6 +27,7 @@ int gmt_daxpy(int64_t n, double a, const double* x, double* y, void*) {
 }
 
 void gmt_daxpy_set_variant(int v) { g_daxpy_variant = v; }
+void gmt_stencil5_set_variant(int) {}
 int gmt_daxpy_get_variant(void) { return g_daxpy_variant; }
 
 int gmt_stencil5_1d(int64_t n_out, const double* c, double scale, const double* in, double* out,

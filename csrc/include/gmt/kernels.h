@@ -41,6 +41,9 @@ int gmt_stencil5_2d(int dim, int64_t nx_out, int64_t ny_out, const double* coef5
                     double scale, const double* in, int64_t ld_in, double* out,
                     int64_t ld_out, void* stream);
 
+/* 0/2 = per-thread kernels (default), 1 = register-window kernels (A/B) */
+void gmt_stencil5_set_variant(int variant);
+
 /* ---- K6/K7/K8: batched strided 2-D copy (halo pack / unpack, fused L+R).
  *      Each descriptor copies `height` rows of `width` elements of
  *      `elem_bytes` (4 or 8) from src (row pitch src_ld elements) to dst

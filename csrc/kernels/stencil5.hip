@@ -12,6 +12,7 @@
 // three overlapping 16-B loads (in[2t..2t+5]); the overlap is served by L1,
 // so HBM sees each input byte once.  A block covers 512 outputs of ROWS0 rows.
 //
+// Variant 1 (kept for A/B; variant 2, below, is the default):
 // dim 1 (taps along the strided axis): each lane owns 2 adjacent columns and
 // walks down ROWS1 rows keeping a 5-row register window, so every input row
 // is loaded once per column strip (+4 halo rows per strip => (R+4)/R reads).
@@ -101,6 +102,44 @@ __global__ __launch_bounds__(kBlock) void stencil5_d1_vec(int64_t nx, int64_t ny
   }
 }
 
+// Default kernels (variant 2): one output pair per thread, 64 x 4 threads per
+// block (128 columns x 4 rows), XCD-swizzled so the tiles that share input
+// rows sit on one XCD's L2, nontemporal stores (the derivative is written
+// once and not re-read by this kernel).  Same structure as the measured
+// fastest Jacobi kernel (jacobi5.hip variant 9): short-lived threads with
+// every load independent, reuse served by L1/L2 instead of registers.
+template <int DIM>
+__global__ __launch_bounds__(kBlock) void stencil5_pt(int64_t nx_out, int64_t ny_out, Coef5 cf,
+                                                      double scale, const double* __restrict__ in,
+                                                      int64_t ld_in, double* __restrict__ out,
+                                                      int64_t ld_out, int64_t nbx, int64_t nblocks) {
+  const int64_t t = xcd_swizzle(blockIdx.x, nblocks);
+  const int64_t bx = t % nbx, by = t / nbx;
+  const int64_t x = (bx * kWave + (threadIdx.x & (kWave - 1))) * 2;
+  const int64_t y = by * (kBlock / kWave) + threadIdx.x / kWave;
+  if (x >= nx_out || y >= ny_out) return;
+  const double c0 = cf.c[0] * scale, c1 = cf.c[1] * scale, c2 = cf.c[2] * scale,
+               c3 = cf.c[3] * scale, c4 = cf.c[4] * scale;
+  const double* p = in + y * ld_in + x;
+  if (x + 1 < nx_out) {
+    d2 o;
+    if (DIM == 0) {
+      const d2 a = ld2(p), m = ld2(p + 2), e = ld2(p + 4);
+      o.x = c0 * a.x + c1 * a.y + c2 * m.x + c3 * m.y + c4 * e.x;
+      o.y = c0 * a.y + c1 * m.x + c2 * m.y + c3 * e.x + c4 * e.y;
+    } else {
+      o = c0 * ld2(p) + c1 * ld2(p + ld_in) + c2 * ld2(p + 2 * ld_in) + c3 * ld2(p + 3 * ld_in) +
+          c4 * ld2(p + 4 * ld_in);
+    }
+    st2_nt(out + y * ld_out + x, o);
+  } else {
+    const int64_t st = DIM == 0 ? 1 : ld_in;
+    out[y * ld_out + x] = c0 * p[0] + c1 * p[st] + c2 * p[2 * st] + c3 * p[3 * st] + c4 * p[4 * st];
+  }
+}
+
+static int g_stencil_variant = 0;
+
 // Generic fallback for unaligned views: one output per lane.
 __global__ __launch_bounds__(kBlock) void stencil5_scalar(int dim, int64_t nx_out,
                                                           int64_t ny_out, Coef5 cf,
@@ -126,6 +165,8 @@ static Coef5 make_coef(const double* c5) {
 
 }  // namespace gmt
 
+extern "C" void gmt_stencil5_set_variant(int v) { gmt::g_stencil_variant = v; }
+
 extern "C" int gmt_stencil5_2d(int dim, int64_t nx_out, int64_t ny_out, const double* coef5,
                                double scale, const double* in, int64_t ld_in, double* out,
                                int64_t ld_out, void* stream) {
@@ -135,7 +176,16 @@ extern "C" int gmt_stencil5_2d(int dim, int64_t nx_out, int64_t ny_out, const do
   hipStream_t s = static_cast<hipStream_t>(stream);
   const Coef5 cf = make_coef(coef5);
   const bool vec_ok = aligned16(in) && aligned16(out) && (ld_in % 2 == 0) && (ld_out % 2 == 0);
-  if (vec_ok) {
+  if (vec_ok && g_stencil_variant != 1) {
+    const int64_t nbx = (nx_out + 2 * kWave - 1) / (2 * kWave);
+    const int64_t nb = nbx * ((ny_out + kBlock / kWave - 1) / (kBlock / kWave));
+    if (dim == 0)
+      stencil5_pt<0><<<grid_1d(nb), kBlock, 0, s>>>(nx_out, ny_out, cf, scale, in, ld_in, out,
+                                                    ld_out, nbx, nb);
+    else
+      stencil5_pt<1><<<grid_1d(nb), kBlock, 0, s>>>(nx_out, ny_out, cf, scale, in, ld_in, out,
+                                                    ld_out, nbx, nb);
+  } else if (vec_ok) {
     const int64_t nbx = (nx_out + 2 * kBlock - 1) / (2 * kBlock);
     if (dim == 0) {
       const int64_t nby = (ny_out + ROWS0 - 1) / ROWS0;

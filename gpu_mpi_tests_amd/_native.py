@@ -63,6 +63,7 @@ _SIGS = {
     ),
     "gmt_jacobi5_set_variant": (None, [c_int]),
     "gmt_daxpy_set_variant": (None, [c_int]),
+    "gmt_stencil5_set_variant": (None, [c_int]),
     "gmt_daxpy_get_variant": (c_int, []),
     "gmt_jacobi5_get_variant": (c_int, []),
     "gmt_error_string": (ctypes.c_char_p, [c_int]),

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 kernel-trace database (``*_results.db``) as markdown.
 
-Usage: python scripts/rocprof_summary.py <results.db> [--bytes KERNEL_SUBSTR=BYTES ...] [-o out.md]
+Usage: python scripts/rocprof_summary.py <results.db | *_kernel_stats.csv> [--bytes KERNEL_SUBSTR=BYTES ...] [-o out.md]
 
 ``--bytes`` attaches a known byte count per dispatch to kernels whose name
 contains the substring, so the table shows the achieved bandwidth (GB/s) next
@@ -10,6 +10,7 @@ to the HBM3E roofline (~6.3 TB/s measured stream rate on MI355X).
 from __future__ import annotations
 
 import argparse
+import csv
 import re
 import sqlite3
 
@@ -40,8 +41,13 @@ def main(argv=None):
     for kv in a.bytes:
         k, v = kv.rsplit("=", 1)
         nbytes.append((k, float(eval(v, {"__builtins__": {}}))))  # simple arithmetic only
-    c = sqlite3.connect(a.db)
-    rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
+    if a.db.endswith(".csv"):  # rocprofv3 --stats --output-format csv (durations in ns)
+        with open(a.db) as f:
+            rows = [(r["Name"], int(r["Calls"]), float(r["TotalDurationNs"]) / 1e3,
+                     float(r["AverageNs"]) / 1e3, float(r["Percentage"])) for r in csv.DictReader(f)]
+    else:
+        c = sqlite3.connect(a.db)
+        rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
     out = [f"# {a.title}", "", f"source: `{a.db}` (rocprofv3 --kernel-trace --stats)", "",
            "| kernel | calls | total µs | avg µs | % | GB/s (known bytes) |", "|---|---|---|---|---|---|"]
     for name, calls, tot, avg, pct in rows:

@@ -68,6 +68,20 @@ def test_stencil5_2d(dim, ny, nx):
     torch.testing.assert_close(out, exp, rtol=1e-13, atol=1e-13)
 
 
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("dim", [0, 1])
+@pytest.mark.parametrize("ny,nx", [(1, 9), (7, 13), (33, 1030), (130, 516), (64, 2049)])
+def test_stencil5_2d_variants(variant, dim, ny, nx):
+    _native.lib().gmt_stencil5_set_variant(variant)
+    try:
+        z = _rand(ny + (4 if dim == 1 else 0), nx + (4 if dim == 0 else 0), seed=16)
+        out = ops.stencil5_2d(z, dim, scale=3.0)
+        exp = ref.stencil5_2d(z.cpu(), dim, 3.0).to(DEV)
+        torch.testing.assert_close(out, exp, rtol=1e-13, atol=1e-13)
+    finally:
+        _native.lib().gmt_stencil5_set_variant(0)
+
+
 @pytest.mark.parametrize("dim", [0, 1])
 def test_stencil5_2d_strided_views(dim):
     big = _rand(100, 700, seed=7)
