@@ -134,7 +134,9 @@ def main(argv=None):
     ap.add_argument("--size", type=int, default=32768, help="global domain is size x size (default 32768)")
     ap.add_argument("--engine", choices=("native", "torch"), default="native")
     ap.add_argument("--no-overlap", action="store_true")
-    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
+                    help="hipGraph replay of the step (auto: on for 1 GPU; eager RCCL steps "
+                         "for N>1, where a step is >100 us of GPU work and launches hide)")
     ap.add_argument("--dims", type=str, default=None, help="process grid PYxPX, e.g. 4x2")
     ap.add_argument("--daxpy-n", type=int, default=1 << 28)
     ap.add_argument("--skip-extras", action="store_true", help="headline stencil only")
@@ -147,9 +149,13 @@ def main(argv=None):
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
     dims = tuple(int(v) for v in args.dims.lower().split("x")) if args.dims else None
     overlap = not args.no_overlap
-    if args.engine == "native":
+    engine = args.engine
+    if engine == "native" and env.world_size > 1 and not env.is_gpu:
+        engine = "torch"  # the native engine's multi-rank data plane is RCCL (GPU only)
+    graph = args.graph == "on" or (args.graph == "auto" and env.world_size == 1)
+    if engine == "native":
         solver, dt, info = bench_native(env, args.size, args.steps, args.warmup, overlap, dims,
-                                        not args.no_graph, args.variant)
+                                        graph, args.variant)
     else:
         if env.is_gpu and args.variant:
             ops.set_jacobi_variant(args.variant)

@@ -1,0 +1,49 @@
+"""bench.py driver contract on CPU: one JSON line from rank 0 with the
+required keys, for 1 process and for 2 processes under torch.distributed.run
+(gloo; the GPU run uses RCCL through the native engine)."""
+import json
+import os
+import random
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _run(cmd, timeout=600):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stdout + p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+def _check(rec, n, steps, warmup):
+    assert KEYS <= set(rec)
+    assert rec["n_gpus"] == n and rec["steps"] == steps and rec["warmup"] == warmup
+    assert rec["value"] > 0 and rec["unit"] == "MLUPS" and rec["higher_is_better"] is True
+    assert rec["dtype"] == "fp64" and rec["scaling"] == "strong"
+    assert {"model", "global_batch", "seq_len", "parallelism"} <= set(rec["config"])
+    assert rec["config"]["global_batch"] == 256 * 256
+
+
+def test_bench_single_process_native_engine_cpu():
+    rec = _run([sys.executable, "bench.py", "--device", "cpu", "--size", "256", "--steps", "4",
+                "--warmup", "1", "--daxpy-n", "20000"])
+    _check(rec, 1, 4, 1)
+    assert rec["config"]["engine"] == "native"
+    assert rec["daxpy_GBps"] > 0
+
+
+def test_bench_two_ranks_torchrun_cpu():
+    port = str(random.randint(20000, 40000))
+    rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
+                "--device", "cpu", "--size", "256", "--steps", "3", "--warmup", "1",
+                "--daxpy-n", "20000"])
+    _check(rec, 2, 3, 1)
+    assert rec["config"]["engine"] == "torch"  # multi-rank CPU runs use torch.distributed (gloo)
+    assert rec["halo_exchange_us"] is not None and rec["halo_exchange_us"] > 0
