@@ -89,6 +89,24 @@ int main(int argc, char** argv) {
       report("jacobi5", v, shape, ms, 16.0 * n * n);
     }
     gmt_jacobi5_set_variant(0);
+    // temporal blocking: two sweeps per call; "GB/s" is the single-sweep
+    // equivalent (2 x 16 B per point), i.e. directly comparable with v1-v9
+    {
+      const int64_t g = 2;
+      const int64_t ld2 = ((xo + n + g + 63) / 64) * 64;
+      Buffer<double> a(static_cast<size_t>(ld2) * (n + 2 * g), GMT_SPACE_DEVICE), b(a.size(), GMT_SPACE_DEVICE);
+      GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, a.data(), ld2, s));
+      GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, b.data(), ld2, s));
+      const int64_t rect[4] = {xo, n, g, n};
+      for (int ty : {8, 16, 32}) {
+        const double ms = time_ms(s, iters, [&] {
+          GMT_CHECK("x2", gmt_jacobi5x2(1, rect, rect, 0, a.data(), b.data(), ld2, ty, s));
+        });
+        char tag[64];
+        std::snprintf(tag, sizeof(tag), "%s x2 ty=%d", shape, ty);
+        report("jacobi5x2", ty, tag, ms, 2 * 16.0 * n * n);
+      }
+    }
   }
   if (only.find("stencil") != std::string::npos) {
     // the reference's default deriv shapes: 1028 x 524288 (dim 0), 524288 x 1028 (dim 1)

@@ -11,7 +11,9 @@
 //   --weak                  n x n PER RANK (global = py*n x px*n)
 //   --dims=PYxPX            process grid (default: minimise halo bytes)
 //   --transport=auto|rccl|ipc|mpi-host|mpi-direct
-//   --no-overlap --graph --periodic --warmup=W --variant=V (1 reg, 2 lds, 3 scalar)
+//   --no-overlap --graph --periodic --warmup=W --variant=V (1 reg, 2 lds, 3 scalar, 9 pt)
+//   --tblock[=TY]           temporal blocking: 2 sweeps per pass and per exchange
+//                           (gmt_jacobi5x2, tile of 128 x TY, TY = 8|16|32)
 //   --halo-iters=K          K blocking halo exchanges -> latency line
 //   --check                 rank 0 re-runs the whole problem serially on the host
 //   --json=FILE
@@ -96,6 +98,8 @@ int main(int argc, char** argv) {
   c.overlap = !cli.flag("no-overlap");
   c.graph = cli.flag("graph");
   c.variant = static_cast<int>(cli.geti("variant", 0));
+  c.tblock = cli.has("tblock") && cli.get("tblock", "1") != "0";
+  if (c.tblock && cli.get("tblock", "1") != "1") c.tile_rows = std::atoi(cli.get("tblock", "16").c_str());
   // with one rank and no periodic wrap there is nothing to exchange; with a
   // periodic wrap a single rank exchanges with itself
   comm::Kind kind = comm::parse_kind(cli.get("transport", "auto"));
@@ -172,8 +176,8 @@ int main(int argc, char** argv) {
     std::printf("grid      = %dx%d (py x px)\n", c.py, c.px);
     std::printf("global    = %lld x %lld\n", (long long)c.ny_global, (long long)c.nx_global);
     std::printf("local     = %lld x %lld (rank 0)\n", (long long)lny, (long long)lnx);
-    std::printf("transport = %s overlap=%d graph=%d periodic=%d backend=%s\n", tr->name(), overlap,
-                graph, c.periodic, gmt_rt_backend_name());
+    std::printf("transport = %s overlap=%d graph=%d periodic=%d tblock=%d backend=%s\n", tr->name(),
+                overlap, graph, c.periodic, c.tblock, gmt_rt_backend_name());
     std::printf("steps     = %d (warmup %d)\n", n_iter, n_warmup);
     std::printf("TIME step : %0.6f ms\n", t_step * 1e3);
     std::printf("MLUPS     : %0.1f (per GPU %0.1f, %0.1f GB/s per GPU at 16 B/pt)\n", mlups,
@@ -186,7 +190,7 @@ int main(int argc, char** argv) {
     JsonRecord j;
     j.add("app", "mpi_jacobi2d").add("ranks", world).add("py", c.py).add("px", c.px)
         .add("ny", (long long)c.ny_global).add("nx", (long long)c.nx_global).add("transport", tr->name())
-        .add("overlap", overlap).add("graph", graph).add("steps", n_iter).add("ms_per_step", t_step * 1e3)
+        .add("overlap", overlap).add("graph", graph).add("tblock", c.tblock).add("steps", n_iter).add("ms_per_step", t_step * 1e3)
         .add("MLUPS", mlups).add("halo_us", halo_us).add("halo_bytes", hbytes).add("residual", resid)
         .add("check_max_diff", max_diff);
     j.append_to(cli.get("json", ""));

@@ -45,6 +45,7 @@ void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank,
   c.periodic = flags & 1;
   c.overlap = (flags & 2) != 0;
   c.graph = (flags & 4) != 0;
+  c.tblock = (flags & 8) != 0;
   c.variant = variant;
   h->py = py;
   h->px = px;
@@ -86,6 +87,7 @@ int gmt_engine_jacobi_info(void* p, int64_t* out) {
   out[7] = s.overlap_active();
   out[8] = h->py;
   out[9] = h->px;
+  out[10] = s.tblock();
   return 0;
 }
 int gmt_engine_jacobi_copy_interior(void* p, double* host) {

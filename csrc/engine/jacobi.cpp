@@ -47,8 +47,10 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   nb_.south = cy > 0 ? at(cy - 1, cx) : (c.periodic ? at(c.py - 1, cx) : -1);
   nb_.north = cy < c.py - 1 ? at(cy + 1, cx) : (c.periodic ? at(0, cx) : -1);
 
-  ld_ = round_up(xo_ + nx_ + 1, 64);
-  const size_t elems = static_cast<size_t>(ld_) * (ny_ + 2);
+  g_ = c.tblock ? 2 : 1;
+  yo_ = g_;
+  ld_ = round_up(xo_ + nx_ + g_, 64);
+  const size_t elems = static_cast<size_t>(ld_) * (ny_ + 2 * g_);
   GMT_CHECK("stream", gmt_rt_stream_create(&s_, 0));
   GMT_CHECK("comm stream", gmt_rt_stream_create(&cs_, 1));
   GMT_CHECK("event", gmt_rt_event_create(&ev_start_, 0));
@@ -61,14 +63,14 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   for (int b = 0; b < 2; ++b) {
     buf_[b] = Buffer<double>(elems, GMT_SPACE_DEVICE);
     GMT_CHECK("memset", gmt_rt_memset_async(buf_[b].data(), 0, buf_[b].bytes(), s_));
-    GMT_CHECK("fill", gmt_fill_poly(0, nx_ + 2, ny_ + 2, (ox_ - 1) * h, h, (oy_ - 1) * h, h,
-                                    buf_[b].data() + (xo_ - 1), ld_, s_));
+    GMT_CHECK("fill", gmt_fill_poly(0, nx_ + 2 * g_, ny_ + 2 * g_, (ox_ - g_) * h, h,
+                                    (oy_ - g_) * h, h, buf_[b].data() + (xo_ - g_), ld_, s_));
   }
   GMT_CHECK("init sync", gmt_rt_stream_synchronize(s_));
   resid_ws_ = Buffer<double>(gmt_jacobi_resid_workspace(nx_, ny_) + 1, GMT_SPACE_DEVICE);
   for (int b = 0; b < 2; ++b) {
-    Span2D<double> f(buf_[b].data() + (xo_ - 1), nx_ + 2, ny_ + 2, ld_);
-    halo_[b] = std::make_unique<Halo2D>(t_, f, 1, 1, nb_, false, GMT_SPACE_DEVICE);
+    Span2D<double> f(buf_[b].data() + (xo_ - g_), nx_ + 2 * g_, ny_ + 2 * g_, ld_);
+    halo_[b] = std::make_unique<Halo2D>(t_, f, g_, g_, nb_, false, GMT_SPACE_DEVICE, c.tblock);
   }
   if (c.graph) capture_graphs();
 }
@@ -77,6 +79,7 @@ JacobiSolver::~JacobiSolver() {
   if (s_) gmt_rt_stream_synchronize(s_);
   if (cs_) gmt_rt_stream_synchronize(cs_);
   for (auto& g : graph_) gmt_rt_graph_destroy(g);
+  for (auto& g : graph2_) gmt_rt_graph_destroy(g);
   gmt_rt_event_destroy(ev_start_);
   gmt_rt_event_destroy(ev_halo_);
   halo_[0].reset();
@@ -88,7 +91,7 @@ JacobiSolver::~JacobiSolver() {
 void JacobiSolver::sweep_full(int parity, double* resid) {
   const double* u = buf_[parity].data();
   double* un = buf_[parity ^ 1].data();
-  GMT_CHECK("jacobi sweep", gmt_jacobi5(xo_, nx_, 1, ny_, u, un, ld_, nullptr, 0, kC0, 0.0, resid, s_));
+  GMT_CHECK("jacobi sweep", gmt_jacobi5(xo_, nx_, yo_, ny_, u, un, ld_, nullptr, 0, kC0, 0.0, resid, s_));
 }
 
 void JacobiSolver::enqueue_step(int parity) {
@@ -108,8 +111,8 @@ void JacobiSolver::enqueue_step(int parity) {
   // core: every cell whose 5-point stencil stays inside the interior; it
   // starts at an even column so the sweep keeps its 16-B vector path
   GMT_CHECK("event", gmt_rt_event_record(ev_start_, s_));
-  GMT_CHECK("core sweep", gmt_jacobi5(xo_ + 2, nx_ - 4, 2, ny_ - 2, u, un, ld_, nullptr, 0, kC0,
-                                      0.0, nullptr, s_));
+  GMT_CHECK("core sweep", gmt_jacobi5(xo_ + 2, nx_ - 4, yo_ + 1, ny_ - 2, u, un, ld_, nullptr, 0,
+                                      kC0, 0.0, nullptr, s_));
   // halo on the high-priority stream, concurrent with the core sweep
   GMT_CHECK("wait", gmt_rt_stream_wait_event(cs_, ev_start_));
   h.start(cs_);
@@ -117,9 +120,65 @@ void JacobiSolver::enqueue_step(int parity) {
   GMT_CHECK("event", gmt_rt_event_record(ev_halo_, cs_));
   GMT_CHECK("wait", gmt_rt_stream_wait_event(s_, ev_halo_));
   // boundary frame: first/last row, first/last two columns
-  const int64_t rects[16] = {xo_,           nx_, 1, 1,       xo_, nx_, ny_, 1,
-                             xo_,           2,   2, ny_ - 2, xo_ + nx_ - 2, 2, 2, ny_ - 2};
+  const int64_t y0 = yo_, y1 = yo_ + 1;
+  const int64_t rects[16] = {xo_, nx_, y0,            1,       xo_,           nx_, yo_ + ny_ - 1, 1,
+                             xo_, 2,   y1,            ny_ - 2, xo_ + nx_ - 2, 2,   y1,            ny_ - 2};
   GMT_CHECK("frame sweep", gmt_jacobi5_rects(4, rects, u, un, ld_, nullptr, 0, kC0, 0.0, s_));
+}
+
+int JacobiSolver::halo_mask() const {
+  return (nb_.west >= 0 ? 1 : 0) | (nb_.east >= 0 ? 2 : 0) | (nb_.south >= 0 ? 4 : 0) |
+         (nb_.north >= 0 ? 8 : 0);
+}
+
+// Two sweeps u(t) -> u(t+2) in one pass: the 2-wide halo (corners included)
+// travels on the comm stream while the fused kernel updates the core whose
+// two-step dependency cone stays inside the interior; the 2-wide frame
+// follows once the halo has landed.
+void JacobiSolver::enqueue_pair(int parity) {
+  Halo2D& h = *halo_[parity];
+  const double* u = buf_[parity].data();
+  double* un = buf_[parity ^ 1].data();
+  const int64_t dom[4] = {xo_, nx_, yo_, ny_};
+  const int mask = halo_mask();
+  const int tr = cfg_.tile_rows;
+  if (!h.active()) {
+    GMT_CHECK("jacobi x2", gmt_jacobi5x2(1, dom, dom, mask, u, un, ld_, tr, s_));
+    return;
+  }
+  if (!cfg_.overlap || nx_ < 10 || ny_ < 8) {
+    h.start(s_);
+    h.finish(s_);
+    GMT_CHECK("jacobi x2", gmt_jacobi5x2(1, dom, dom, mask, u, un, ld_, tr, s_));
+    return;
+  }
+  // right frame starts at an even column (16-B staging): 2 or 3 columns wide
+  const int64_t xr = (xo_ + nx_ - 2) & ~int64_t(1);
+  const int64_t core[4] = {xo_ + 2, xr - xo_ - 2, yo_ + 2, ny_ - 4};
+  GMT_CHECK("event", gmt_rt_event_record(ev_start_, s_));
+  GMT_CHECK("core x2", gmt_jacobi5x2(1, core, dom, mask, u, un, ld_, tr, s_));
+  GMT_CHECK("wait", gmt_rt_stream_wait_event(cs_, ev_start_));
+  h.start(cs_);
+  h.finish(cs_);
+  GMT_CHECK("event", gmt_rt_event_record(ev_halo_, cs_));
+  GMT_CHECK("wait", gmt_rt_stream_wait_event(s_, ev_halo_));
+  const int64_t frame[16] = {xo_, nx_,            yo_,           2,        xo_, nx_, yo_ + ny_ - 2, 2,
+                             xo_, 2,              yo_ + 2,       ny_ - 4,  xr,  xo_ + nx_ - xr, yo_ + 2, ny_ - 4};
+  GMT_CHECK("frame x2", gmt_jacobi5x2(4, frame, dom, mask, u, un, ld_, tr, s_));
+}
+
+void JacobiSolver::step_pair() {
+  if (graph2_[parity_])
+    GMT_CHECK("graph launch", gmt_rt_graph_launch(graph2_[parity_], s_));
+  else
+    enqueue_pair(parity_);
+  parity_ ^= 1;  // u(t+2) lives in the other buffer
+}
+
+void JacobiSolver::run(int k) {
+  if (cfg_.tblock)
+    for (; k >= 2; k -= 2) step_pair();
+  for (; k > 0; --k) step();
 }
 
 void JacobiSolver::capture_graphs() {
@@ -136,19 +195,24 @@ void JacobiSolver::capture_graphs() {
     halo_[b]->finish(cs_);
   }
   GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));
-  for (int p = 0; p < 2; ++p) {
+  for (int p = 0; p < 4; ++p) {
+    if (p >= 2 && !cfg_.tblock) break;
     int e = gmt_rt_stream_begin_capture(s_);
     if (e == 0) {
-      enqueue_step(p);
-      e = gmt_rt_stream_end_capture(s_, &graph_[p]);
+      if (p < 2)
+        enqueue_step(p);
+      else
+        enqueue_pair(p - 2);
+      e = gmt_rt_stream_end_capture(s_, p < 2 ? &graph_[p] : &graph2_[p - 2]);
     }
     if (e != 0) {
       std::printf("# jacobi: hipGraph capture unavailable (%s); running eagerly\n",
                   gmt_rt_error_string(e));
-      for (auto& g : graph_) {
-        gmt_rt_graph_destroy(g);
-        g = nullptr;
-      }
+      for (auto* arr : {graph_, graph2_})
+        for (int i = 0; i < 2; ++i) {
+          gmt_rt_graph_destroy(arr[i]);
+          arr[i] = nullptr;
+        }
       return;
     }
   }
@@ -188,7 +252,7 @@ void JacobiSolver::exchange_only() {
 }
 
 void JacobiSolver::copy_interior(double* host) const {
-  const double* src = buf_[parity_].data() + xo_ + ld_;
+  const double* src = buf_[parity_].data() + xo_ + yo_ * ld_;
   GMT_CHECK("interior D2H", gmt_rt_memcpy2d_async(host, nx_ * sizeof(double), src,
                                                   ld_ * sizeof(double), nx_ * sizeof(double), ny_, s_));
   GMT_CHECK("interior sync", gmt_rt_stream_synchronize(s_));

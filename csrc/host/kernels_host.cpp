@@ -149,6 +149,33 @@ int gmt_jacobi5_rects(int n_rect, const int64_t* r, const double* u, double* un,
   return 0;
 }
 
+int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int mask, const double* u,
+                  double* un, int64_t ld, int, void*) {
+  if (n_rect < 0 || n_rect > 4) return 1;
+  const int64_t dx0 = dom[0], dx1 = dom[0] + dom[1], dy0 = dom[2], dy1 = dom[2] + dom[3];
+  for (int k = 0; k < n_rect; ++k) {
+    const int64_t x0 = rects[4 * k], nx = rects[4 * k + 1], y0 = rects[4 * k + 2], ny = rects[4 * k + 3];
+    if (nx <= 0 || ny <= 0) continue;
+    // u(t+1) on the rect + 1 ring (same rule as the GPU kernel), then u(t+2)
+    const int64_t bw = nx + 2, bh = ny + 2;
+    std::vector<double> b(static_cast<size_t>(bw * bh));
+    for (int64_t j = 0; j < bh; ++j)
+      for (int64_t i = 0; i < bw; ++i) {
+        const int64_t x = x0 - 1 + i, y = y0 - 1 + j;
+        const bool rx = (x >= dx0 && x < dx1) || (x < dx0 ? (mask & 1) : (mask & 2));
+        const bool ry = (y >= dy0 && y < dy1) || (y < dy0 ? (mask & 4) : (mask & 8));
+        const double* p = u + y * ld + x;
+        b[j * bw + i] = (rx && ry) ? 0.25 * ((p[-1] + p[1]) + (p[-ld] + p[ld])) : p[0];
+      }
+    for (int64_t j = 1; j <= ny; ++j)
+      for (int64_t i = 1; i <= nx; ++i) {
+        const double* c = &b[j * bw + i];
+        un[(y0 - 1 + j) * ld + x0 - 1 + i] = 0.25 * ((c[-1] + c[1]) + (c[-bw] + c[bw]));
+      }
+  }
+  return 0;
+}
+
 void gmt_jacobi5_set_variant(int v) { g_variant = v; }
 int gmt_jacobi5_get_variant(void) { return g_variant; }
 

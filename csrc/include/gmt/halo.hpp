@@ -35,19 +35,26 @@ class Halo2D {
  public:
   static constexpr int kTagLow = 456, kTagHigh = 123, kTagY = 1000;
 
-  // field: the whole ghosted array, nrows = nx + 2*gx (contiguous), ncols = ny + 2*gy
+  // field: the whole ghosted array, nrows = nx + 2*gx (contiguous), ncols = ny + 2*gy.
+  // corners: two-phase exchange (y faces first, then x faces that include the
+  // freshly received y-ghost rows) so diagonal ghost cells are valid too — the
+  // temporal-blocking kernel (two sweeps per exchange) reads them.
   Halo2D(comm::Transport& t, Span2D<double> field, int gx, int gy, Neighbors nb, bool pack_y,
-         int buf_space)
+         int buf_space, bool corners = false)
       : t_(t), f_(field), gx_(gx), gy_(gy), nb_(nb) {
     nx_ = f_.nrows - 2 * gx;
     ny_ = f_.ncols - 2 * gy;
+    corners_ = corners && gx > 0 && gy > 0 && (nb.west >= 0 || nb.east >= 0) &&
+               (nb.south >= 0 || nb.north >= 0);
+    // x faces span the y ghosts too in corner mode
+    const size_t xrow0 = corners_ ? 0 : gy, xrows = corners_ ? ny_ + 2 * gy : ny_;
     std::vector<comm::Msg> recvs, sends;
     auto x_face = [&](int peer, size_t send_row, size_t recv_row, int send_tag, int recv_tag) {
       Face fc;
-      fc.sbuf = Buffer<double>(static_cast<size_t>(gx) * ny_, buf_space);
-      fc.rbuf = Buffer<double>(static_cast<size_t>(gx) * ny_, buf_space);
-      fc.send = f_.sub(send_row, gx, gy, ny_);
-      fc.recv = f_.sub(recv_row, gx, gy, ny_);
+      fc.sbuf = Buffer<double>(static_cast<size_t>(gx) * xrows, buf_space);
+      fc.rbuf = Buffer<double>(static_cast<size_t>(gx) * xrows, buf_space);
+      fc.send = f_.sub(send_row, gx, xrow0, xrows);
+      fc.recv = f_.sub(recv_row, gx, xrow0, xrows);
       sends.push_back({fc.sbuf.data(), fc.sbuf.bytes(), peer, send_tag});
       recvs.push_back({fc.rbuf.data(), fc.rbuf.bytes(), peer, recv_tag});
       xfaces_.push_back(std::move(fc));
@@ -84,22 +91,48 @@ class Halo2D {
     }
     for (auto& m : sends) bytes_ += m.bytes;
     nmsg_ = sends.size();
-    if (!sends.empty() || !recvs.empty()) ex_ = t_.plan(recvs, sends);
+    if (corners_) {
+      // phase 1 = y faces (the messages after the x faces), phase 2 = x faces
+      const size_t nxm = xfaces_.size();
+      std::vector<comm::Msg> rx(recvs.begin(), recvs.begin() + nxm), sx(sends.begin(), sends.begin() + nxm);
+      std::vector<comm::Msg> ry(recvs.begin() + nxm, recvs.end()), sy(sends.begin() + nxm, sends.end());
+      ex_ = t_.plan(ry, sy);
+      ex_x_ = t_.plan(rx, sx);
+    } else if (!sends.empty() || !recvs.empty()) {
+      ex_ = t_.plan(recvs, sends);
+    }
   }
 
   bool active() const { return ex_ != nullptr; }
+  bool corners() const { return corners_; }
   // the whole exchange is stream-ordered (capturable into a hipGraph)
-  bool capturable() const { return !ex_ || ex_->graph_capturable(); }
+  bool capturable() const {
+    return (!ex_ || ex_->graph_capturable()) && (!ex_x_ || ex_x_->graph_capturable());
+  }
   size_t bytes_sent() const { return bytes_; }
   size_t messages() const { return nmsg_; }
 
   void start(gmt_stream_t s) {
     if (!ex_) return;
+    if (corners_) {  // y faces complete before the x faces (with their corners) are packed
+      pack_y_faces(s);
+      ex_->start(s);
+      ex_->wait(s);
+      unpack_y_faces(s);
+      pack_x_faces(s);
+      ex_x_->start(s);
+      return;
+    }
     pack(s);
     ex_->start(s);
   }
   void finish(gmt_stream_t s) {
     if (!ex_) return;
+    if (corners_) {
+      ex_x_->wait(s);
+      unpack_x_faces(s);
+      return;
+    }
     ex_->wait(s);
     unpack(s);
   }
@@ -121,26 +154,36 @@ class Halo2D {
   };
 
   void pack(gmt_stream_t s) {
-    if (!xfaces_.empty()) {
-      gmt_copy2d_desc d[GMT_MAX_COPY2D];
-      int n = 0;
-      for (auto& fc : xfaces_)
-        d[n++] = {fc.send.data, fc.sbuf.data(), static_cast<int64_t>(fc.send.ld),
-                  static_cast<int64_t>(gx_), gx_, static_cast<int64_t>(ny_)};
-      GMT_CHECK("halo pack", gmt_copy2d_batched(n, d, sizeof(double), s));
-    }
+    pack_x_faces(s);
+    pack_y_faces(s);
+  }
+  void unpack(gmt_stream_t s) {
+    unpack_x_faces(s);
+    unpack_y_faces(s);
+  }
+  void pack_x_faces(gmt_stream_t s) {
+    if (xfaces_.empty()) return;
+    gmt_copy2d_desc d[GMT_MAX_COPY2D];
+    int n = 0;
+    for (auto& fc : xfaces_)
+      d[n++] = {fc.send.data, fc.sbuf.data(), static_cast<int64_t>(fc.send.ld),
+                static_cast<int64_t>(gx_), gx_, static_cast<int64_t>(fc.send.ncols)};
+    GMT_CHECK("halo pack", gmt_copy2d_batched(n, d, sizeof(double), s));
+  }
+  void unpack_x_faces(gmt_stream_t s) {
+    if (xfaces_.empty()) return;
+    gmt_copy2d_desc d[GMT_MAX_COPY2D];
+    int n = 0;
+    for (auto& fc : xfaces_)
+      d[n++] = {fc.rbuf.data(), fc.recv.data, static_cast<int64_t>(gx_),
+                static_cast<int64_t>(fc.recv.ld), gx_, static_cast<int64_t>(fc.recv.ncols)};
+    GMT_CHECK("halo unpack", gmt_copy2d_batched(n, d, sizeof(double), s));
+  }
+  void pack_y_faces(gmt_stream_t s) {
     for (auto& fc : yfaces_)
       GMT_CHECK("halo pack y", gmt_rt_memcpy_async(fc.sbuf.data(), fc.ysrc, fc.ybytes, s));
   }
-  void unpack(gmt_stream_t s) {
-    if (!xfaces_.empty()) {
-      gmt_copy2d_desc d[GMT_MAX_COPY2D];
-      int n = 0;
-      for (auto& fc : xfaces_)
-        d[n++] = {fc.rbuf.data(), fc.recv.data, static_cast<int64_t>(gx_),
-                  static_cast<int64_t>(fc.recv.ld), gx_, static_cast<int64_t>(ny_)};
-      GMT_CHECK("halo unpack", gmt_copy2d_batched(n, d, sizeof(double), s));
-    }
+  void unpack_y_faces(gmt_stream_t s) {
     for (auto& fc : yfaces_)
       GMT_CHECK("halo unpack y", gmt_rt_memcpy_async(fc.ydst, fc.rbuf.data(), fc.ybytes, s));
   }
@@ -151,7 +194,9 @@ class Halo2D {
   size_t nx_ = 0, ny_ = 0;
   Neighbors nb_;
   std::vector<Face> xfaces_, yfaces_;
-  std::unique_ptr<comm::Exchange> ex_;
+  bool corners_ = false;
+  std::unique_ptr<comm::Exchange> ex_;    // all faces, or the y faces in corner mode
+  std::unique_ptr<comm::Exchange> ex_x_;  // x faces in corner mode
   size_t bytes_ = 0, nmsg_ = 0;
 };
 

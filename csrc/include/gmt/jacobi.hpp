@@ -6,7 +6,8 @@
 // against compute (mpi_stencil2d_gt.cc:511-535); this engine is the
 // MI355X-first version of that loop:
 //
-//   * 2-D Cartesian decomposition (py x px ranks), ghost width 1, fp64;
+//   * 2-D Cartesian decomposition (py x px ranks), ghost width 1 (2 with
+//     tblock), fp64;
 //   * one step = halo exchange of u + one Jacobi sweep u -> un + swap;
 //   * overlap: the interior "core" sweep runs on the compute stream while
 //     the halo (fused pack kernel + RCCL/IPC/MPI transfer + unpack) runs on a
@@ -16,6 +17,10 @@
 //     are captured into hipGraphs and replayed — one host call per step, so
 //     small per-GPU domains (strong scaling at 8 GPUs) are not launch-bound.
 //
+//   * tblock: two sweeps per kernel and per exchange (temporal blocking):
+//     u(t) is read once and u(t+2) written once (gmt_jacobi5x2), the halo is
+//     2 wide and exchanged every other sweep, with corners (two-phase
+//     exchange) — bitwise the same result as single sweeps.
 // Storage is column-major (x contiguous) with the interior origin at x = 8
 // so every interior row starts 64-B aligned and the sweep kernels take their
 // 16-B vector path; the row pitch is padded to 64 doubles.
@@ -36,6 +41,11 @@ struct JacobiConfig {
   bool overlap = true;
   bool graph = false;
   int variant = 0;                               // gmt_jacobi5_set_variant
+  // temporal blocking: two sweeps per memory pass (gmt_jacobi5x2) and per
+  // halo exchange (ghost width 2, corners via a two-phase exchange) — half
+  // the HBM bytes and half the messages per lattice update
+  bool tblock = false;
+  int tile_rows = 16;                            // gmt_jacobi5x2 tile height
 };
 
 class JacobiSolver {
@@ -45,10 +55,8 @@ class JacobiSolver {
   JacobiSolver(const JacobiSolver&) = delete;
   JacobiSolver& operator=(const JacobiSolver&) = delete;
 
-  void step();  // asynchronous (compute stream)
-  void run(int k) {
-    for (int i = 0; i < k; ++i) step();
-  }
+  void step();  // one sweep, asynchronous (compute stream)
+  void run(int k);  // k sweeps: pairs through the fused kernel when tblock
   void synchronize();
   // sqrt(global sum (u_{k+1} - u_k)^2) of one extra sweep (advances the solution)
   double residual();
@@ -63,27 +71,34 @@ class JacobiSolver {
   int64_t off_y() const { return oy_; }
   size_t bytes_per_exchange() const { return halo_[0] ? halo_[0]->bytes_sent() : 0; }
   size_t messages() const { return halo_[0] ? halo_[0]->messages() : 0; }
-  bool graph_active() const { return graph_[0] != nullptr; }
+  bool graph_active() const { return graph_[0] != nullptr || graph2_[0] != nullptr; }
+  bool tblock() const { return cfg_.tblock; }
+  int ghost() const { return g_; }
   bool overlap_active() const { return cfg_.overlap && halo_[0] && halo_[0]->active(); }
   const Neighbors& neighbors() const { return nb_; }
   gmt_stream_t stream() const { return s_; }
 
  private:
   void enqueue_step(int parity);
+  void enqueue_pair(int parity);
+  void step_pair();
   void sweep_full(int parity, double* resid);
   void capture_graphs();
+  int halo_mask() const;
 
   comm::Transport& t_;
   JacobiConfig cfg_;
   int64_t nx_ = 0, ny_ = 0, ox_ = 0, oy_ = 0;  // local interior + global offset
-  int64_t xo_ = 8, ld_ = 0;                    // interior origin column, row pitch
+  int64_t xo_ = 8, yo_ = 1, ld_ = 0;           // interior origin (absolute), row pitch
+  int g_ = 1;                                  // ghost width
   Neighbors nb_;
   Buffer<double> buf_[2];
   std::unique_ptr<Halo2D> halo_[2];
   Buffer<double> resid_ws_;
   gmt_stream_t s_ = nullptr, cs_ = nullptr;
   gmt_event_t ev_start_ = nullptr, ev_halo_ = nullptr;
-  gmt_graph_t graph_[2] = {nullptr, nullptr};
+  gmt_graph_t graph_[2] = {nullptr, nullptr};   // single sweep, per parity
+  gmt_graph_t graph2_[2] = {nullptr, nullptr};  // fused sweep pair, per parity
   int parity_ = 0;  // buf_[parity_] holds the current u
 };
 

@@ -100,6 +100,16 @@ int gmt_jacobi5(int64_t x0, int64_t nx, int64_t y0, int64_t ny, const double* u,
 int gmt_jacobi5_rects(int n_rect, const int64_t* rects, const double* u, double* un,
                       int64_t ld, const double* f, int64_t ldf, double c0, double c1,
                       void* stream);
+/* Two fused Jacobi sweeps (temporal blocking, Laplace form c0 = 1/4):
+ * un = J(J(u)) on up to 4 output rects {x0, nx, y0, ny} (absolute array
+ * coordinates, x0 even) in one launch.  dom = the rank's interior
+ * {x0, nx, y0, ny}.  halo_mask bit0/1/2/3 = west/east/south/north ghost cells
+ * belong to a neighbour (they get the intermediate update); a clear bit means
+ * a fixed Dirichlet ghost.  u must be valid on each rect + 2 cells.
+ * tile_rows: 8, 16 (default) or 32 output rows per workgroup. */
+int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
+                  const double* u, double* un, int64_t ld, int tile_rows, void* stream);
+
 /* Kernel variant selection for A/B measurement: 0 = auto, 1 = register
  * sliding window (vector x2, W/E from L1), 2 = LDS-tiled, 3 = scalar
  * reference kernel, 4-8 = register window with lane-exchanged W/E

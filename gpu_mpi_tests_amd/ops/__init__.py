@@ -13,6 +13,7 @@ from .kernels import (  # noqa: F401
     fill_poly,
     jacobi5,
     jacobi5_rects,
+    jacobi5x2,
     set_jacobi_variant,
     stencil5_1d,
     stencil5_2d,

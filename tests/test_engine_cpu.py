@@ -20,7 +20,8 @@ from gpu_mpi_tests_amd import engine
 from gpu_mpi_tests_amd.parallel import dist as gd
 env = gd.init(device="cpu")
 ny, nx, steps, periodic, overlap = {ny}, {nx}, {steps}, {periodic}, {overlap}
-e = engine.NativeJacobi(ny, nx, env, periodic=periodic, overlap=overlap, graph=True)
+e = engine.NativeJacobi(ny, nx, env, periodic=periodic, overlap=overlap, graph=True,
+                        tblock={tblock})
 e.run(steps); e.synchronize()
 got = e.interior()
 ref = engine.serial_jacobi(ny, nx, steps, periodic)
@@ -32,9 +33,9 @@ e.close()
 """
 
 
-def _run(**kw):
+def _run(tblock=False, **kw):
     ensure_host_build()
-    code = CODE.format(root=ROOT, **kw)
+    code = CODE.format(root=ROOT, tblock=tblock, **kw)
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
                        env=dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES=""))
     assert p.returncode == 0, p.stdout + p.stderr
@@ -57,3 +58,10 @@ def test_native_engine_matches_numpy(ny, nx, steps, periodic):
 def test_native_engine_serial_mode():
     r = _run(ny=40, nx=41, steps=6, periodic=True, overlap=False)
     assert r["diff"] < 1e-13 and r["overlap"] is False
+
+
+@pytest.mark.parametrize("steps", [6, 7])
+@pytest.mark.parametrize("periodic", [False, True])
+def test_native_engine_temporal_blocking(steps, periodic):
+    r = _run(ny=41, nx=66, steps=steps, periodic=periodic, overlap=True, tblock=True)
+    assert r["diff"] < 1e-13

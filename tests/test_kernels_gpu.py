@@ -275,3 +275,35 @@ def test_stream_semantics():
         ops.daxpy(2.0, x, y)
     s.synchronize()
     assert torch.equal(y, exp)
+
+
+@pytest.mark.parametrize("tile_rows", [8, 16, 32])
+@pytest.mark.parametrize("ny,nx", [(1, 2), (5, 7), (17, 130), (40, 256), (70, 515), (129, 1024)])
+@pytest.mark.parametrize("mask", [0, 15, 5, 10])
+def test_jacobi5x2_fused_two_sweeps(tile_rows, ny, nx, mask):
+    """Temporal blocking: bitwise equal to the fp64 two-sweep reference, incl.
+    partial tiles, odd widths and every ghost-side ownership pattern."""
+    g, xo = 2, 8
+    u = _rand(ny + 2 * g, xo + nx + 8, seed=51)
+    dom = (xo, nx, g, ny)
+    un = torch.zeros_like(u)
+    ops.jacobi5x2(u, un, [(xo, nx, g, ny)], dom, mask, tile_rows)
+    exp = torch.zeros(u.shape, dtype=torch.float64)
+    ref.jacobi5x2(u.cpu(), exp, [(xo, nx, g, ny)], dom, mask)
+    torch.cuda.synchronize()
+    assert torch.equal(un[g:g + ny, xo:xo + nx].cpu(), exp[g:g + ny, xo:xo + nx])
+
+
+def test_jacobi5x2_frame_rects_match_full():
+    """core + 4 frame rects in two launches == one full-interior launch."""
+    g, xo, ny, nx = 2, 8, 64, 300
+    u = _rand(ny + 2 * g, xo + nx + 8, seed=52)
+    dom = (xo, nx, g, ny)
+    full = torch.zeros_like(u)
+    ops.jacobi5x2(u, full, [dom], dom, 15)
+    split = torch.zeros_like(u)
+    ops.jacobi5x2(u, split, [(xo + 2, nx - 4, g + 2, ny - 4)], dom, 15)
+    ops.jacobi5x2(u, split, [(xo, nx, g, 2), (xo, nx, g + ny - 2, 2), (xo, 2, g + 2, ny - 4),
+                             (xo + nx - 2, 2, g + 2, ny - 4)], dom, 15)
+    torch.cuda.synchronize()
+    assert torch.equal(split[g:g + ny, xo:xo + nx], full[g:g + ny, xo:xo + nx])

@@ -191,6 +191,15 @@ def test_mpi_stencil2d_sycl_oo_strong_scaling_and_debug():
     (["41", "7", "--dims=2x2", "--periodic"], 4),
     (["41", "7", "--dims=1x3", "--transport=mpi-host"], 3),
     (["21", "5", "--weak", "--periodic", "--transport=ipc"], 3),
+    # temporal blocking: 2 sweeps per pass, 2-wide halos, corners (two-phase exchange)
+    (["64", "10", "--tblock"], 1),
+    (["37", "9", "--tblock", "--periodic"], 1),
+    (["50", "10", "--tblock", "--transport=ipc"], 2),
+    (["51", "9", "--tblock", "--periodic", "--transport=mpi-host"], 2),
+    (["60", "10", "--tblock", "--dims=2x2"], 4),
+    (["61", "11", "--tblock", "--dims=2x2", "--periodic", "--transport=ipc"], 4),
+    (["45", "8", "--tblock=8", "--dims=2x3", "--periodic"], 6),
+    (["45", "8", "--tblock=32", "--dims=1x3", "--no-overlap"], 3),
 ])
 def test_mpi_jacobi2d_matches_serial(args, np_):
     out = run_app("mpi_jacobi2d", *args, "--check", "--warmup=2", "--halo-iters=3", np=np_).stdout
