@@ -10,12 +10,16 @@ exchange/interior overlap".  The global domain is FIXED at 32768² for every N
 carries the single-GPU-per-rank DAXPY bandwidth (BASELINE config "daxpy
 N=2^28 fp64 on one MI355X") and the measured halo-exchange latency.
 
-One step = halo exchange of u (RCCL over xGMI on a high-priority stream,
-overlapped with the interior sweep) + one full Jacobi sweep of the global
-domain + swap.  The step loop runs in the native engine (C++ + hipGraph
-replay, ``csrc/engine/jacobi.cpp``); ``--engine torch`` runs the same
-algorithm through torch.distributed P2P from Python instead.  Nothing is
-skipped inside the timed region.
+One step = one full Jacobi sweep of the global domain (every point updated
+once).  The native engine (C++ + hipGraph replay, ``csrc/engine/jacobi.cpp``)
+runs the steps in pairs by default (temporal blocking, ``--tblock on``): one
+2-wide halo exchange (RCCL over xGMI on a high-priority stream, overlapped
+with the interior update) and one fused kernel that reads u(t) once and
+writes u(t+2) once — bitwise the same result as two single sweeps, half the
+HBM bytes.  ``--tblock off`` runs one exchange + one sweep per step;
+``--engine torch`` runs the single-sweep algorithm through torch.distributed
+P2P from Python.  Nothing is skipped inside the timed region: K steps are K
+sweeps of every lattice point (an odd K ends with one single sweep).
 
 Launch (driver contract):
     python bench.py --gpus 1 --steps K --warmup W
@@ -58,12 +62,13 @@ def _timed(env, fn_run, fn_sync, steps, warmup):
     return gdist.allreduce_max(dt, env)
 
 
-def bench_native(env, n, steps, warmup, overlap, dims, graph, variant):
+def bench_native(env, n, steps, warmup, overlap, dims, graph, variant, tblock):
     from gpu_mpi_tests_amd.engine import NativeJacobi
 
-    eng = NativeJacobi(n, n, env, dims=dims, overlap=overlap, graph=graph, variant=variant)
+    eng = NativeJacobi(n, n, env, dims=dims, overlap=overlap, graph=graph, variant=variant,
+                       tblock=tblock)
     dt = _timed(env, eng.run, eng.synchronize, steps, warmup)
-    info = {"engine": "native", "graph": eng.graph, "overlap": eng.overlap,
+    info = {"engine": "native", "graph": eng.graph, "overlap": eng.overlap, "tblock": eng.tblock,
             "transport": eng.transport if env.world_size > 1 else "none",
             "halo_bytes_per_rank": eng.halo_bytes, "dims": (eng.py, eng.px)}
     return eng, dt, info
@@ -75,7 +80,7 @@ def bench_torch(env, n, steps, warmup, overlap, dims):
     solver = Jacobi2D(n, n, env=env, dims=dims, overlap=overlap)
     dt = _timed(env, solver.run, lambda: _sync(env), steps, warmup)
     ex = solver.ex[id(solver.u)]
-    info = {"engine": "torch", "graph": False, "overlap": overlap,
+    info = {"engine": "torch", "graph": False, "overlap": overlap, "tblock": False,
             "transport": env.backend if env.world_size > 1 else "none",
             "halo_bytes_per_rank": ex.bytes_per_exchange() if ex.active else 0,
             "dims": (solver.decomp.py, solver.decomp.px)}
@@ -137,6 +142,9 @@ def main(argv=None):
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="hipGraph replay of the step (auto: on for 1 GPU; eager RCCL steps "
                          "for N>1, where a step is >100 us of GPU work and launches hide)")
+    ap.add_argument("--tblock", choices=("on", "off"), default="on",
+                    help="temporal blocking (native engine): two sweeps per memory pass and per "
+                         "2-wide halo exchange; bitwise the same result as single sweeps")
     ap.add_argument("--dims", type=str, default=None, help="process grid PYxPX, e.g. 4x2")
     ap.add_argument("--daxpy-n", type=int, default=1 << 28)
     ap.add_argument("--skip-extras", action="store_true", help="headline stencil only")
@@ -155,7 +163,7 @@ def main(argv=None):
     graph = args.graph == "on" or (args.graph == "auto" and env.world_size == 1)
     if engine == "native":
         solver, dt, info = bench_native(env, args.size, args.steps, args.warmup, overlap, dims,
-                                        graph, args.variant)
+                                        graph, args.variant, args.tblock == "on")
     else:
         if env.is_gpu and args.variant:
             ops.set_jacobi_variant(args.variant)
@@ -202,6 +210,7 @@ def main(argv=None):
                                f"{'overlap' if info['overlap'] else 'serial'}",
                 "engine": info["engine"],
                 "hipgraph": info["graph"],
+                "temporal_blocking": info["tblock"],
                 "transport": info["transport"],
                 "halo_bytes_per_rank": info["halo_bytes_per_rank"],
                 "device": str(env.device),

@@ -98,13 +98,15 @@ int main(int argc, char** argv) {
       GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, a.data(), ld2, s));
       GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, b.data(), ld2, s));
       const int64_t rect[4] = {xo, n, g, n};
-      for (int ty : {8, 16, 32}) {
+      const int tiles[][2] = {{64, 4}, {64, 8}, {64, 16}, {128, 4}, {128, 8}, {128, 16}, {256, 4}, {256, 8}};
+      for (auto& t : tiles) {
+        const int tile = (t[0] << 16) | t[1];
         const double ms = time_ms(s, iters, [&] {
-          GMT_CHECK("x2", gmt_jacobi5x2(1, rect, rect, 0, a.data(), b.data(), ld2, ty, s));
+          GMT_CHECK("x2", gmt_jacobi5x2(1, rect, rect, 0, a.data(), b.data(), ld2, tile, s));
         });
         char tag[64];
-        std::snprintf(tag, sizeof(tag), "%s x2 ty=%d", shape, ty);
-        report("jacobi5x2", ty, tag, ms, 2 * 16.0 * n * n);
+        std::snprintf(tag, sizeof(tag), "%s x2 %dx%d", shape, t[0], t[1]);
+        report("jacobi5x2", t[1], tag, ms, 2 * 16.0 * n * n);
       }
     }
   }

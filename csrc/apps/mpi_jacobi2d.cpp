@@ -13,7 +13,7 @@
 //   --transport=auto|rccl|ipc|mpi-host|mpi-direct
 //   --no-overlap --graph --periodic --warmup=W --variant=V (1 reg, 2 lds, 3 scalar, 9 pt)
 //   --tblock[=TY]           temporal blocking: 2 sweeps per pass and per exchange
-//                           (gmt_jacobi5x2, tile of 128 x TY, TY = 8|16|32)
+//                           (gmt_jacobi5x2; --tblock=TXxTY picks the tile, default 128x8)
 //   --halo-iters=K          K blocking halo exchanges -> latency line
 //   --check                 rank 0 re-runs the whole problem serially on the host
 //   --json=FILE
@@ -99,7 +99,15 @@ int main(int argc, char** argv) {
   c.graph = cli.flag("graph");
   c.variant = static_cast<int>(cli.geti("variant", 0));
   c.tblock = cli.has("tblock") && cli.get("tblock", "1") != "0";
-  if (c.tblock && cli.get("tblock", "1") != "1") c.tile_rows = std::atoi(cli.get("tblock", "16").c_str());
+  if (c.tblock && cli.get("tblock", "1") != "1") {
+    int tx = 128, ty = 8;  // --tblock=TY or --tblock=TXxTY
+    const std::string v = cli.get("tblock", "8");
+    if (std::sscanf(v.c_str(), "%dx%d", &tx, &ty) != 2) {
+      tx = 128;
+      ty = std::atoi(v.c_str());
+    }
+    c.tile = (tx << 16) | ty;
+  }
   // with one rank and no periodic wrap there is nothing to exchange; with a
   // periodic wrap a single rank exchanges with itself
   comm::Kind kind = comm::parse_kind(cli.get("transport", "auto"));

@@ -141,7 +141,7 @@ void JacobiSolver::enqueue_pair(int parity) {
   double* un = buf_[parity ^ 1].data();
   const int64_t dom[4] = {xo_, nx_, yo_, ny_};
   const int mask = halo_mask();
-  const int tr = cfg_.tile_rows;
+  const int tr = cfg_.tile;
   if (!h.active()) {
     GMT_CHECK("jacobi x2", gmt_jacobi5x2(1, dom, dom, mask, u, un, ld_, tr, s_));
     return;

@@ -45,7 +45,7 @@ struct JacobiConfig {
   // halo exchange (ghost width 2, corners via a two-phase exchange) — half
   // the HBM bytes and half the messages per lattice update
   bool tblock = false;
-  int tile_rows = 16;                            // gmt_jacobi5x2 tile height
+  int tile = 0;                                  // gmt_jacobi5x2 tile ((TX<<16)|TY, 0 = default)
 };
 
 class JacobiSolver {

@@ -106,9 +106,10 @@ int gmt_jacobi5_rects(int n_rect, const int64_t* rects, const double* u, double*
  * {x0, nx, y0, ny}.  halo_mask bit0/1/2/3 = west/east/south/north ghost cells
  * belong to a neighbour (they get the intermediate update); a clear bit means
  * a fixed Dirichlet ghost.  u must be valid on each rect + 2 cells.
- * tile_rows: 8, 16 (default) or 32 output rows per workgroup. */
+ * tile: (TX << 16) | TY output tile per workgroup (64x4..16, 128x4..32,
+ * 256x4..8); a plain row count means 128 columns; 0 = default (128 x 8). */
 int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
-                  const double* u, double* un, int64_t ld, int tile_rows, void* stream);
+                  const double* u, double* un, int64_t ld, int tile, void* stream);
 
 /* Kernel variant selection for A/B measurement: 0 = auto, 1 = register
  * sliding window (vector x2, W/E from L1), 2 = LDS-tiled, 3 = scalar

@@ -23,8 +23,6 @@
 
 namespace gmt {
 
-constexpr int X2_TX = 128;  // output columns per tile
-
 struct X2Args {
   int64_t r[4][4];       // output rects: x0, nx, y0, ny (absolute array coordinates)
   int64_t ntx[4];        // tiles per rect row
@@ -34,11 +32,11 @@ struct X2Args {
   int mask;              // bit0 west, bit1 east, bit2 south, bit3 north: ghost cells are real
 };
 
-template <int TY>
+template <int X2_TX, int TY>
 __global__ __launch_bounds__(kBlock) void jacobi5x2_kernel(X2Args a, const double* __restrict__ u,
                                                            double* __restrict__ un, int64_t ld,
                                                            int64_t nblocks) {
-  constexpr int AP = X2_TX + 4;  // LDS row pitch (doubles): 264 dwords, conflict-free rows
+  constexpr int AP = X2_TX + 4;  // LDS row pitch (doubles)
   constexpr int AR = TY + 4;
   __shared__ __attribute__((aligned(16))) double A[AR * AP];
   __shared__ __attribute__((aligned(16))) double B[AR * AP];
@@ -106,12 +104,34 @@ __global__ __launch_bounds__(kBlock) void jacobi5x2_kernel(X2Args a, const doubl
 
 }  // namespace gmt
 
+namespace gmt {
+// tile = (TX << 16) | TY; 0 = default.  Measured (8192^2, 1x MI355X): 128x8
+// 0.306 ms, 128x16 0.389, 128x32 0.456 — short tiles win on occupancy (LDS).
+struct X2Tile {
+  int tx, ty;
+};
+static X2Tile x2_tile(int tile) {
+  X2Tile t{128, 8};
+  if (tile > 0) {
+    t.tx = tile >> 16;
+    t.ty = tile & 0xffff;
+    if (tile < 0x10000) t.tx = 128;  // plain row count: 128-column tiles
+  }
+  const bool ok = (t.tx == 64 && (t.ty == 4 || t.ty == 8 || t.ty == 16)) ||
+                  (t.tx == 128 && (t.ty == 4 || t.ty == 8 || t.ty == 16 || t.ty == 32)) ||
+                  (t.tx == 256 && (t.ty == 4 || t.ty == 8));
+  if (!ok) t = {128, 8};
+  return t;
+}
+}  // namespace gmt
+
 extern "C" int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
-                             const double* u, double* un, int64_t ld, int tile_rows, void* stream) {
+                             const double* u, double* un, int64_t ld, int tile, void* stream) {
   using namespace gmt;
   if (n_rect < 0 || n_rect > 4) return static_cast<int>(hipErrorInvalidValue);
   if (!aligned16(u) || !aligned16(un) || (ld % 2) != 0) return static_cast<int>(hipErrorInvalidValue);
-  const int ty = tile_rows == 8 || tile_rows == 32 ? tile_rows : 16;
+  const X2Tile tl = x2_tile(tile);
+  const int ty = tl.ty, X2_TX = tl.tx;
   X2Args a{};
   a.n = 0;
   a.tstart[0] = 0;
@@ -130,10 +150,12 @@ extern "C" int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* do
   for (int k = a.n + 1; k <= 4; ++k) a.tstart[k] = a.tstart[a.n];
   const int64_t nb = a.tstart[a.n];
   hipStream_t s = static_cast<hipStream_t>(stream);
-  switch (ty) {
-    case 8: jacobi5x2_kernel<8><<<grid_1d(nb), kBlock, 0, s>>>(a, u, un, ld, nb); break;
-    case 32: jacobi5x2_kernel<32><<<grid_1d(nb), kBlock, 0, s>>>(a, u, un, ld, nb); break;
-    default: jacobi5x2_kernel<16><<<grid_1d(nb), kBlock, 0, s>>>(a, u, un, ld, nb); break;
-  }
+  const unsigned g = grid_1d(nb);
+#define GMT_X2(TX, TY) \
+  if (X2_TX == TX && ty == TY) jacobi5x2_kernel<TX, TY><<<g, kBlock, 0, s>>>(a, u, un, ld, nb)
+  GMT_X2(64, 4); else GMT_X2(64, 8); else GMT_X2(64, 16);
+  else GMT_X2(128, 4); else GMT_X2(128, 8); else GMT_X2(128, 16); else GMT_X2(128, 32);
+  else GMT_X2(256, 4); else GMT_X2(256, 8);
+#undef GMT_X2
   GMT_RET_LAUNCH();
 }
