@@ -13,7 +13,7 @@
 //   --transport=auto|rccl|ipc|mpi-host|mpi-direct
 //   --no-overlap --graph --periodic --warmup=W --variant=V (1 reg, 2 lds, 3 scalar, 9 pt)
 //   --tblock[=TY]           temporal blocking: 2 sweeps per pass and per exchange
-//                           (gmt_jacobi5x2; --tblock=TXxTY picks the tile, default 128x8)
+//                           (gmt_jacobi5x2; --tblock=TXxTY picks the tile, default 64x16)
 //   --halo-iters=K          K blocking halo exchanges -> latency line
 //   --check                 rank 0 re-runs the whole problem serially on the host
 //   --json=FILE
@@ -100,8 +100,8 @@ int main(int argc, char** argv) {
   c.variant = static_cast<int>(cli.geti("variant", 0));
   c.tblock = cli.has("tblock") && cli.get("tblock", "1") != "0";
   if (c.tblock && cli.get("tblock", "1") != "1") {
-    int tx = 128, ty = 8;  // --tblock=TY or --tblock=TXxTY
-    const std::string v = cli.get("tblock", "8");
+    int tx = 64, ty = 16;  // --tblock=TY (128-column tiles) or --tblock=TXxTY
+    const std::string v = cli.get("tblock", "16");
     if (std::sscanf(v.c_str(), "%dx%d", &tx, &ty) != 2) {
       tx = 128;
       ty = std::atoi(v.c_str());

@@ -41,7 +41,8 @@ int gmt_stencil5_2d(int dim, int64_t nx_out, int64_t ny_out, const double* coef5
                     double scale, const double* in, int64_t ld_in, double* out,
                     int64_t ld_out, void* stream);
 
-/* 0/2 = per-thread kernels (default), 1 = register-window kernels (A/B) */
+/* 0 = default (per-thread dim 0, register window dim 1), 1 = register-window
+ * kernels, 2 = per-thread kernels (A/B) */
 void gmt_stencil5_set_variant(int variant);
 
 /* ---- K6/K7/K8: batched strided 2-D copy (halo pack / unpack, fused L+R).
@@ -106,8 +107,9 @@ int gmt_jacobi5_rects(int n_rect, const int64_t* rects, const double* u, double*
  * {x0, nx, y0, ny}.  halo_mask bit0/1/2/3 = west/east/south/north ghost cells
  * belong to a neighbour (they get the intermediate update); a clear bit means
  * a fixed Dirichlet ghost.  u must be valid on each rect + 2 cells.
- * tile: (TX << 16) | TY output tile per workgroup (64x4..16, 128x4..32,
- * 256x4..8); a plain row count means 128 columns; 0 = default (128 x 8). */
+ * tile: (TX << 16) | TY output tile per workgroup (32x16/32, 64x4..32,
+ * 128x4..32, 256x4..8); a plain row count means 128 columns; 0 = default
+ * (64 x 16, the measured best). */
 int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
                   const double* u, double* un, int64_t ld, int tile, void* stream);
 

@@ -105,22 +105,26 @@ __global__ __launch_bounds__(kBlock) void jacobi5x2_kernel(X2Args a, const doubl
 }  // namespace gmt
 
 namespace gmt {
-// tile = (TX << 16) | TY; 0 = default.  Measured (8192^2, 1x MI355X): 128x8
-// 0.306 ms, 128x16 0.389, 128x32 0.456 — short tiles win on occupancy (LDS).
+// tile = (TX << 16) | TY; 0 = default.  Measured on 1x MI355X, two sweeps of
+// 32768^2 (profiles/r01_x2_tiles.md): 64x16 3.77 ms, 128x8 4.50, 64x8 4.67,
+// 128x4 5.31, 128x16 6.06, 256x8 6.37, 64x4 7.30 — the LDS footprint (two
+// (TY+4) x (TX+4) fp64 tiles) sets the workgroups per CU, the ring sets the
+// redundant loads: 64 x 16 balances both (22 KB, 7 workgroups per CU).
 struct X2Tile {
   int tx, ty;
 };
 static X2Tile x2_tile(int tile) {
-  X2Tile t{128, 8};
+  X2Tile t{64, 16};
   if (tile > 0) {
     t.tx = tile >> 16;
     t.ty = tile & 0xffff;
     if (tile < 0x10000) t.tx = 128;  // plain row count: 128-column tiles
   }
-  const bool ok = (t.tx == 64 && (t.ty == 4 || t.ty == 8 || t.ty == 16)) ||
+  const bool ok = (t.tx == 32 && (t.ty == 16 || t.ty == 32)) ||
+                  (t.tx == 64 && (t.ty == 4 || t.ty == 8 || t.ty == 16 || t.ty == 24 || t.ty == 32)) ||
                   (t.tx == 128 && (t.ty == 4 || t.ty == 8 || t.ty == 16 || t.ty == 32)) ||
                   (t.tx == 256 && (t.ty == 4 || t.ty == 8));
-  if (!ok) t = {128, 8};
+  if (!ok) t = {64, 16};
   return t;
 }
 }  // namespace gmt
@@ -153,7 +157,8 @@ extern "C" int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* do
   const unsigned g = grid_1d(nb);
 #define GMT_X2(TX, TY) \
   if (X2_TX == TX && ty == TY) jacobi5x2_kernel<TX, TY><<<g, kBlock, 0, s>>>(a, u, un, ld, nb)
-  GMT_X2(64, 4); else GMT_X2(64, 8); else GMT_X2(64, 16);
+  GMT_X2(32, 16); else GMT_X2(32, 32);
+  else GMT_X2(64, 4); else GMT_X2(64, 8); else GMT_X2(64, 16); else GMT_X2(64, 24); else GMT_X2(64, 32);
   else GMT_X2(128, 4); else GMT_X2(128, 8); else GMT_X2(128, 16); else GMT_X2(128, 32);
   else GMT_X2(256, 4); else GMT_X2(256, 8);
 #undef GMT_X2

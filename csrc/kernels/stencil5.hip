@@ -82,13 +82,13 @@ __global__ __launch_bounds__(kBlock) void stencil5_d1_vec(int64_t nx, int64_t ny
 #pragma unroll 8
       for (int r = 0; r < ROWS1; ++r) {
         const d2 w4 = ld2(p + (r + 4) * ld_in);
-        st2(q + r * ld_out, c0 * w0 + c1 * w1 + c2 * w2 + c3 * w3 + c4 * w4);
+        st2_nt(q + r * ld_out, c0 * w0 + c1 * w1 + c2 * w2 + c3 * w3 + c4 * w4);
         w0 = w1; w1 = w2; w2 = w3; w3 = w4;
       }
     } else {
       for (int64_t r = 0; r < nrows; ++r) {
         const d2 w4 = ld2(p + (r + 4) * ld_in);
-        st2(q + r * ld_out, c0 * w0 + c1 * w1 + c2 * w2 + c3 * w3 + c4 * w4);
+        st2_nt(q + r * ld_out, c0 * w0 + c1 * w1 + c2 * w2 + c3 * w3 + c4 * w4);
         w0 = w1; w1 = w2; w2 = w3; w3 = w4;
       }
     }
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(kBlock) void stencil5_d1_vec(int64_t nx, int64_t ny
   }
 }
 
-// Default kernels (variant 2): one output pair per thread, 64 x 4 threads per
+// Per-thread kernels (variant 2; default for dim 0): one output pair per thread, 64 x 4 threads per
 // block (128 columns x 4 rows), XCD-swizzled so the tiles that share input
 // rows sit on one XCD's L2, nontemporal stores (the derivative is written
 // once and not re-read by this kernel).  Same structure as the measured
@@ -176,7 +176,11 @@ extern "C" int gmt_stencil5_2d(int dim, int64_t nx_out, int64_t ny_out, const do
   hipStream_t s = static_cast<hipStream_t>(stream);
   const Coef5 cf = make_coef(coef5);
   const bool vec_ok = aligned16(in) && aligned16(out) && (ld_in % 2 == 0) && (ld_out % 2 == 0);
-  if (vec_ok && g_stencil_variant != 1) {
+  // default: per-thread kernel for dim 0 (taps along the contiguous axis,
+  // 6.34 TB/s), register window for dim 1 (a 5-row window per lane beats
+  // five L2-served row loads per thread: 1.87 vs 2.05 ms at 1024 x 524288)
+  const bool pt = g_stencil_variant == 2 || (g_stencil_variant == 0 && dim == 0);
+  if (vec_ok && pt) {
     const int64_t nbx = (nx_out + 2 * kWave - 1) / (2 * kWave);
     const int64_t nb = nbx * ((ny_out + kBlock / kWave - 1) / (kBlock / kWave));
     if (dim == 0)

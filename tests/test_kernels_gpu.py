@@ -277,8 +277,8 @@ def test_stream_semantics():
     assert torch.equal(y, exp)
 
 
-@pytest.mark.parametrize("tile_rows", [8, 16, 32, (64 << 16) | 4, (64 << 16) | 16, (128 << 16) | 4,
-                                       (256 << 16) | 8])
+@pytest.mark.parametrize("tile_rows", [0, 8, 16, 32, (64 << 16) | 4, (64 << 16) | 16, (128 << 16) | 4,
+                                       (256 << 16) | 8, (32 << 16) | 32, (64 << 16) | 24])
 @pytest.mark.parametrize("ny,nx", [(1, 2), (5, 7), (17, 130), (40, 256), (70, 515), (129, 1024)])
 @pytest.mark.parametrize("mask", [0, 15, 5, 10])
 def test_jacobi5x2_fused_two_sweeps(tile_rows, ny, nx, mask):
