@@ -89,10 +89,10 @@ int main(int argc, char** argv) {
       report("jacobi5", v, shape, ms, 16.0 * n * n);
     }
     gmt_jacobi5_set_variant(0);
-    // temporal blocking: two sweeps per call; "GB/s" is the single-sweep
-    // equivalent (2 x 16 B per point), i.e. directly comparable with v1-v9
-    {
-      const int64_t g = 2;
+    // temporal blocking: K sweeps per call; "GB/s" is the single-sweep
+    // equivalent (K x 16 B per point), i.e. directly comparable with v1-v9
+    for (int K = 2; K <= 4; ++K) {
+      const int64_t g = K;
       const int64_t ld2 = ((xo + n + g + 63) / 64) * 64;
       Buffer<double> a(static_cast<size_t>(ld2) * (n + 2 * g), GMT_SPACE_DEVICE), b(a.size(), GMT_SPACE_DEVICE);
       GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, a.data(), ld2, s));
@@ -102,11 +102,11 @@ int main(int argc, char** argv) {
       for (auto& t : tiles) {
         const int tile = (t[0] << 16) | t[1];
         const double ms = time_ms(s, iters, [&] {
-          GMT_CHECK("x2", gmt_jacobi5x2(1, rect, rect, 0, a.data(), b.data(), ld2, tile, s));
+          GMT_CHECK("xk", gmt_jacobi5xk(K, 1, rect, rect, 0, a.data(), b.data(), ld2, tile, s));
         });
         char tag[64];
-        std::snprintf(tag, sizeof(tag), "%s x2 %dx%d", shape, t[0], t[1]);
-        report("jacobi5x2", t[1], tag, ms, 2 * 16.0 * n * n);
+        std::snprintf(tag, sizeof(tag), "%s x%d %dx%d", shape, K, t[0], t[1]);
+        report("jacobi5xk", K, tag, ms, K * 16.0 * n * n);
       }
     }
   }

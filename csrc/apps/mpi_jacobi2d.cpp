@@ -14,6 +14,7 @@
 //   --no-overlap --graph --periodic --warmup=W --variant=V (1 reg, 2 lds, 3 scalar, 9 pt)
 //   --tblock[=TY]           temporal blocking: 2 sweeps per pass and per exchange
 //                           (gmt_jacobi5x2; --tblock=TXxTY picks the tile, default 64x16)
+//   --tsteps=K              sweeps per fused pass with --tblock (2, 3 or 4; default 2)
 //   --halo-iters=K          K blocking halo exchanges -> latency line
 //   --check                 rank 0 re-runs the whole problem serially on the host
 //   --json=FILE
@@ -99,6 +100,7 @@ int main(int argc, char** argv) {
   c.graph = cli.flag("graph");
   c.variant = static_cast<int>(cli.geti("variant", 0));
   c.tblock = cli.has("tblock") && cli.get("tblock", "1") != "0";
+  if (c.tblock) c.tsteps = static_cast<int>(cli.geti("tsteps", 2));
   if (c.tblock && cli.get("tblock", "1") != "1") {
     int tx = 64, ty = 16;  // --tblock=TY (128-column tiles) or --tblock=TXxTY
     const std::string v = cli.get("tblock", "16");

@@ -46,6 +46,7 @@ void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank,
   c.overlap = (flags & 2) != 0;
   c.graph = (flags & 4) != 0;
   c.tblock = (flags & 8) != 0;
+  c.tsteps = (flags >> 8) & 0xf;  // bits 8-11: sweeps per fused pass (0 = from bit 3)
   c.variant = variant;
   h->py = py;
   h->px = px;
@@ -87,7 +88,7 @@ int gmt_engine_jacobi_info(void* p, int64_t* out) {
   out[7] = s.overlap_active();
   out[8] = h->py;
   out[9] = h->px;
-  out[10] = s.tblock();
+  out[10] = s.tsteps();
   return 0;
 }
 int gmt_engine_jacobi_copy_interior(void* p, double* host) {

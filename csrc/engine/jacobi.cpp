@@ -47,7 +47,9 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   nb_.south = cy > 0 ? at(cy - 1, cx) : (c.periodic ? at(c.py - 1, cx) : -1);
   nb_.north = cy < c.py - 1 ? at(cy + 1, cx) : (c.periodic ? at(0, cx) : -1);
 
-  g_ = c.tblock ? 2 : 1;
+  ks_ = c.tsteps > 1 ? c.tsteps : (c.tblock ? 2 : 1);
+  if (ks_ > 4) ks_ = 4;
+  g_ = ks_;
   yo_ = g_;
   ld_ = round_up(xo_ + nx_ + g_, 64);
   const size_t elems = static_cast<size_t>(ld_) * (ny_ + 2 * g_);
@@ -70,7 +72,7 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   resid_ws_ = Buffer<double>(gmt_jacobi_resid_workspace(nx_, ny_) + 1, GMT_SPACE_DEVICE);
   for (int b = 0; b < 2; ++b) {
     Span2D<double> f(buf_[b].data() + (xo_ - g_), nx_ + 2 * g_, ny_ + 2 * g_, ld_);
-    halo_[b] = std::make_unique<Halo2D>(t_, f, g_, g_, nb_, false, GMT_SPACE_DEVICE, c.tblock);
+    halo_[b] = std::make_unique<Halo2D>(t_, f, g_, g_, nb_, false, GMT_SPACE_DEVICE, ks_ > 1);
   }
   if (c.graph) capture_graphs();
 }
@@ -131,53 +133,54 @@ int JacobiSolver::halo_mask() const {
          (nb_.north >= 0 ? 8 : 0);
 }
 
-// Two sweeps u(t) -> u(t+2) in one pass: the 2-wide halo (corners included)
+// ks_ sweeps u(t) -> u(t+ks) in one pass: the ks-wide halo (corners included)
 // travels on the comm stream while the fused kernel updates the core whose
-// two-step dependency cone stays inside the interior; the 2-wide frame
+// ks-step dependency cone stays inside the interior; the ks-wide frame
 // follows once the halo has landed.
-void JacobiSolver::enqueue_pair(int parity) {
+void JacobiSolver::enqueue_block(int parity) {
   Halo2D& h = *halo_[parity];
   const double* u = buf_[parity].data();
   double* un = buf_[parity ^ 1].data();
   const int64_t dom[4] = {xo_, nx_, yo_, ny_};
   const int mask = halo_mask();
-  const int tr = cfg_.tile;
+  const int tr = cfg_.tile, K = ks_;
+  const int64_t KA = (K + 1) & ~1;  // x offsets stay even (16-B staging)
   if (!h.active()) {
-    GMT_CHECK("jacobi x2", gmt_jacobi5x2(1, dom, dom, mask, u, un, ld_, tr, s_));
+    GMT_CHECK("jacobi xk", gmt_jacobi5xk(K, 1, dom, dom, mask, u, un, ld_, tr, s_));
     return;
   }
-  if (!cfg_.overlap || nx_ < 10 || ny_ < 8) {
+  if (!cfg_.overlap || nx_ < 4 * KA + 2 || ny_ < 4 * K) {
     h.start(s_);
     h.finish(s_);
-    GMT_CHECK("jacobi x2", gmt_jacobi5x2(1, dom, dom, mask, u, un, ld_, tr, s_));
+    GMT_CHECK("jacobi xk", gmt_jacobi5xk(K, 1, dom, dom, mask, u, un, ld_, tr, s_));
     return;
   }
-  // right frame starts at an even column (16-B staging): 2 or 3 columns wide
-  const int64_t xr = (xo_ + nx_ - 2) & ~int64_t(1);
-  const int64_t core[4] = {xo_ + 2, xr - xo_ - 2, yo_ + 2, ny_ - 4};
+  // right frame starts at an even column: KA or KA+1 columns wide
+  const int64_t xr = (xo_ + nx_ - K) & ~int64_t(1);
+  const int64_t core[4] = {xo_ + KA, xr - xo_ - KA, yo_ + K, ny_ - 2 * K};
   GMT_CHECK("event", gmt_rt_event_record(ev_start_, s_));
-  GMT_CHECK("core x2", gmt_jacobi5x2(1, core, dom, mask, u, un, ld_, tr, s_));
+  GMT_CHECK("core xk", gmt_jacobi5xk(K, 1, core, dom, mask, u, un, ld_, tr, s_));
   GMT_CHECK("wait", gmt_rt_stream_wait_event(cs_, ev_start_));
   h.start(cs_);
   h.finish(cs_);
   GMT_CHECK("event", gmt_rt_event_record(ev_halo_, cs_));
   GMT_CHECK("wait", gmt_rt_stream_wait_event(s_, ev_halo_));
-  const int64_t frame[16] = {xo_, nx_,            yo_,           2,        xo_, nx_, yo_ + ny_ - 2, 2,
-                             xo_, 2,              yo_ + 2,       ny_ - 4,  xr,  xo_ + nx_ - xr, yo_ + 2, ny_ - 4};
-  GMT_CHECK("frame x2", gmt_jacobi5x2(4, frame, dom, mask, u, un, ld_, tr, s_));
+  const int64_t frame[16] = {xo_, nx_, yo_,            K,          xo_, nx_,            yo_ + ny_ - K, K,
+                             xo_, KA,  yo_ + K,        ny_ - 2 * K, xr, xo_ + nx_ - xr, yo_ + K,       ny_ - 2 * K};
+  GMT_CHECK("frame xk", gmt_jacobi5xk(K, 4, frame, dom, mask, u, un, ld_, tr, s_));
 }
 
-void JacobiSolver::step_pair() {
+void JacobiSolver::step_block() {
   if (graph2_[parity_])
     GMT_CHECK("graph launch", gmt_rt_graph_launch(graph2_[parity_], s_));
   else
-    enqueue_pair(parity_);
-  parity_ ^= 1;  // u(t+2) lives in the other buffer
+    enqueue_block(parity_);
+  parity_ ^= 1;  // u(t+ks) lives in the other buffer
 }
 
 void JacobiSolver::run(int k) {
-  if (cfg_.tblock)
-    for (; k >= 2; k -= 2) step_pair();
+  if (ks_ > 1)
+    for (; k >= ks_; k -= ks_) step_block();
   for (; k > 0; --k) step();
 }
 
@@ -196,13 +199,13 @@ void JacobiSolver::capture_graphs() {
   }
   GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));
   for (int p = 0; p < 4; ++p) {
-    if (p >= 2 && !cfg_.tblock) break;
+    if (p >= 2 && ks_ < 2) break;
     int e = gmt_rt_stream_begin_capture(s_);
     if (e == 0) {
       if (p < 2)
         enqueue_step(p);
       else
-        enqueue_pair(p - 2);
+        enqueue_block(p - 2);
       e = gmt_rt_stream_end_capture(s_, p < 2 ? &graph_[p] : &graph2_[p - 2]);
     }
     if (e != 0) {

@@ -149,31 +149,47 @@ int gmt_jacobi5_rects(int n_rect, const int64_t* r, const double* u, double* un,
   return 0;
 }
 
-int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int mask, const double* u,
-                  double* un, int64_t ld, int, void*) {
-  if (n_rect < 0 || n_rect > 4) return 1;
+int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom, int mask,
+                  const double* u, double* un, int64_t ld, int, void*) {
+  if (n_rect < 0 || n_rect > 4 || nsweeps < 2 || nsweeps > 4) return 1;
+  const int K = nsweeps;
   const int64_t dx0 = dom[0], dx1 = dom[0] + dom[1], dy0 = dom[2], dy1 = dom[2] + dom[3];
   for (int k = 0; k < n_rect; ++k) {
     const int64_t x0 = rects[4 * k], nx = rects[4 * k + 1], y0 = rects[4 * k + 2], ny = rects[4 * k + 3];
     if (nx <= 0 || ny <= 0) continue;
-    // u(t+1) on the rect + 1 ring (same rule as the GPU kernel), then u(t+2)
-    const int64_t bw = nx + 2, bh = ny + 2;
-    std::vector<double> b(static_cast<size_t>(bw * bh));
+    // level 0 = u on rect + K ring; each level shrinks the ring by one (same
+    // ghost-side rule as the GPU kernel), the last one is written to un
+    const int64_t bw = nx + 2 * K, bh = ny + 2 * K;
+    std::vector<double> cur(static_cast<size_t>(bw * bh)), nxt(cur.size());
     for (int64_t j = 0; j < bh; ++j)
       for (int64_t i = 0; i < bw; ++i) {
-        const int64_t x = x0 - 1 + i, y = y0 - 1 + j;
-        const bool rx = (x >= dx0 && x < dx1) || (x < dx0 ? (mask & 1) : (mask & 2));
-        const bool ry = (y >= dy0 && y < dy1) || (y < dy0 ? (mask & 4) : (mask & 8));
-        const double* p = u + y * ld + x;
-        b[j * bw + i] = (rx && ry) ? 0.25 * ((p[-1] + p[1]) + (p[-ld] + p[ld])) : p[0];
+        const int64_t y = y0 - K + j, x = x0 - K + i;
+        const bool in_ring = y >= dy0 - K && y < dy1 + K && x >= dx0 - K && x < dx1 + K;
+        cur[j * bw + i] = in_ring ? u[y * ld + x] : 0.0;
       }
-    for (int64_t j = 1; j <= ny; ++j)
-      for (int64_t i = 1; i <= nx; ++i) {
-        const double* c = &b[j * bw + i];
-        un[(y0 - 1 + j) * ld + x0 - 1 + i] = 0.25 * ((c[-1] + c[1]) + (c[-bw] + c[bw]));
-      }
+    for (int p = 1; p <= K; ++p) {
+      const int ring = K - p;
+      for (int64_t j = K - ring; j < K + ny + ring; ++j)
+        for (int64_t i = K - ring; i < K + nx + ring; ++i) {
+          const int64_t x = x0 - K + i, y = y0 - K + j;
+          const bool rx = (x >= dx0 && x < dx1) || (x < dx0 ? (mask & 1) : (mask & 2));
+          const bool ry = (y >= dy0 && y < dy1) || (y < dy0 ? (mask & 4) : (mask & 8));
+          const double* c = &cur[j * bw + i];
+          const double v = 0.25 * ((c[-1] + c[1]) + (c[-bw] + c[bw]));
+          if (p == K)
+            un[y * ld + x] = v;
+          else
+            nxt[j * bw + i] = (rx && ry) ? v : c[0];
+        }
+      std::swap(cur, nxt);
+    }
   }
   return 0;
+}
+
+int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int mask, const double* u,
+                  double* un, int64_t ld, int tile, void* stream) {
+  return gmt_jacobi5xk(2, n_rect, rects, dom, mask, u, un, ld, tile, stream);
 }
 
 void gmt_jacobi5_set_variant(int v) { g_variant = v; }

@@ -41,10 +41,12 @@ struct JacobiConfig {
   bool overlap = true;
   bool graph = false;
   int variant = 0;                               // gmt_jacobi5_set_variant
-  // temporal blocking: two sweeps per memory pass (gmt_jacobi5x2) and per
-  // halo exchange (ghost width 2, corners via a two-phase exchange) — half
-  // the HBM bytes and half the messages per lattice update
+  // temporal blocking: tsteps (2-4) sweeps per memory pass (gmt_jacobi5xk)
+  // and per halo exchange (ghost width tsteps, corners via a two-phase
+  // exchange) — 1/tsteps of the HBM bytes and messages per lattice update.
+  // 1 = off.  tblock = true is tsteps = 2.
   bool tblock = false;
+  int tsteps = 0;
   int tile = 0;                                  // gmt_jacobi5x2 tile ((TX<<16)|TY, 0 = default)
 };
 
@@ -72,7 +74,8 @@ class JacobiSolver {
   size_t bytes_per_exchange() const { return halo_[0] ? halo_[0]->bytes_sent() : 0; }
   size_t messages() const { return halo_[0] ? halo_[0]->messages() : 0; }
   bool graph_active() const { return graph_[0] != nullptr || graph2_[0] != nullptr; }
-  bool tblock() const { return cfg_.tblock; }
+  bool tblock() const { return ks_ > 1; }
+  int tsteps() const { return ks_; }
   int ghost() const { return g_; }
   bool overlap_active() const { return cfg_.overlap && halo_[0] && halo_[0]->active(); }
   const Neighbors& neighbors() const { return nb_; }
@@ -80,8 +83,8 @@ class JacobiSolver {
 
  private:
   void enqueue_step(int parity);
-  void enqueue_pair(int parity);
-  void step_pair();
+  void enqueue_block(int parity);
+  void step_block();
   void sweep_full(int parity, double* resid);
   void capture_graphs();
   int halo_mask() const;
@@ -91,6 +94,7 @@ class JacobiSolver {
   int64_t nx_ = 0, ny_ = 0, ox_ = 0, oy_ = 0;  // local interior + global offset
   int64_t xo_ = 8, yo_ = 1, ld_ = 0;           // interior origin (absolute), row pitch
   int g_ = 1;                                  // ghost width
+  int ks_ = 1;                                 // sweeps per fused pass
   Neighbors nb_;
   Buffer<double> buf_[2];
   std::unique_ptr<Halo2D> halo_[2];
@@ -98,7 +102,7 @@ class JacobiSolver {
   gmt_stream_t s_ = nullptr, cs_ = nullptr;
   gmt_event_t ev_start_ = nullptr, ev_halo_ = nullptr;
   gmt_graph_t graph_[2] = {nullptr, nullptr};   // single sweep, per parity
-  gmt_graph_t graph2_[2] = {nullptr, nullptr};  // fused sweep pair, per parity
+  gmt_graph_t graph2_[2] = {nullptr, nullptr};  // fused ks_-sweep block, per parity
   int parity_ = 0;  // buf_[parity_] holds the current u
 };
 

@@ -112,6 +112,10 @@ int gmt_jacobi5_rects(int n_rect, const int64_t* rects, const double* u, double*
  * (64 x 16, the measured best). */
 int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
                   const double* u, double* un, int64_t ld, int tile, void* stream);
+/* The same for nsweeps = 2, 3 or 4 fused sweeps (u valid on rect + nsweeps;
+ * ghost width >= nsweeps).  gmt_jacobi5x2 == gmt_jacobi5xk(2, ...). */
+int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
+                  const double* u, double* un, int64_t ld, int tile, void* stream);
 
 /* Kernel variant selection for A/B measurement: 0 = auto, 1 = register
  * sliding window (vector x2, W/E from L1), 2 = LDS-tiled, 3 = scalar

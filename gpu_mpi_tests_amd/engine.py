@@ -97,7 +97,7 @@ class NativeJacobi:
     def __init__(self, ny: int, nx: int, env: "gdist.DistEnv | None" = None,
                  dims: tuple[int, int] | None = None, periodic: bool = False,
                  overlap: bool = True, graph: bool = True, variant: int = 0,
-                 tblock: bool = False):
+                 tblock: bool | int = False):
         from .parallel.decomp import choose_dims
 
         self.env = env or gdist.get()
@@ -116,8 +116,9 @@ class NativeJacobi:
                                   "use the mpi_jacobi2d app or the torch engine on CPU")
             transport = RCCL
             cid = ctypes.create_string_buffer(_broadcast_unique_id(self.lib, e), 128)
+        ks = 0 if not tblock else (2 if tblock is True else int(tblock))
         flags = ((1 if periodic else 0) | (2 if overlap else 0) | (4 if graph else 0)
-                 | (8 if tblock else 0))
+                 | ((ks & 0xF) << 8))
         self.h = self.lib.gmt_engine_jacobi_create(ny, nx, py, px, e.rank, e.world_size, transport,
                                                    cid, flags, variant)
         if not self.h:
@@ -126,7 +127,8 @@ class NativeJacobi:
         self.lib.gmt_engine_jacobi_info(self.h, info)
         (self.nx, self.ny, self.off_x, self.off_y, self.halo_bytes, self.halo_msgs,
          graph_on, overlap_on, _, _, tb) = list(info)
-        self.tblock = bool(tb)
+        self.tsteps = int(tb)
+        self.tblock = self.tsteps > 1
         self.graph = bool(graph_on)
         self.overlap = bool(overlap_on)
         self.transport = "rccl" if transport == RCCL else "local"

@@ -14,6 +14,7 @@ from .kernels import (  # noqa: F401
     jacobi5,
     jacobi5_rects,
     jacobi5x2,
+    jacobi5xk,
     set_jacobi_variant,
     stencil5_1d,
     stencil5_2d,

@@ -255,25 +255,32 @@ def jacobi5_rects(u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, 
                                       _stream(u)), "gmt_jacobi5_rects")
 
 
-def jacobi5x2(u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, int, int, int]],
-              dom: tuple[int, int, int, int], halo_mask: int = 0, tile_rows: int = 16) -> None:
-    """Two fused Laplace Jacobi sweeps (temporal blocking): ``un = J(J(u))`` on each
-    output rect (absolute coordinates, x0 even).  ``dom`` is the interior; bits of
-    ``halo_mask`` (1 W, 2 E, 4 S, 8 N) mark ghost sides owned by a neighbour."""
+def jacobi5xk(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, int, int, int]],
+              dom: tuple[int, int, int, int], halo_mask: int = 0, tile: int = 0) -> None:
+    """``k`` (2-4) fused Laplace Jacobi sweeps (temporal blocking): ``un = J^k(u)`` on
+    each output rect (absolute coordinates, x0 even).  ``dom`` is the interior; bits
+    of ``halo_mask`` (1 W, 2 E, 4 S, 8 N) mark ghost sides owned by a neighbour.
+    ``tile`` = (TX << 16) | TY (0 = default)."""
     rects = [tuple(int(v) for v in r) for r in rects if r[1] > 0 and r[3] > 0]
     if not rects:
         return
     if not _is_dev(u):
-        ref.jacobi5x2(u, un, rects, dom, halo_mask)
+        ref.jacobi5xk(k, u, un, rects, dom, halo_mask)
         return
     assert len(rects) <= 4 and u.stride(0) == un.stride(0)
     L = _native.lib()
     arr = (ctypes.c_int64 * (4 * len(rects)))(*[v for r in rects for v in r])
     d = (ctypes.c_int64 * 4)(*[int(v) for v in dom])
-    _native.check(L.gmt_jacobi5x2(len(rects), ctypes.cast(arr, ctypes.c_void_p),
+    _native.check(L.gmt_jacobi5xk(int(k), len(rects), ctypes.cast(arr, ctypes.c_void_p),
                                   ctypes.cast(d, ctypes.c_void_p), int(halo_mask), u.data_ptr(),
-                                  un.data_ptr(), u.stride(0), int(tile_rows), _stream(u)),
-                  "gmt_jacobi5x2")
+                                  un.data_ptr(), u.stride(0), int(tile), _stream(u)),
+                  "gmt_jacobi5xk")
+
+
+def jacobi5x2(u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, int, int, int]],
+              dom: tuple[int, int, int, int], halo_mask: int = 0, tile_rows: int = 0) -> None:
+    """Two fused Laplace Jacobi sweeps: ``jacobi5xk(2, ...)``."""
+    jacobi5xk(2, u, un, rects, dom, halo_mask, tile_rows)
 
 
 def set_jacobi_variant(v: int) -> None:

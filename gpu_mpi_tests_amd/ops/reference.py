@@ -85,19 +85,31 @@ def jacobi5(u: torch.Tensor, un: torch.Tensor, x0: int, nx: int, y0: int, ny: in
     return (d * d).sum()
 
 
-def jacobi5x2(u: torch.Tensor, un: torch.Tensor, rects, dom, halo_mask: int = 0) -> None:
-    """fp64 reference of two fused Laplace sweeps with the ghost-side rule of
-    csrc/kernels/jacobi5x2.hip: a ring cell outside ``dom`` gets the
+def jacobi5xk(k: int, u: torch.Tensor, un: torch.Tensor, rects, dom, halo_mask: int = 0) -> None:
+    """fp64 reference of k fused Laplace sweeps with the ghost-side rule of
+    csrc/kernels/jacobi5x2.hip: a ring cell outside ``dom`` gets an
     intermediate update only if its side's bit is set in ``halo_mask``."""
     dx0, dnx, dy0, dny = dom
     dx1, dy1 = dx0 + dnx, dy0 + dny
     for (x0, nx, y0, ny) in rects:
-        xs = torch.arange(x0 - 1, x0 + nx + 1)
-        ys = torch.arange(y0 - 1, y0 + ny + 1)
-        rx = ((xs >= dx0) & (xs < dx1)) | torch.where(xs < dx0, bool(halo_mask & 1), bool(halo_mask & 2))
-        ry = ((ys >= dy0) & (ys < dy1)) | torch.where(ys < dy0, bool(halo_mask & 4), bool(halo_mask & 8))
-        c = u[y0 - 1:y0 + ny + 1, x0 - 1:x0 + nx + 1]
-        upd = 0.25 * ((u[y0 - 1:y0 + ny + 1, x0 - 2:x0 + nx] + u[y0 - 1:y0 + ny + 1, x0:x0 + nx + 2])
-                      + (u[y0 - 2:y0 + ny, x0 - 1:x0 + nx + 1] + u[y0:y0 + ny + 2, x0 - 1:x0 + nx + 1]))
-        b = torch.where(ry[:, None] & rx[None, :], upd, c)
-        un[y0:y0 + ny, x0:x0 + nx] = 0.25 * ((b[1:-1, :-2] + b[1:-1, 2:]) + (b[:-2, 1:-1] + b[2:, 1:-1]))
+        cur = u[y0 - k:y0 + ny + k, x0 - k:x0 + nx + k].clone()
+        for p in range(1, k + 1):
+            r = k - p  # ring of this level
+            xs = torch.arange(x0 - r, x0 + nx + r)
+            ys = torch.arange(y0 - r, y0 + ny + r)
+            sl = (slice(p, cur.shape[0] - p), slice(p, cur.shape[1] - p))
+            upd = 0.25 * ((cur[p:-p, p - 1:cur.shape[1] - p - 1] + cur[p:-p, p + 1:cur.shape[1] - p + 1])
+                          + (cur[p - 1:cur.shape[0] - p - 1, p:-p] + cur[p + 1:cur.shape[0] - p + 1, p:-p]))
+            if p == k:
+                un[y0:y0 + ny, x0:x0 + nx] = upd
+                break
+            rx = ((xs >= dx0) & (xs < dx1)) | torch.where(xs < dx0, bool(halo_mask & 1), bool(halo_mask & 2))
+            ry = ((ys >= dy0) & (ys < dy1)) | torch.where(ys < dy0, bool(halo_mask & 4), bool(halo_mask & 8))
+            nxt = cur.clone()
+            nxt[sl] = torch.where(ry[:, None] & rx[None, :], upd, cur[sl])
+            cur = nxt
+
+
+def jacobi5x2(u: torch.Tensor, un: torch.Tensor, rects, dom, halo_mask: int = 0) -> None:
+    """Two fused sweeps: ``jacobi5xk(2, ...)``."""
+    jacobi5xk(2, u, un, rects, dom, halo_mask)

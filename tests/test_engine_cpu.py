@@ -65,3 +65,9 @@ def test_native_engine_serial_mode():
 def test_native_engine_temporal_blocking(steps, periodic):
     r = _run(ny=41, nx=66, steps=steps, periodic=periodic, overlap=True, tblock=True)
     assert r["diff"] < 1e-13
+
+
+@pytest.mark.parametrize("k", [3, 4])
+def test_native_engine_k_sweeps(k):
+    r = _run(ny=41, nx=66, steps=11, periodic=True, overlap=True, tblock=k)
+    assert r["diff"] < 1e-13

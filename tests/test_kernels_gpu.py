@@ -308,3 +308,19 @@ def test_jacobi5x2_frame_rects_match_full():
                              (xo + nx - 2, 2, g + 2, ny - 4)], dom, 15)
     torch.cuda.synchronize()
     assert torch.equal(split[g:g + ny, xo:xo + nx], full[g:g + ny, xo:xo + nx])
+
+
+@pytest.mark.parametrize("k", [3, 4])
+@pytest.mark.parametrize("tile", [0, (32 << 16) | 32, (64 << 16) | 8, (128 << 16) | 8])
+@pytest.mark.parametrize("ny,nx", [(1, 2), (6, 9), (33, 130), (70, 515)])
+@pytest.mark.parametrize("mask", [0, 15, 6])
+def test_jacobi5xk_fused_k_sweeps(k, tile, ny, nx, mask):
+    g, xo = k, 8
+    u = _rand(ny + 2 * g, (xo + nx + 9) // 2 * 2, seed=61)
+    dom = (xo, nx, g, ny)
+    un = torch.zeros_like(u)
+    ops.jacobi5xk(k, u, un, [(xo, nx, g, ny)], dom, mask, tile)
+    exp = torch.zeros(u.shape, dtype=torch.float64)
+    ref.jacobi5xk(k, u.cpu(), exp, [(xo, nx, g, ny)], dom, mask)
+    torch.cuda.synchronize()
+    assert torch.equal(un[g:g + ny, xo:xo + nx].cpu(), exp[g:g + ny, xo:xo + nx])

@@ -200,6 +200,12 @@ def test_mpi_stencil2d_sycl_oo_strong_scaling_and_debug():
     (["61", "11", "--tblock", "--dims=2x2", "--periodic", "--transport=ipc"], 4),
     (["45", "8", "--tblock=8", "--dims=2x3", "--periodic"], 6),
     (["45", "8", "--tblock=32", "--dims=1x3", "--no-overlap"], 3),
+    # 3 and 4 sweeps per pass (ghost width 3/4, odd K stages an even-aligned ring)
+    (["64", "13", "--tblock", "--tsteps=3"], 1),
+    (["64", "13", "--tblock", "--tsteps=4", "--periodic"], 1),
+    (["61", "11", "--tblock", "--tsteps=3", "--dims=2x2", "--periodic", "--transport=ipc"], 4),
+    (["70", "10", "--tblock", "--tsteps=4", "--dims=2x3"], 6),
+    (["50", "10", "--tblock", "--tsteps=4", "--transport=mpi-host"], 3),
 ])
 def test_mpi_jacobi2d_matches_serial(args, np_):
     out = run_app("mpi_jacobi2d", *args, "--check", "--warmup=2", "--halo-iters=3", np=np_).stdout
