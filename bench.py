@@ -38,6 +38,8 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+DEFAULT_TSTEPS = 2  # fused sweeps per memory pass / halo exchange (native engine)
+
 from gpu_mpi_tests_amd import ops  # noqa: E402
 from gpu_mpi_tests_amd.parallel import dist as gdist  # noqa: E402
 from gpu_mpi_tests_amd.parallel.decomp import choose_dims  # noqa: E402
@@ -69,6 +71,7 @@ def bench_native(env, n, steps, warmup, overlap, dims, graph, variant, tblock):
                        tblock=tblock)
     dt = _timed(env, eng.run, eng.synchronize, steps, warmup)
     info = {"engine": "native", "graph": eng.graph, "overlap": eng.overlap, "tblock": eng.tblock,
+            "tsteps": eng.tsteps,
             "transport": eng.transport if env.world_size > 1 else "none",
             "halo_bytes_per_rank": eng.halo_bytes, "dims": (eng.py, eng.px)}
     return eng, dt, info
@@ -145,6 +148,8 @@ def main(argv=None):
     ap.add_argument("--tblock", choices=("on", "off"), default="on",
                     help="temporal blocking (native engine): two sweeps per memory pass and per "
                          "2-wide halo exchange; bitwise the same result as single sweeps")
+    ap.add_argument("--tsteps", type=int, default=0,
+                    help="sweeps per fused pass with --tblock on (2-8; 0 = default %d)" % DEFAULT_TSTEPS)
     ap.add_argument("--dims", type=str, default=None, help="process grid PYxPX, e.g. 4x2")
     ap.add_argument("--daxpy-n", type=int, default=1 << 28)
     ap.add_argument("--skip-extras", action="store_true", help="headline stencil only")
@@ -163,7 +168,8 @@ def main(argv=None):
     graph = args.graph == "on" or (args.graph == "auto" and env.world_size == 1)
     if engine == "native":
         solver, dt, info = bench_native(env, args.size, args.steps, args.warmup, overlap, dims,
-                                        graph, args.variant, args.tblock == "on")
+                                        graph, args.variant,
+                                        (args.tsteps or DEFAULT_TSTEPS) if args.tblock == "on" else False)
     else:
         if env.is_gpu and args.variant:
             ops.set_jacobi_variant(args.variant)
@@ -211,6 +217,7 @@ def main(argv=None):
                 "engine": info["engine"],
                 "hipgraph": info["graph"],
                 "temporal_blocking": info["tblock"],
+                "sweeps_per_pass": info.get("tsteps", 1),
                 "transport": info["transport"],
                 "halo_bytes_per_rank": info["halo_bytes_per_rank"],
                 "device": str(env.device),

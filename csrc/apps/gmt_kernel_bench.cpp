@@ -109,6 +109,23 @@ int main(int argc, char** argv) {
         report("jacobi5xk", K, tag, ms, K * 16.0 * n * n);
       }
     }
+    // register-pipelined K-sweep kernel: rows per wave
+    for (int K = 2; K <= 8; K += 2) {
+      const int64_t g = K;
+      const int64_t ld2 = ((xo + n + g + 63) / 64) * 64;
+      Buffer<double> a(static_cast<size_t>(ld2) * (n + 2 * g), GMT_SPACE_DEVICE), b(a.size(), GMT_SPACE_DEVICE);
+      GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, a.data(), ld2, s));
+      GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, b.data(), ld2, s));
+      const int64_t rect[4] = {xo, n, g, n};
+      for (int seg : {64, 128, 256, 512, 1024}) {
+        const double ms = time_ms(s, iters, [&] {
+          GMT_CHECK("pipe", gmt_jacobi5xk(K, 1, rect, rect, 0, a.data(), b.data(), ld2, GMT_XK_PIPE | seg, s));
+        });
+        char tag[64];
+        std::snprintf(tag, sizeof(tag), "%s x%d seg%d", shape, K, seg);
+        report("jacobi5pipe", K, tag, ms, K * 16.0 * n * n);
+      }
+    }
   }
   if (only.find("stencil") != std::string::npos) {
     // the reference's default deriv shapes: 1028 x 524288 (dim 0), 524288 x 1028 (dim 1)

@@ -48,7 +48,8 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   nb_.north = cy < c.py - 1 ? at(cy + 1, cx) : (c.periodic ? at(0, cx) : -1);
 
   ks_ = c.tsteps > 1 ? c.tsteps : (c.tblock ? 2 : 1);
-  if (ks_ > 4) ks_ = 4;
+  if (ks_ > 8) ks_ = 8;
+  if (ks_ > 4 && ks_ % 2) --ks_;  // 5..8 sweeps: register-pipelined kernel, even counts only
   g_ = ks_;
   yo_ = g_;
   ld_ = round_up(xo_ + nx_ + g_, 64);
@@ -137,13 +138,14 @@ int JacobiSolver::halo_mask() const {
 // travels on the comm stream while the fused kernel updates the core whose
 // ks-step dependency cone stays inside the interior; the ks-wide frame
 // follows once the halo has landed.
-void JacobiSolver::enqueue_block(int parity) {
+void JacobiSolver::enqueue_block(int parity, int K) {
   Halo2D& h = *halo_[parity];
   const double* u = buf_[parity].data();
   double* un = buf_[parity ^ 1].data();
   const int64_t dom[4] = {xo_, nx_, yo_, ny_};
   const int mask = halo_mask();
-  const int tr = cfg_.tile, K = ks_;
+  // the remainder pass of run() (K < ks_) uses the kernel default tile
+  const int tr = K == ks_ ? cfg_.tile : 0;
   const int64_t KA = (K + 1) & ~1;  // x offsets stay even (16-B staging)
   if (!h.active()) {
     GMT_CHECK("jacobi xk", gmt_jacobi5xk(K, 1, dom, dom, mask, u, un, ld_, tr, s_));
@@ -174,14 +176,24 @@ void JacobiSolver::step_block() {
   if (graph2_[parity_])
     GMT_CHECK("graph launch", gmt_rt_graph_launch(graph2_[parity_], s_));
   else
-    enqueue_block(parity_);
+    enqueue_block(parity_, ks_);
   parity_ ^= 1;  // u(t+ks) lives in the other buffer
 }
 
 void JacobiSolver::run(int k) {
-  if (ks_ > 1)
+  if (ks_ > 1) {
     for (; k >= ks_; k -= ks_) step_block();
+    // remainder: one shorter fused pass (eager; the ks-wide halo covers it)
+    // — even counts on the pipelined kernel, 3 on the LDS-tiled one
+    const int r = (k % 2 == 0 || k == 3) ? k : k - 1;
+    if (r >= 2) {
+      enqueue_block(parity_, r);
+      parity_ ^= 1;
+      k -= r;
+    }
+  }
   for (; k > 0; --k) step();
+  watchdog_kick("jacobi steps enqueued");
 }
 
 void JacobiSolver::capture_graphs() {
@@ -205,7 +217,7 @@ void JacobiSolver::capture_graphs() {
       if (p < 2)
         enqueue_step(p);
       else
-        enqueue_block(p - 2);
+        enqueue_block(p - 2, ks_);
       e = gmt_rt_stream_end_capture(s_, p < 2 ? &graph_[p] : &graph2_[p - 2]);
     }
     if (e != 0) {
@@ -232,6 +244,7 @@ void JacobiSolver::step() {
 void JacobiSolver::synchronize() {
   GMT_CHECK("sync", gmt_rt_stream_synchronize(s_));
   GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));
+  watchdog_kick("jacobi synchronize");
 }
 
 double JacobiSolver::residual() {

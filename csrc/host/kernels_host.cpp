@@ -150,8 +150,10 @@ int gmt_jacobi5_rects(int n_rect, const int64_t* r, const double* u, double* un,
 }
 
 int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom, int mask,
-                  const double* u, double* un, int64_t ld, int, void*) {
-  if (n_rect < 0 || n_rect > 4 || nsweeps < 2 || nsweeps > 4) return 1;
+                  const double* u, double* un, int64_t ld, int tile, void*) {
+  if (n_rect < 0 || n_rect > 4 || nsweeps < 2 || nsweeps > 8) return 1;
+  if (nsweeps > 4 && nsweeps % 2) return 1;  // same support matrix as the HIP build
+  (void)tile;
   const int K = nsweeps;
   const int64_t dx0 = dom[0], dx1 = dom[0] + dom[1], dy0 = dom[2], dy1 = dom[2] + dom[3];
   for (int k = 0; k < n_rect; ++k) {
@@ -190,6 +192,12 @@ int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, const int64_t* 
 int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int mask, const double* u,
                   double* un, int64_t ld, int tile, void* stream) {
   return gmt_jacobi5xk(2, n_rect, rects, dom, mask, u, un, ld, tile, stream);
+}
+
+int gmt_jacobi5xk_pipe(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom, int mask,
+                       const double* u, double* un, int64_t ld, int, void* stream) {
+  if (nsweeps % 2) return 1;
+  return gmt_jacobi5xk(nsweeps, n_rect, rects, dom, mask, u, un, ld, 0, stream);
 }
 
 void gmt_jacobi5_set_variant(int v) { g_variant = v; }

@@ -17,6 +17,7 @@
 #include <cstdlib>
 
 #include "gmt/mpi.hpp"
+#include "gmt/watchdog.hpp"
 
 namespace gmt {
 
@@ -80,6 +81,8 @@ inline RankBinding set_rank_device(MPI_Comm comm, bool print) {
     std::printf("RANK[%d/%d] => DEVICE[%d/%d] mem=%zd\n", b.rank + 1, b.world_size, b.device + 1,
                 b.n_devices, b.mem_per_rank);
   GMT_CHECK("set device", gmt_rt_set_device(b.device));
+  watchdog_start(b.rank, b.device);
+  watchdog_kick("device bound");
   return b;
 }
 

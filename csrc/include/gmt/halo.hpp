@@ -23,6 +23,7 @@
 
 #include "gmt/buffer.hpp"
 #include "gmt/transport.hpp"
+#include "gmt/watchdog.hpp"
 
 namespace gmt {
 
@@ -114,6 +115,7 @@ class Halo2D {
 
   void start(gmt_stream_t s) {
     if (!ex_) return;
+    fault_point_exchange(t_.rank());
     if (corners_) {  // y faces complete before the x faces (with their corners) are packed
       pack_y_faces(s);
       ex_->start(s);
@@ -131,10 +133,11 @@ class Halo2D {
     if (corners_) {
       ex_x_->wait(s);
       unpack_x_faces(s);
-      return;
+    } else {
+      ex_->wait(s);
+      unpack(s);
     }
-    ex_->wait(s);
-    unpack(s);
+    watchdog_kick("halo exchange");
   }
   // Blocking exchange, reference semantics: ghosts valid and the stream
   // drained on return.

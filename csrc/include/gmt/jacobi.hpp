@@ -83,7 +83,7 @@ class JacobiSolver {
 
  private:
   void enqueue_step(int parity);
-  void enqueue_block(int parity);
+  void enqueue_block(int parity, int k);  // k <= ks_ fused sweeps
   void step_block();
   void sweep_full(int parity, double* resid);
   void capture_graphs();

@@ -112,10 +112,20 @@ int gmt_jacobi5_rects(int n_rect, const int64_t* rects, const double* u, double*
  * (64 x 16, the measured best). */
 int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
                   const double* u, double* un, int64_t ld, int tile, void* stream);
-/* The same for nsweeps = 2, 3 or 4 fused sweeps (u valid on rect + nsweeps;
- * ghost width >= nsweeps).  gmt_jacobi5x2 == gmt_jacobi5xk(2, ...). */
+/* The same for nsweeps = 2..8 fused sweeps (u valid on rect + nsweeps;
+ * ghost width >= nsweeps).  gmt_jacobi5x2 == gmt_jacobi5xk(2, ...).
+ * Two kernels: the register-pipelined one (jacobi5pipe.hip, even nsweeps;
+ * tile = GMT_XK_PIPE | rows-per-wave, or tile = 0 with an even nsweeps) and
+ * the LDS-tiled one (jacobi5x2.hip, nsweeps 2..4; tile = (TX << 16) | TY,
+ * or tile = 0 with nsweeps = 3). */
+#define GMT_XK_PIPE 0x40000000
 int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
                   const double* u, double* un, int64_t ld, int tile, void* stream);
+/* Register-pipelined K-sweep kernel: one wave per 128-column strip and
+ * `seg` output rows (0 = 256); nsweeps even, 2..8. */
+int gmt_jacobi5xk_pipe(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom,
+                       int halo_mask, const double* u, double* un, int64_t ld, int seg,
+                       void* stream);
 
 /* Kernel variant selection for A/B measurement: 0 = auto, 1 = register
  * sliding window (vector x2, W/E from L1), 2 = LDS-tiled, 3 = scalar

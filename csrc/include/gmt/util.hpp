@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "gmt/rt.h"
+#include "gmt/watchdog.hpp"
 
 namespace gmt {
 
@@ -81,6 +82,8 @@ struct Cli {
         pos.push_back(a);
       }
     }
+    // every app accepts --timeout=S: hang watchdog (gmt/watchdog.hpp)
+    if (has("timeout")) watchdog_set_timeout(getd("timeout", 0.0));
   }
   bool has(const std::string& k) const { return opt.count(k) != 0; }
   std::string get(const std::string& k, const std::string& d) const {

@@ -27,6 +27,19 @@ __device__ __forceinline__ void st2_nt(double* p, d2 v) {
   __builtin_nontemporal_store(v, reinterpret_cast<d2*>(p));
 }
 
+// Whole-wave lane shifts of a double through DPP (wave_shr:1 / wave_shl:1, a
+// VALU source modifier: no LDS traffic).  The edge lane receives 0.
+__device__ __forceinline__ double dpp_from_lower(double v) {  // lane i <- lane i-1
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_from_upper(double v) {  // lane i <- lane i+1
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
 // Bijective XCD-aware remap of a linear block id: consecutive tiles (which
 // share halo rows) land on the same XCD's L2.  Valid for any nblocks.
 __device__ __forceinline__ int64_t xcd_swizzle(int64_t bid, int64_t nblocks) {

@@ -98,17 +98,6 @@ __global__ __launch_bounds__(kBlock) void jacobi5_reg(int64_t x0, int64_t nx, in
 // keeps the L1 loads.  Only the two wave-edge lanes load a neighbour from
 // memory.  R rows per tile; NTS = nontemporal stores of un (streamed out,
 // not re-read before the next step).  Requires an even region width.
-__device__ __forceinline__ double dpp_from_lower(double v) {  // lane i <- lane i-1
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xf, 0xf, false);
-  return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ double dpp_from_upper(double v) {  // lane i <- lane i+1
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xf, 0xf, false);
-  return __hiloint2double(hi, lo);
-}
-
 template <int R, int XCHG, bool NTS>
 __global__ __launch_bounds__(kBlock) void jacobi5_lane(int64_t x0, int64_t nx, int64_t y0,
                                                        int64_t ny, const double* __restrict__ u,

@@ -55,22 +55,34 @@ __global__ __launch_bounds__(kBlock) void jacobi5xk_kernel(XkArgs a, const doubl
   // LDS (yy, xx) <-> global (ya + yy, xa + xx)
   const int64_t xa = ox - KA, ya = oy - K;
 
+  // tile-relative (32-bit) interior bounds; a tile whose whole K-ring lies
+  // inside the interior needs no ghost-side rule (the common case)
+  const int lx0 = static_cast<int>(dx0 - xa), lx1 = static_cast<int>(dx1 - xa);
+  const int ly0 = static_cast<int>(dy0 - ya), ly1 = static_cast<int>(dy1 - ya);
+  const bool inner = lx0 <= KA - K && lx1 >= KA + w + K && ly0 <= 0 && ly1 >= h + 2 * K;
+  const bool full = w == TX && h == TY;
+
   // 1. stage u(t) on the tile + ring (clamped to the stored ghost ring)
   {
-    const int pairs = (w + 2 * KA + 1) / 2;
-    const int64_t xlim = dx1 + K, ylim = dy1 + K;
-    for (int i = tid; i < (h + 2 * K) * pairs; i += kBlock) {
-      const int rr = i / pairs, cp = i - rr * pairs;
-      const int64_t y = ya + rr, x = xa + 2 * cp;
+    const int xlim = lx1 + K, ylim = ly1 + K;  // first column / row past the stored ring
+    auto stage = [&](int rr, int cp) {
+      const int xx = 2 * cp;
       d2 v = {0.0, 0.0};
-      if (y < ylim) {
-        const double* p = u + y * ld + x;
-        if (x + 1 < xlim)
+      if (rr < ylim) {
+        const double* p = u + (ya + rr) * ld + xa + xx;
+        if (xx + 1 < xlim)
           v = ld2(p);
-        else if (x < xlim)
+        else if (xx < xlim)
           v.x = p[0];
       }
-      *reinterpret_cast<d2*>(&L[0][rr * AP + 2 * cp]) = v;
+      *reinterpret_cast<d2*>(&L[0][rr * AP + xx]) = v;
+    };
+    if (full) {
+      constexpr int PAIRS = AP / 2;  // compile-time divisor
+      for (int i = tid; i < AR * PAIRS; i += kBlock) stage(i / PAIRS, i % PAIRS);
+    } else {
+      const int pairs = (w + 2 * KA + 1) / 2;
+      for (int i = tid; i < (h + 2 * K) * pairs; i += kBlock) stage(i / pairs, i % pairs);
     }
   }
   __syncthreads();
@@ -82,24 +94,43 @@ __global__ __launch_bounds__(kBlock) void jacobi5xk_kernel(XkArgs a, const doubl
     const double* S = L[(p - 1) & 1];
     double* D = L[p & 1];
     const int ring = K - p;
-    const int bw = w + 2 * ring, bh = h + 2 * ring;
     const int x_off = KA - ring, y_off = K - ring;
-    for (int i = tid; i < bh * bw; i += kBlock) {
-      const int yy = y_off + i / bw, xx = x_off + i % bw;
-      const int64_t y = ya + yy, x = xa + xx;
-      const bool rx = (x >= dx0 && x < dx1) || (x < dx0 ? gw : ge);
-      const bool ry = (y >= dy0 && y < dy1) || (y < dy0 ? gs : gn);
+    auto cell = [&](int yy, int xx, bool rule) {
       const double* c = &S[yy * AP + xx];
-      D[yy * AP + xx] = (rx && ry) ? 0.25 * ((c[-1] + c[1]) + (c[-AP] + c[AP])) : c[0];
+      const double v = 0.25 * ((c[-1] + c[1]) + (c[-AP] + c[AP]));
+      if (rule) {
+        const bool rx = (xx >= lx0 && xx < lx1) || (xx < lx0 ? gw : ge);
+        const bool ry = (yy >= ly0 && yy < ly1) || (yy < ly0 ? gs : gn);
+        D[yy * AP + xx] = (rx && ry) ? v : c[0];
+      } else {
+        D[yy * AP + xx] = v;
+      }
+    };
+    if (full) {
+      constexpr int BW = TX + 2 * (K - 1);  // widest level; narrower rings skip columns
+      const int bw = TX + 2 * ring, bh = TY + 2 * ring;
+      if (inner) {
+        for (int i = tid; i < bh * BW; i += kBlock) {
+          const int r = i / BW, cc = i % BW;
+          if (cc < bw) cell(y_off + r, x_off + cc, false);
+        }
+      } else {
+        for (int i = tid; i < bh * BW; i += kBlock) {
+          const int r = i / BW, cc = i % BW;
+          if (cc < bw) cell(y_off + r, x_off + cc, true);
+        }
+      }
+    } else {
+      const int bw = w + 2 * ring, bh = h + 2 * ring;
+      for (int i = tid; i < bh * bw; i += kBlock) cell(y_off + i / bw, x_off + i % bw, true);
     }
     __syncthreads();
   }
 
   // 3. u(t+K) on the tile, 16-B nontemporal stores (ox even, ld even)
   const double* S = L[(K - 1) & 1];
-  const int wp = (w + 1) / 2;
-  for (int i = tid; i < h * wp; i += kBlock) {
-    const int yy = K + i / wp, xx = KA + 2 * (i % wp);
+  auto out = [&](int r, int cp) {
+    const int yy = K + r, xx = KA + 2 * cp;
     const double* c = &S[yy * AP + xx];
     double* q = un + (ya + yy) * ld + xa + xx;
     const double o0 = 0.25 * ((c[-1] + c[1]) + (c[-AP] + c[AP]));
@@ -111,6 +142,13 @@ __global__ __launch_bounds__(kBlock) void jacobi5xk_kernel(XkArgs a, const doubl
     } else {
       q[0] = o0;
     }
+  };
+  if (full) {
+    constexpr int WP = TX / 2;
+    for (int i = tid; i < TY * WP; i += kBlock) out(i / WP, i % WP);
+  } else {
+    const int wp = (w + 1) / 2;
+    for (int i = tid; i < h * wp; i += kBlock) out(i / wp, i % wp);
   }
 }
 
@@ -154,6 +192,8 @@ extern "C" int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, cons
                              int halo_mask, const double* u, double* un, int64_t ld, int tile,
                              void* stream) {
   using namespace gmt;
+  if ((tile & GMT_XK_PIPE) || (tile == 0 && nsweeps % 2 == 0))
+    return gmt_jacobi5xk_pipe(nsweeps, n_rect, rects, dom, halo_mask, u, un, ld, tile & 0xffff, stream);
   if (nsweeps < 2 || nsweeps > 4) return static_cast<int>(hipErrorInvalidValue);
   if (n_rect < 0 || n_rect > 4) return static_cast<int>(hipErrorInvalidValue);
   if (!aligned16(u) || !aligned16(un) || (ld % 2) != 0) return static_cast<int>(hipErrorInvalidValue);

@@ -255,12 +255,17 @@ def jacobi5_rects(u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, 
                                       _stream(u)), "gmt_jacobi5_rects")
 
 
+XK_PIPE = 0x40000000  # gmt_jacobi5xk tile flag: register-pipelined kernel (jacobi5pipe.hip)
+
+
 def jacobi5xk(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, int, int, int]],
               dom: tuple[int, int, int, int], halo_mask: int = 0, tile: int = 0) -> None:
-    """``k`` (2-4) fused Laplace Jacobi sweeps (temporal blocking): ``un = J^k(u)`` on
+    """``k`` (2-8) fused Laplace Jacobi sweeps (temporal blocking): ``un = J^k(u)`` on
     each output rect (absolute coordinates, x0 even).  ``dom`` is the interior; bits
     of ``halo_mask`` (1 W, 2 E, 4 S, 8 N) mark ghost sides owned by a neighbour.
-    ``tile`` = (TX << 16) | TY (0 = default)."""
+    ``tile``: 0 = default (register-pipelined kernel for even k, LDS tiles for k = 3),
+    ``XK_PIPE | rows`` = pipelined kernel with ``rows`` output rows per wave,
+    ``(TX << 16) | TY`` = LDS-tiled kernel (k <= 4)."""
     rects = [tuple(int(v) for v in r) for r in rects if r[1] > 0 and r[3] > 0]
     if not rects:
         return

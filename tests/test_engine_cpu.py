@@ -67,7 +67,7 @@ def test_native_engine_temporal_blocking(steps, periodic):
     assert r["diff"] < 1e-13
 
 
-@pytest.mark.parametrize("k", [3, 4])
+@pytest.mark.parametrize("k", [3, 4, 6, 8])
 def test_native_engine_k_sweeps(k):
     r = _run(ny=41, nx=66, steps=11, periodic=True, overlap=True, tblock=k)
     assert r["diff"] < 1e-13

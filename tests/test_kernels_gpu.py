@@ -324,3 +324,42 @@ def test_jacobi5xk_fused_k_sweeps(k, tile, ny, nx, mask):
     ref.jacobi5xk(k, u.cpu(), exp, [(xo, nx, g, ny)], dom, mask)
     torch.cuda.synchronize()
     assert torch.equal(un[g:g + ny, xo:xo + nx].cpu(), exp[g:g + ny, xo:xo + nx])
+
+
+@pytest.mark.parametrize("k", [2, 4, 6, 8])
+@pytest.mark.parametrize("seg", [0, 1, 5, 64])
+@pytest.mark.parametrize("ny,nx", [(1, 2), (7, 9), (40, 126), (33, 130), (70, 515)])
+@pytest.mark.parametrize("mask", [0, 15, 6, 9])
+def test_jacobi5xk_pipelined(k, seg, ny, nx, mask):
+    """Register-pipelined K-sweep kernel (jacobi5pipe.hip): bitwise equal to k
+    fp64 reference sweeps — partial strips (128 - 2k output columns per wave),
+    segments shorter than the pipeline depth, every ghost-side pattern."""
+    g, xo = k, 8
+    u = _rand(ny + 2 * g, (xo + nx + 9) // 2 * 2, seed=71)
+    dom = (xo, nx, g, ny)
+    un = torch.zeros_like(u)
+    ops.jacobi5xk(k, u, un, [(xo, nx, g, ny)], dom, mask, ops.XK_PIPE | seg)
+    exp = torch.zeros(u.shape, dtype=torch.float64)
+    ref.jacobi5xk(k, u.cpu(), exp, [(xo, nx, g, ny)], dom, mask)
+    torch.cuda.synchronize()
+    assert torch.equal(un[g:g + ny, xo:xo + nx].cpu(), exp[g:g + ny, xo:xo + nx])
+
+
+@pytest.mark.parametrize("k", [4, 8])
+def test_jacobi5xk_pipelined_frame_rects(k):
+    """core + 4 frame rects (the engine's overlapped block step) == full launch,
+    and the output never touches cells outside the rects."""
+    g, xo, ny, nx = k, 8, 90, 400
+    u = _rand(ny + 2 * g, xo + nx + 8, seed=72)
+    dom = (xo, nx, g, ny)
+    full = torch.zeros_like(u)
+    ops.jacobi5xk(k, u, full, [dom], dom, 15)
+    split = torch.full_like(u, 7.0)
+    ops.jacobi5xk(k, u, split, [(xo + k, nx - 2 * k, g + k, ny - 2 * k)], dom, 15)
+    ops.jacobi5xk(k, u, split, [(xo, nx, g, k), (xo, nx, g + ny - k, k), (xo, k, g + k, ny - 2 * k),
+                                (xo + nx - k, k, g + k, ny - 2 * k)], dom, 15)
+    torch.cuda.synchronize()
+    assert torch.equal(split[g:g + ny, xo:xo + nx], full[g:g + ny, xo:xo + nx])
+    outside = torch.ones_like(u, dtype=torch.bool)
+    outside[g:g + ny, xo:xo + nx] = False
+    assert bool((split[outside] == 7.0).all())

@@ -206,6 +206,12 @@ def test_mpi_stencil2d_sycl_oo_strong_scaling_and_debug():
     (["61", "11", "--tblock", "--tsteps=3", "--dims=2x2", "--periodic", "--transport=ipc"], 4),
     (["70", "10", "--tblock", "--tsteps=4", "--dims=2x3"], 6),
     (["50", "10", "--tblock", "--tsteps=4", "--transport=mpi-host"], 3),
+    # 6 and 8 sweeps per pass (register-pipelined kernel on the GPU); 13 steps
+    # = one 8-pass + a 4-sweep remainder pass + one single sweep
+    (["64", "13", "--tblock", "--tsteps=8"], 1),
+    (["70", "13", "--tblock", "--tsteps=6", "--periodic"], 1),
+    (["75", "17", "--tblock", "--tsteps=8", "--dims=2x2", "--periodic", "--transport=ipc"], 4),
+    (["80", "12", "--tblock", "--tsteps=6", "--dims=1x2"], 2),
 ])
 def test_mpi_jacobi2d_matches_serial(args, np_):
     out = run_app("mpi_jacobi2d", *args, "--check", "--warmup=2", "--halo-iters=3", np=np_).stdout
@@ -234,3 +240,20 @@ def test_kernel_bench_host():
                   "--only=daxpy,jacobi").stdout
     assert len(re.findall(r"^daxpy\s+v\d", out, re.M)) == 6
     assert len(re.findall(r"^jacobi5\s+v\d", out, re.M)) == 9
+
+
+def test_watchdog_aborts_hung_exchange():
+    """Fault injection: rank 1 stops in its 3rd halo exchange; the --timeout
+    watchdog (gmt/watchdog.hpp) names the stalled phase and MPI_Abort takes
+    the whole job down instead of leaving rank 0 blocked forever."""
+    p = run_app("mpi_jacobi2d", "50", "40", "--transport=ipc", "--timeout=2", np=2,
+                env={"GMT_INJECT_HANG": "1:2"}, check=False, timeout=90)
+    out = p.stdout + p.stderr
+    assert p.returncode != 0, out
+    assert "GMT FAULT INJECTION: rank 1" in out
+    assert "GMT WATCHDOG: rank" in out and "no progress" in out
+
+
+def test_watchdog_quiet_on_healthy_run():
+    p = run_app("mpi_jacobi2d", "50", "20", "--transport=ipc", "--timeout=30", np=2)
+    assert "WATCHDOG" not in p.stdout + p.stderr
