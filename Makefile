@@ -31,9 +31,11 @@ LIBH_ENG  := $(LIBH_DIR)/libgmt_engine.so
 HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
              -Icsrc/include -munsafe-fp-atomics
 ROCM_HOST := -O2 -std=c++17 -fPIC -Wall -Icsrc/include -I$(ROCM)/include -D__HIP_PLATFORM_AMD__=1
-HOSTFLAGS := -O3 -std=c++17 -fPIC -Wall -Icsrc/include
-APPFLAGS  := -O2 -std=c++17 -Wall -Icsrc/include -Icsrc/apps -I$(MPI_HOME)/include
-ENGFLAGS  := -O2 -std=c++17 -Wall -fPIC -Icsrc/include
+# SAN: host-side sanitizer flags (make asan-host); never applied to GPU code
+SAN       ?=
+HOSTFLAGS := -O3 -std=c++17 -fPIC -Wall -Icsrc/include $(SAN)
+APPFLAGS  := -O2 -std=c++17 -Wall -Icsrc/include -Icsrc/apps -I$(MPI_HOME)/include $(SAN)
+ENGFLAGS  := -O2 -std=c++17 -Wall -fPIC -Icsrc/include $(SAN)
 MPI_LIBS  := $(MPI_HOME)/lib/libmpi.so -Wl,-rpath,$(MPI_HOME)/lib -static-libstdc++ -static-libgcc -Wl,--allow-shlib-undefined
 
 KERNEL_SRCS := $(wildcard csrc/kernels/*.hip)
@@ -52,7 +54,7 @@ APPS := daxpy daxpy_nvtx mpi_daxpy mpi_daxpy_nvtx_managed mpi_daxpy_nvtx_unmanag
         mpienv mpigatherinplace mpi_daxpy_gt mpi_stencil_gt mpi_stencil2d_gt \
         mpi_stencil2d_sycl mpi_stencil2d_sycl_oo mpi_jacobi2d mpi_halo_bench gmt_kernel_bench
 
-.PHONY: all lib host apps host-apps sweep clean
+.PHONY: all lib host apps host-apps asan-host sweep clean
 all: lib host apps sweep
 
 lib: $(LIB) $(LIB_CCL) $(LIB_ENG)
@@ -81,11 +83,11 @@ $(OBJ)/host/%.o: csrc/host/%.cpp csrc/include/gmt/rt.h csrc/include/gmt/kernels.
 
 $(LIBH): $(HOST_OBJS)
 	@mkdir -p $(LIBH_DIR)
-	$(CXX) -shared -fPIC -o $@ $^ -Wl,-soname,libgmt.so
+	$(CXX) $(SAN) -shared -fPIC -o $@ $^ -Wl,-soname,libgmt.so
 
 $(LIBH_CCL): $(HOSTCCL_OBJ)
 	@mkdir -p $(LIBH_DIR)
-	$(CXX) -shared -fPIC -o $@ $^ -Wl,-soname,libgmt_ccl.so
+	$(CXX) $(SAN) -shared -fPIC -o $@ $^ -Wl,-soname,libgmt_ccl.so
 
 $(OBJ)/comm/%.o: csrc/comm/%.cpp $(APP_HDRS)
 	@mkdir -p $(dir $@)
@@ -128,8 +130,13 @@ $(BIN)/%: $(OBJ)/apps/%.o $(COMM_OBJS) $(LIB) $(LIB_CCL)
 
 $(BINH)/%: $(OBJ)/apps/%.o $(COMM_OBJS) $(LIBH) $(LIBH_CCL)
 	@mkdir -p $(BINH)
-	$(CXX) -o $@ $< $(COMM_OBJS) -L$(LIBH_DIR) -lgmt -lgmt_ccl \
+	$(CXX) $(SAN) -o $@ $< $(COMM_OBJS) -L$(LIBH_DIR) -lgmt -lgmt_ccl \
 	  -Wl,-rpath,'$$ORIGIN/../lib-host' $(MPI_LIBS)
+
+# CPU backend + apps under AddressSanitizer/UBSan (host code only; the
+# SURVEY §5.2 plan: sanitizers on host code for CPU-only CI).  Separate tree.
+asan-host:
+	$(MAKE) BUILD=$(BUILD)/asan SAN="-fsanitize=address,undefined -fno-omit-frame-pointer -g" host-apps
 
 # tuning harness (standalone, not part of the libraries)
 sweep: $(BUILD)/bench/stream_sweep

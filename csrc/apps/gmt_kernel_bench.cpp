@@ -80,7 +80,10 @@ int main(int argc, char** argv) {
     GMT_CHECK("fill", gmt_fill_poly(0, ld, n + 2, 0.0, 1e-5, 0.0, 1e-5, un.data(), ld, s));
     char shape[64];
     std::snprintf(shape, sizeof(shape), "%lldx%lld", (long long)n, (long long)n);
-    for (int v = 1; v <= 9; ++v) {
+    // --sections=v,xk,pipe (default all): single-sweep variants, LDS-tiled
+    // K-sweep kernel, register-pipelined K-sweep kernel
+    const std::string sec = cli.get("sections", "v,xk,pipe");
+    for (int v = 1; v <= 9 && sec.find('v') != std::string::npos; ++v) {
       if (v == 3 && n > 16384) continue;  // scalar reference kernel: too slow to matter
       gmt_jacobi5_set_variant(v);
       const double ms = time_ms(s, iters, [&] {
@@ -91,7 +94,7 @@ int main(int argc, char** argv) {
     gmt_jacobi5_set_variant(0);
     // temporal blocking: K sweeps per call; "GB/s" is the single-sweep
     // equivalent (K x 16 B per point), i.e. directly comparable with v1-v9
-    for (int K = 2; K <= 4; ++K) {
+    for (int K = 2; K <= 4 && sec.find("xk") != std::string::npos; ++K) {
       const int64_t g = K;
       const int64_t ld2 = ((xo + n + g + 63) / 64) * 64;
       Buffer<double> a(static_cast<size_t>(ld2) * (n + 2 * g), GMT_SPACE_DEVICE), b(a.size(), GMT_SPACE_DEVICE);
@@ -110,21 +113,24 @@ int main(int argc, char** argv) {
       }
     }
     // register-pipelined K-sweep kernel: rows per wave
-    for (int K = 2; K <= 8; K += 2) {
+    for (int K = 2; K <= 8 && sec.find("pipe") != std::string::npos; K += 2) {
       const int64_t g = K;
       const int64_t ld2 = ((xo + n + g + 63) / 64) * 64;
       Buffer<double> a(static_cast<size_t>(ld2) * (n + 2 * g), GMT_SPACE_DEVICE), b(a.size(), GMT_SPACE_DEVICE);
       GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, a.data(), ld2, s));
       GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, b.data(), ld2, s));
       const int64_t rect[4] = {xo, n, g, n};
-      for (int seg : {64, 128, 256, 512, 1024}) {
-        const double ms = time_ms(s, iters, [&] {
-          GMT_CHECK("pipe", gmt_jacobi5xk(K, 1, rect, rect, 0, a.data(), b.data(), ld2, GMT_XK_PIPE | seg, s));
-        });
-        char tag[64];
-        std::snprintf(tag, sizeof(tag), "%s x%d seg%d", shape, K, seg);
-        report("jacobi5pipe", K, tag, ms, K * 16.0 * n * n);
-      }
+      for (int occ : {0, 3, 4})
+        for (int seg : {64, 128, 256, 512}) {
+          if (occ && K < 4) continue;
+          const int tile = GMT_XK_PIPE | (occ << 16) | seg;
+          const double ms = time_ms(s, iters, [&] {
+            GMT_CHECK("pipe", gmt_jacobi5xk(K, 1, rect, rect, 0, a.data(), b.data(), ld2, tile, s));
+          });
+          char tag[64];
+          std::snprintf(tag, sizeof(tag), "%s x%d seg%d occ%d", shape, K, seg, occ);
+          report("jacobi5pipe", K, tag, ms, K * 16.0 * n * n);
+        }
     }
   }
   if (only.find("stencil") != std::string::npos) {

@@ -115,14 +115,16 @@ int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int halo
 /* The same for nsweeps = 2..8 fused sweeps (u valid on rect + nsweeps;
  * ghost width >= nsweeps).  gmt_jacobi5x2 == gmt_jacobi5xk(2, ...).
  * Two kernels: the register-pipelined one (jacobi5pipe.hip, even nsweeps;
- * tile = GMT_XK_PIPE | rows-per-wave, or tile = 0 with an even nsweeps) and
+ * tile = GMT_XK_PIPE | (occ << 16) | rows-per-wave, occ = waves-per-SIMD hint
+ * 3/4 or 0; or tile = 0 with an even nsweeps) and
  * the LDS-tiled one (jacobi5x2.hip, nsweeps 2..4; tile = (TX << 16) | TY,
  * or tile = 0 with nsweeps = 3). */
 #define GMT_XK_PIPE 0x40000000
 int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
                   const double* u, double* un, int64_t ld, int tile, void* stream);
 /* Register-pipelined K-sweep kernel: one wave per 128-column strip and
- * `seg` output rows (0 = 256); nsweeps even, 2..8. */
+ * `seg & 0xffff` output rows (0 = 256), `(seg >> 16) & 0xf` = waves-per-SIMD
+ * register-allocation hint (0 = none); nsweeps even, 2..8. */
 int gmt_jacobi5xk_pipe(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom,
                        int halo_mask, const double* u, double* un, int64_t ld, int seg,
                        void* stream);

@@ -9,17 +9,18 @@
 //
 // Here one wave owns a 128-column strip (2 columns per lane) and walks down
 // a segment of rows.  Time level p of row r is computed from level p-1 of
-// rows r-1, r, r+1, which the wave computed in its three previous steps, so
-// every level lives in a 3-row register window:
-//   step s: load row s of u(t)             -> level 0
-//           level 1 of row s-1, level 2 of row s-2, ..., level K of row s-K
-//           store level K (= u(t+K)) of row s-K (16-B nontemporal stores)
+// rows r-1, r, r+1, which the wave computed in its three PREVIOUS steps, so
+// every level lives in a 3-row register window (a skewed pipeline):
+//   step s: level p of row s-2p for p = K..1 (independent of each other:
+//           K-way instruction-level parallelism, no intra-step chain)
+//           store level K (= u(t+K)) of row s-2K (16-B nontemporal stores)
+//           level 0 <- row s of u(t) (prefetched three steps earlier)
 // West/east neighbours come from the adjacent lane through DPP
 // (wave_shr/wave_shl: no LDS, no barriers).  The wave edges lose one column
 // per level, so a strip yields 128 - 2K output columns; a segment of L rows
-// loads L + 2K rows.  Per update and sweep: 3 DADD + 1 DMUL + 2 DPP movs.
-// The three-slot register window is rotated by unrolling the row loop by 3
-// (no register moves).
+// loads L + 2K rows in L + 3K steps.  Per update and sweep: 3 DADD + 1 DMUL
+// + 2 DPP movs.  The three-slot register window is rotated by unrolling the
+// row loop by 3 (no register moves).
 //
 // Same arithmetic and operand order as K single sweeps: bitwise equal.
 // Dirichlet/halo rule as in jacobi5x2.hip: a ring cell outside the interior
@@ -61,14 +62,20 @@ __device__ __forceinline__ void pipe_strip(const PipeArgs& a, const double* __re
   // store mask
   const bool st0 = c0 >= xs && c0 < xe, st1 = c0 + 1 >= xs && c0 + 1 < xe;
 
-  const int64_t yl = ys - K;                // row of step 0
-  const int nsteps = static_cast<int>(ye - ys) + 2 * K;
+  // Skewed pipeline: level p at step s is row yl + s - 2p, computed from
+  // level p-1 of the three PREVIOUS steps, so the K levels of one step are
+  // independent (K-way ILP instead of a K-deep dependency chain); levels are
+  // evaluated top-down so level p reads slot s%3 of level p-1 before level
+  // p-1 overwrites it.
+  const int64_t yl = ys - K;                 // row loaded at step 0
+  const int nload = static_cast<int>(ye - ys) + 2 * K;
+  const int nsteps = static_cast<int>(ye - ys) + 3 * K;
   const double* up = u + yl * ld + c0;
-  double* op = un + (ys - 2 * K) * ld + c0;  // output row of step s: ys - 2K + s
+  double* op = un + (ys - 3 * K) * ld + c0;  // output row of step s: ys - 3K + s
 
   auto load = [&](int s) -> d2 {
     d2 v = {0.0, 0.0};
-    if (s < nsteps && yl + s < ylim) {
+    if (s < nload && yl + s < ylim) {
       const double* p = up + static_cast<int64_t>(s) * ld;
       if (lmode == 2)
         v = ld2(p);
@@ -89,25 +96,24 @@ __device__ __forceinline__ void pipe_strip(const PipeArgs& a, const double* __re
   Q[2] = load(2);
 
   auto step = [&](auto P, int s) {
-    constexpr int cur = decltype(P)::value, old = (cur + 1) % 3, mid = (cur + 2) % 3;
-    W[0][cur] = Q[cur];
-    Q[cur] = load(s + 3);
+    // slots of level p-1 written at steps s-3, s-2, s-1
+    constexpr int cur = decltype(P)::value, s3 = cur, s2 = (cur + 1) % 3, s1 = (cur + 2) % 3;
 #pragma unroll
-    for (int p = 1; p <= K; ++p) {
-      const d2 up_ = W[p - 1][old], c = W[p - 1][mid], dn = W[p - 1][cur];
+    for (int p = K; p >= 1; --p) {
+      const d2 up_ = W[p - 1][s3], c = W[p - 1][s2], dn = W[p - 1][s1];
       const double w = dpp_from_lower(c.y), e = dpp_from_upper(c.x);
       d2 v;
       v.x = 0.25 * ((w + c.y) + (up_.x + dn.x));
       v.y = 0.25 * ((c.x + e) + (up_.y + dn.y));
       if (RULE) {
-        const int64_t r = yl + s - p;  // row of this level's value
+        const int64_t r = yl + s - 2 * p;  // row of this level's value
         const bool ry = (r >= dy0 && r < dy1) || (r < dy0 ? gs : gn);
         v.x = (ry && rx0) ? v.x : c.x;
         v.y = (ry && rx1) ? v.y : c.y;
       }
       if (p < K) {
         W[p][cur] = v;
-      } else if (s >= 2 * K) {
+      } else if (s >= 3 * K) {
         double* q = op + static_cast<int64_t>(s) * ld;
         if (st0 && st1)
           st2_nt(q, v);
@@ -117,6 +123,8 @@ __device__ __forceinline__ void pipe_strip(const PipeArgs& a, const double* __re
           q[1] = v.y;
       }
     }
+    W[0][cur] = Q[cur];
+    Q[cur] = load(s + 3);
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -128,10 +136,12 @@ __device__ __forceinline__ void pipe_strip(const PipeArgs& a, const double* __re
   }
 }
 
-template <int K>
-__global__ __launch_bounds__(kBlock) void jacobi5pipe_kernel(PipeArgs a, const double* __restrict__ u,
-                                                             double* __restrict__ un, int64_t ld,
-                                                             int64_t nblocks) {
+// OCC: minimum waves per SIMD requested from the register allocator (1 = no
+// constraint); caps the VGPR budget of the deep (K = 6, 8) pipelines.
+template <int K, int OCC>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC)))
+void jacobi5pipe_kernel(PipeArgs a, const double* __restrict__ u, double* __restrict__ un, int64_t ld,
+                        int64_t nblocks) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wid = xcd_swizzle(blockIdx.x, nblocks) * (kBlock / kWave) + threadIdx.x / kWave;
   if (wid >= a.wstart[a.n]) return;  // whole wave
@@ -167,7 +177,7 @@ extern "C" int gmt_jacobi5xk_pipe(int nsweeps, int n_rect, const int64_t* rects,
   if (n_rect < 0 || n_rect > 4) return static_cast<int>(hipErrorInvalidValue);
   if (!aligned16(u) || !aligned16(un) || (ld % 2) != 0) return static_cast<int>(hipErrorInvalidValue);
   PipeArgs a{};
-  a.seg = seg > 0 ? seg : 256;
+  a.seg = (seg & 0xffff) > 0 ? (seg & 0xffff) : 256;
   a.mask = halo_mask;
   for (int j = 0; j < 4; ++j) a.dom[j] = dom[j];
   const int wout = kPipeCols - 2 * nsweeps;
@@ -186,11 +196,18 @@ extern "C" int gmt_jacobi5xk_pipe(int nsweeps, int n_rect, const int64_t* rects,
   const int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const unsigned g = grid_1d(nb);
+  const int occ = (seg >> 16) & 0xf;  // waves-per-SIMD hint (0 = per-K default)
+  bool ok = true;
+#define GMT_PIPE(KK, OO) jacobi5pipe_kernel<KK, OO><<<g, kBlock, 0, s>>>(a, u, un, ld, nb)
   switch (nsweeps) {
-    case 2: jacobi5pipe_kernel<2><<<g, kBlock, 0, s>>>(a, u, un, ld, nb); break;
-    case 4: jacobi5pipe_kernel<4><<<g, kBlock, 0, s>>>(a, u, un, ld, nb); break;
-    case 6: jacobi5pipe_kernel<6><<<g, kBlock, 0, s>>>(a, u, un, ld, nb); break;
-    default: jacobi5pipe_kernel<8><<<g, kBlock, 0, s>>>(a, u, un, ld, nb); break;
+    case 2: GMT_PIPE(2, 1); break;
+    case 4: if (occ == 4) GMT_PIPE(4, 4); else GMT_PIPE(4, 1); break;
+    case 6: if (occ == 3) GMT_PIPE(6, 3); else if (occ == 4) GMT_PIPE(6, 4); else GMT_PIPE(6, 1); break;
+    default:
+      if (occ == 3) GMT_PIPE(8, 3); else if (occ == 4) GMT_PIPE(8, 4); else GMT_PIPE(8, 1);
+      break;
   }
+#undef GMT_PIPE
+  (void)ok;
   GMT_RET_LAUNCH();
 }

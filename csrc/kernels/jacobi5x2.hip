@@ -193,7 +193,7 @@ extern "C" int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, cons
                              void* stream) {
   using namespace gmt;
   if ((tile & GMT_XK_PIPE) || (tile == 0 && nsweeps % 2 == 0))
-    return gmt_jacobi5xk_pipe(nsweeps, n_rect, rects, dom, halo_mask, u, un, ld, tile & 0xffff, stream);
+    return gmt_jacobi5xk_pipe(nsweeps, n_rect, rects, dom, halo_mask, u, un, ld, tile & 0xfffff, stream);
   if (nsweeps < 2 || nsweeps > 4) return static_cast<int>(hipErrorInvalidValue);
   if (n_rect < 0 || n_rect > 4) return static_cast<int>(hipErrorInvalidValue);
   if (!aligned16(u) || !aligned16(un) || (ld % 2) != 0) return static_cast<int>(hipErrorInvalidValue);
