@@ -12,11 +12,13 @@ N=2^28 fp64 on one MI355X") and the measured halo-exchange latency.
 
 One step = one full Jacobi sweep of the global domain (every point updated
 once).  The native engine (C++ + hipGraph replay, ``csrc/engine/jacobi.cpp``)
-runs the steps in pairs by default (temporal blocking, ``--tblock on``): one
-2-wide halo exchange (RCCL over xGMI on a high-priority stream, overlapped
-with the interior update) and one fused kernel that reads u(t) once and
-writes u(t+2) once — bitwise the same result as two single sweeps, half the
-HBM bytes.  ``--tblock off`` runs one exchange + one sweep per step;
+runs the steps in blocks of 8 by default (temporal blocking, ``--tblock on
+--tsteps 8``): one 8-wide halo exchange (RCCL over xGMI on a high-priority
+stream, overlapped with the interior update) and one fused pass of the
+register-pipelined kernel (``csrc/kernels/jacobi5pipe.hip``) that reads u(t)
+once and writes u(t+8) once — bitwise the same result as eight single
+sweeps, 1/8 of the HBM bytes.  100 steps = 12 fused 8-sweep passes + one
+4-sweep pass.  ``--tblock off`` runs one exchange + one sweep per step;
 ``--engine torch`` runs the single-sweep algorithm through torch.distributed
 P2P from Python.  Nothing is skipped inside the timed region: K steps are K
 sweeps of every lattice point (an odd K ends with one single sweep).
@@ -38,7 +40,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-DEFAULT_TSTEPS = 2  # fused sweeps per memory pass / halo exchange (native engine)
+DEFAULT_TSTEPS = 8  # fused sweeps per memory pass / halo exchange (native engine; profiles/r01_pipe.md)
 
 from gpu_mpi_tests_amd import ops  # noqa: E402
 from gpu_mpi_tests_amd.parallel import dist as gdist  # noqa: E402

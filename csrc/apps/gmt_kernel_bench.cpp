@@ -120,15 +120,16 @@ int main(int argc, char** argv) {
       GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, a.data(), ld2, s));
       GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, b.data(), ld2, s));
       const int64_t rect[4] = {xo, n, g, n};
-      for (int occ : {0, 3, 4})
-        for (int seg : {64, 128, 256, 512}) {
-          if (occ && K < 4) continue;
-          const int tile = GMT_XK_PIPE | (occ << 16) | seg;
+      for (int single : {0, 1})
+      for (int order : {1, 2})
+        for (int seg : {64, 128, 256}) {
+          const int tile = GMT_XK_PIPE | (single << 21) | (order << 19) | seg;
           const double ms = time_ms(s, iters, [&] {
             GMT_CHECK("pipe", gmt_jacobi5xk(K, 1, rect, rect, 0, a.data(), b.data(), ld2, tile, s));
           });
           char tag[64];
-          std::snprintf(tag, sizeof(tag), "%s x%d seg%d occ%d", shape, K, seg, occ);
+          std::snprintf(tag, sizeof(tag), "%s x%d seg%d %s%s", shape, K, seg, order == 1 ? "skew" : "chain",
+                        single ? " single" : "");
           report("jacobi5pipe", K, tag, ms, K * 16.0 * n * n);
         }
     }

@@ -13,6 +13,9 @@
 //   --host-init --host-verify   reference host loops instead of GPU fill/check
 //   --alloc-per-call      re-create halo buffers inside the timed region (gt parity)
 //   --json=FILE           one JSON record per test (per-exchange µs, GB/s, transport)
+//   --dim=0|1 --mem=device|managed --buf=0|1   run one slice of the test matrix
+//   --iters=N --warmup=W  (positional n_iter still wins when given; warmup default 5)
+//   --timeout=S           hang watchdog (gmt/watchdog.hpp)
 #include <mpi.h>
 
 #include <cstdio>
@@ -28,12 +31,15 @@ using namespace gmt::apps;
 int main(int argc, char** argv) {
   Cli cli(argc, argv);
   size_t n_local_deriv = 1024;
-  int n_iter = 1000;
-  const int n_warmup = 5;
+  int n_iter = static_cast<int>(cli.geti("iters", 1000));
+  const int n_warmup = static_cast<int>(cli.geti("warmup", 5));
   if (cli.positional(0)) n_local_deriv = std::atol(cli.positional(0));
   if (cli.positional(1)) n_iter = std::atoi(cli.positional(1));
+  const int only_dim = static_cast<int>(cli.geti("dim", -1));
+  const std::string only_mem = cli.get("mem", "");
+  const int only_buf = static_cast<int>(cli.geti("buf", -1));
   const size_t n_global_other = static_cast<size_t>(cli.geti("n-other", 512 * 1024));
-  const bool managed = !cli.flag("no-managed");
+  const bool managed = !cli.flag("no-managed") && only_mem != "device";
   const std::string tests = cli.get("tests", "deriv,sum");
   const std::string json = cli.get("json", "");
 
@@ -86,8 +92,11 @@ int main(int argc, char** argv) {
 
   if (tests.find("deriv") != std::string::npos) {
     for (int dim = 0; dim < 2; ++dim) {
+      if (only_dim >= 0 && dim != only_dim) continue;
       for (int m = 0; m < (managed ? 2 : 1); ++m) {
+        if (only_mem == "managed" && m == 0) continue;
         for (int buf = 1; buf >= 0; --buf) {
+          if (only_buf >= 0 && buf != only_buf) continue;
           DerivConfig c;
           c.dim = dim;
           c.n_local = n_local_deriv;
@@ -108,7 +117,9 @@ int main(int argc, char** argv) {
   }
   if (tests.find("sum") != std::string::npos) {
     for (int dim = 0; dim < 2; ++dim) {
+      if (only_dim >= 0 && dim != only_dim) continue;
       for (int m = 0; m < (managed ? 2 : 1); ++m) {
+        if (only_mem == "managed" && m == 0) continue;
         const int space = m ? GMT_SPACE_MANAGED : GMT_SPACE_DEVICE;
         SumResult r = run_sum(dim, space, n_local_deriv, n_global_other, n_iter, n_warmup, want,
                               b, pool);

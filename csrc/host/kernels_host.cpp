@@ -107,7 +107,7 @@ int gmt_fill_poly(int mode, int64_t nx, int64_t ny, double x0, double dx, double
   for (int64_t j = 0; j < ny; ++j)
     for (int64_t i = 0; i < nx; ++i) {
       const double x = x0 + i * dx, y = y0 + j * dy;
-      z[j * ld + i] = mode == 0 ? x * x * x + y * y : (mode == 1 ? 3 * x * x : 2 * y);
+      z[j * ld + i] = mode == 0 ? x * x * x + y * y : (mode == 1 ? 3 * x * x : (mode == 2 ? 2 * y : x));
     }
   return 0;
 }

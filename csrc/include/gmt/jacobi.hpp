@@ -41,7 +41,8 @@ struct JacobiConfig {
   bool overlap = true;
   bool graph = false;
   int variant = 0;                               // gmt_jacobi5_set_variant
-  // temporal blocking: tsteps (2-4) sweeps per memory pass (gmt_jacobi5xk)
+  // temporal blocking: tsteps (2-8) sweeps per memory pass (gmt_jacobi5xk;
+  // even counts run the register-pipelined kernel, 3 the LDS-tiled one)
   // and per halo exchange (ghost width tsteps, corners via a two-phase
   // exchange) — 1/tsteps of the HBM bytes and messages per lattice update.
   // 1 = off.  tblock = true is tsteps = 2.

@@ -82,7 +82,7 @@ int gmt_diff_sq(int64_t nx, int64_t ny, const double* a, int64_t lda, const doub
 /* ---- analytic fill z[y][x] = (x0+i*dx)^3 + (y0+j*dy)^2 over nx x ny (device
  *      side replacement of the reference's host init loops,
  *      mpi_stencil2d_gt.cc:439-497).  mode 0: x^3+y^2 (z), 1: 3x^2 (dz/dx),
- *      2: 2y (dz/dy). */
+ *      2: 2y (dz/dy), 3: x (linear ramp; DAXPY inputs). */
 int gmt_fill_poly(int mode, int64_t nx, int64_t ny, double x0, double dx, double y0,
                   double dy, double* z, int64_t ld, void* stream);
 
@@ -115,16 +115,17 @@ int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int halo
 /* The same for nsweeps = 2..8 fused sweeps (u valid on rect + nsweeps;
  * ghost width >= nsweeps).  gmt_jacobi5x2 == gmt_jacobi5xk(2, ...).
  * Two kernels: the register-pipelined one (jacobi5pipe.hip, even nsweeps;
- * tile = GMT_XK_PIPE | (occ << 16) | rows-per-wave, occ = waves-per-SIMD hint
- * 3/4 or 0; or tile = 0 with an even nsweeps) and
+ * tile = GMT_XK_PIPE | (pipe << 19) | rows-per-wave, pipe 0 = default, 1 =
+ * skewed, 2 = chained level order; or tile = 0 with an even nsweeps) and
  * the LDS-tiled one (jacobi5x2.hip, nsweeps 2..4; tile = (TX << 16) | TY,
  * or tile = 0 with nsweeps = 3). */
 #define GMT_XK_PIPE 0x40000000
 int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
                   const double* u, double* un, int64_t ld, int tile, void* stream);
 /* Register-pipelined K-sweep kernel: one wave per 128-column strip and
- * `seg & 0xffff` output rows (0 = 256), `(seg >> 16) & 0xf` = waves-per-SIMD
- * register-allocation hint (0 = none); nsweeps even, 2..8. */
+ * `seg & 0xffff` output rows (0 = auto: 256, fewer for small rects),
+ * `(seg >> 19) & 3` = level order (0 default, 1 skewed, 2 chained);
+ * nsweeps even, 2..8. */
 int gmt_jacobi5xk_pipe(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom,
                        int halo_mask, const double* u, double* un, int64_t ld, int seg,
                        void* stream);

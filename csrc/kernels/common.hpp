@@ -28,15 +28,16 @@ __device__ __forceinline__ void st2_nt(double* p, d2 v) {
 }
 
 // Whole-wave lane shifts of a double through DPP (wave_shr:1 / wave_shl:1, a
-// VALU source modifier: no LDS traffic).  The edge lane receives 0.
+// VALU source modifier: no LDS traffic).  bound_ctrl: the edge lane reads 0
+// without an "old" operand, so no zero-initialising v_mov per shift.
 __device__ __forceinline__ double dpp_from_lower(double v) {  // lane i <- lane i-1
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xf, 0xf, true);
   return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double dpp_from_upper(double v) {  // lane i <- lane i+1
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x130, 0xf, 0xf, true);
   return __hiloint2double(hi, lo);
 }
 

@@ -166,8 +166,10 @@ __global__ __launch_bounds__(kBlock) void fill_poly_kernel(int mode, int64_t nx,
     v = x * x * x + y * y;
   else if (mode == 1)
     v = 3 * x * x;
-  else
+  else if (mode == 2)
     v = 2 * y;
+  else
+    v = x;
   z[iy * ld + ix] = v;
 }
 

@@ -327,7 +327,7 @@ def test_jacobi5xk_fused_k_sweeps(k, tile, ny, nx, mask):
 
 
 @pytest.mark.parametrize("k", [2, 4, 6, 8])
-@pytest.mark.parametrize("seg", [0, 1, 5, 64])
+@pytest.mark.parametrize("seg", [0, 1, 5, 64, (1 << 19) | 7, (1 << 19) | 64, (2 << 19) | 33, (2 << 19) | 3])
 @pytest.mark.parametrize("ny,nx", [(1, 2), (7, 9), (40, 126), (33, 130), (70, 515)])
 @pytest.mark.parametrize("mask", [0, 15, 6, 9])
 def test_jacobi5xk_pipelined(k, seg, ny, nx, mask):

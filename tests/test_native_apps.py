@@ -53,6 +53,25 @@ def test_mpi_daxpy_memory_per_core_env():
     assert "MEMORY_PER_CORE=4096" in out
 
 
+@pytest.mark.parametrize("np_", [1, 3])
+def test_mpi_daxpy_bench_allreduce(np_, tmp_path):
+    """BASELINE config "mpi_daxpy N ranks x 1 GPU, allreduce of partial sums":
+    timed DAXPY + device partial sum + transport all-reduce, ALLSUM checked."""
+    j = tmp_path / "d.jsonl"
+    out = run_app("mpi_daxpy", "--bench=50000", "--iters=4", f"--json={j}", np=np_).stdout
+    assert re.search(r"BENCH daxpy n=50000 per rank x %d ranks: [\d.]+ ms/call" % np_, out)
+    m = re.search(r"ALLSUM = (\S+) \(expected (\S+), rel err \S+\) OK", out)
+    assert m and abs(float(m.group(1)) - 9 * 50001 / 2 * np_) < 1e-6 * np_ * 50001 * 9
+    import json
+    rec = json.loads(j.read_text().splitlines()[0])
+    assert rec["ranks"] == np_ and rec["GBps_aggregate"] > 0
+
+
+def test_mpi_stencil2d_alias():
+    out = run_app("mpi_stencil2d", "40", "4", "--check", np=2).stdout
+    assert "OK" in out and "MLUPS" in out
+
+
 def test_mpi_daxpy_gt_every_rank():
     out = run_app("mpi_daxpy_gt", np=3).stdout
     for r in range(3):
@@ -145,6 +164,16 @@ def test_mpi_stencil2d_gt_transport_parity(transport):
     assert len(tests) == 4
     for *_, err in tests:
         assert float(err) < 1e-5
+
+
+def test_mpi_stencil2d_gt_matrix_slice():
+    """--dim/--mem/--buf select one cell of the reference's test matrix."""
+    out = run_app("mpi_stencil2d_gt", "32", "--iters=3", "--warmup=1", "--n-other=128", "--dim=1",
+                  "--mem=managed", "--buf=0", np=2).stdout
+    tests = _TEST_RE.findall(out)
+    assert [(d, m, b) for d, m, b, _, _ in tests] == [("1", "managed", "0")]
+    assert [(d, m) for d, m, _ in _SUM_RE.findall(out)] == [("1", "managed")]
+    assert "n_iter         = 3" in out and "n_warmup       = 1" in out
 
 
 def test_mpi_stencil2d_gt_json(tmp_path):
