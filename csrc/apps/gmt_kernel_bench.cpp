@@ -113,23 +113,38 @@ int main(int argc, char** argv) {
       }
     }
     // register-pipelined K-sweep kernel: rows per wave
-    for (int K = 2; K <= 8 && sec.find("pipe") != std::string::npos; K += 2) {
-      const int64_t g = K;
-      const int64_t ld2 = ((xo + n + g + 63) / 64) * 64;
+    for (int K = 2; K <= 12 && sec.find("pipe") != std::string::npos; K += 2) {
+      const int64_t g = K, xk = g > xo ? g : xo;  // the K-wide ring fits left of the interior
+      const int64_t ld2 = ((xk + n + g + 63) / 64) * 64;
       Buffer<double> a(static_cast<size_t>(ld2) * (n + 2 * g), GMT_SPACE_DEVICE), b(a.size(), GMT_SPACE_DEVICE);
       GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, a.data(), ld2, s));
       GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, b.data(), ld2, s));
-      const int64_t rect[4] = {xo, n, g, n};
-      for (int single : {0, 1})
+      const int64_t rect[4] = {xk, n, g, n};
+      // launch: 0 = rule bands split off (default), 1 = per-wave split over
+      // two launches, 2 = one kernel for both paths
+      static const char* lname[] = {"", " nosplit", " single"};
+      for (int launch : {0, 1, 2})
       for (int order : {1, 2})
         for (int seg : {64, 128, 256}) {
-          const int tile = GMT_XK_PIPE | (single << 21) | (order << 19) | seg;
+          const int tile = GMT_XK_PIPE | (launch == 2 ? 1 << 21 : 0) | (launch == 1 ? 1 << 22 : 0) |
+                           (order << 19) | seg;
           const double ms = time_ms(s, iters, [&] {
             GMT_CHECK("pipe", gmt_jacobi5xk(K, 1, rect, rect, 0, a.data(), b.data(), ld2, tile, s));
           });
           char tag[64];
           std::snprintf(tag, sizeof(tag), "%s x%d seg%d %s%s", shape, K, seg, order == 1 ? "skew" : "chain",
-                        single ? " single" : "");
+                        lname[launch]);
+          report("jacobi5pipe", K, tag, ms, K * 16.0 * n * n);
+        }
+      // rows per rule-band wave (split launch, default level order)
+      for (int rr : {4, 8, 32})
+        for (int seg : {64, 128, 256}) {
+          const int tile = GMT_XK_PIPE | (rr << 23) | seg;
+          const double ms = time_ms(s, iters, [&] {
+            GMT_CHECK("pipe", gmt_jacobi5xk(K, 1, rect, rect, 0, a.data(), b.data(), ld2, tile, s));
+          });
+          char tag[64];
+          std::snprintf(tag, sizeof(tag), "%s x%d seg%d rule%d", shape, K, seg, rr);
           report("jacobi5pipe", K, tag, ms, K * 16.0 * n * n);
         }
     }

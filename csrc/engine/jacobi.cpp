@@ -1,8 +1,10 @@
 // Native distributed Jacobi engine (gmt/jacobi.hpp).
 #include "gmt/jacobi.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <vector>
 
 namespace gmt {
 
@@ -48,10 +50,11 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   nb_.north = cy < c.py - 1 ? at(cy + 1, cx) : (c.periodic ? at(0, cx) : -1);
 
   ks_ = c.tsteps > 1 ? c.tsteps : (c.tblock ? 2 : 1);
-  if (ks_ > 8) ks_ = 8;
-  if (ks_ > 4 && ks_ % 2) --ks_;  // 5..8 sweeps: register-pipelined kernel, even counts only
+  if (ks_ > 12) ks_ = 12;
+  if (ks_ > 4 && ks_ % 2) --ks_;  // 5..12 sweeps: register-pipelined kernel, even counts only
   g_ = ks_;
   yo_ = g_;
+  xo_ = round_up(g_, 8);  // ghost columns fit left of the interior; 64-B aligned interior
   ld_ = round_up(xo_ + nx_ + g_, 64);
   const size_t elems = static_cast<size_t>(ld_) * (ny_ + 2 * g_);
   GMT_CHECK("stream", gmt_rt_stream_create(&s_, 0));
@@ -180,19 +183,49 @@ void JacobiSolver::step_block() {
   parity_ ^= 1;  // u(t+ks) lives in the other buffer
 }
 
+// Relative cost of one fused pass of K sweeps on a large domain (ms at
+// 32768², gmt_kernel_bench, profiles/r01_k12.md): per-pass time is nearly
+// flat in K up to 8 (HBM-bound: one read + one write of the field), so a
+// remainder is cheaper as two 8-passes than as a 12-pass plus a 4-pass.
+// 0 = no kernel for that K (odd K > 3).
+static constexpr double kPassCost[13] = {0, 3.05, 3.5, 4.5, 3.3, 0, 3.7, 0, 3.22, 0, 3.65, 0, 4.0};
+static constexpr double kPassOverhead = 0.05;  // launches + one halo exchange
+
+std::vector<int> JacobiSolver::plan_passes(int k) const {
+  std::vector<int> plan;
+  if (k <= 0) return plan;
+  if (ks_ <= 1) return std::vector<int>(k, 1);
+  std::vector<double> best(k + 1, 1e300);
+  std::vector<int> pick(k + 1, 0);
+  best[0] = 0.0;
+  for (int s = 1; s <= k; ++s)
+    for (int K = 1; K <= ks_ && K <= s; ++K) {
+      if (kPassCost[K] <= 0) continue;
+      const double c = best[s - K] + kPassCost[K] + kPassOverhead;
+      if (c < best[s]) {
+        best[s] = c;
+        pick[s] = K;
+      }
+    }
+  for (int s = k; s > 0; s -= pick[s]) plan.push_back(pick[s]);
+  // full ks_ passes first (graph replays), then the rest, largest first
+  std::sort(plan.begin(), plan.end(), [&](int a, int b) {
+    return (a == ks_) != (b == ks_) ? a == ks_ : a > b;
+  });
+  return plan;
+}
+
 void JacobiSolver::run(int k) {
-  if (ks_ > 1) {
-    for (; k >= ks_; k -= ks_) step_block();
-    // remainder: one shorter fused pass (eager; the ks-wide halo covers it)
-    // — even counts on the pipelined kernel, 3 on the LDS-tiled one
-    const int r = (k % 2 == 0 || k == 3) ? k : k - 1;
-    if (r >= 2) {
-      enqueue_block(parity_, r);
+  for (int K : plan_passes(k)) {
+    if (K == 1) {
+      step();
+    } else if (K == ks_) {
+      step_block();
+    } else {
+      enqueue_block(parity_, K);  // eager; the ks-wide halo covers it
       parity_ ^= 1;
-      k -= r;
     }
   }
-  for (; k > 0; --k) step();
   watchdog_kick("jacobi steps enqueued");
 }
 

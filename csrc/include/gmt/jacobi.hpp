@@ -27,6 +27,7 @@
 #pragma once
 
 #include <memory>
+#include <vector>
 
 #include "gmt/buffer.hpp"
 #include "gmt/halo.hpp"
@@ -41,7 +42,7 @@ struct JacobiConfig {
   bool overlap = true;
   bool graph = false;
   int variant = 0;                               // gmt_jacobi5_set_variant
-  // temporal blocking: tsteps (2-8) sweeps per memory pass (gmt_jacobi5xk;
+  // temporal blocking: tsteps (2-12) sweeps per memory pass (gmt_jacobi5xk;
   // even counts run the register-pipelined kernel, 3 the LDS-tiled one)
   // and per halo exchange (ghost width tsteps, corners via a two-phase
   // exchange) — 1/tsteps of the HBM bytes and messages per lattice update.
@@ -59,7 +60,9 @@ class JacobiSolver {
   JacobiSolver& operator=(const JacobiSolver&) = delete;
 
   void step();  // one sweep, asynchronous (compute stream)
-  void run(int k);  // k sweeps: pairs through the fused kernel when tblock
+  void run(int k);  // k sweeps through the fused kernel (plan_passes) when tblock
+  // cheapest sequence of fused passes (sweeps per pass <= tsteps) covering k sweeps
+  std::vector<int> plan_passes(int k) const;
   void synchronize();
   // sqrt(global sum (u_{k+1} - u_k)^2) of one extra sweep (advances the solution)
   double residual();

@@ -27,25 +27,43 @@
 // is updated only if that side's ghost cells belong to a neighbour
 // (halo_mask bit0..3 = W/E/S/N); otherwise it keeps its (boundary) value.
 // Waves whose influence cone stays inside the interior skip the rule.
+#include <algorithm>
+
 #include "common.hpp"
 #include "gmt/kernels.h"
 
 namespace gmt {
 
+// An input rect is split on the host into a fast core (full strips whose
+// influence cone stays inside the interior) and up to 4 rule bands around it.
+// The bands get short segments, so the few ghost-rule waves (branchy: about
+// one HBM latency per step) finish in tens of microseconds instead of one
+// long segment's worth (0.68 ms of a 4.2 ms pass at 256 rows per wave,
+// profiles/r01_pipe.md).
+constexpr int kMaxPipeRect = 20;
+
 struct PipeArgs {
-  int64_t r[4][4];     // output rects: x0, nx, y0, ny (absolute array coordinates, x0 even)
-  int64_t nstrip[4];   // strips per rect
-  int64_t wstart[5];   // prefix sum of waves (strips x segments)
+  int64_t r[kMaxPipeRect][4];        // output rects: x0, nx, y0, ny (absolute array coordinates, x0 even)
+  int64_t nstrip[kMaxPipeRect];      // strips per rect
+  int64_t wstart[kMaxPipeRect + 1];  // prefix sum of waves (strips x segments)
   int64_t dom[4];      // interior: x0, nx, y0, ny
+  int64_t wbase, wend; // this launch runs waves [wbase, wend)
   int n;
   int mask;
-  int seg[4];          // output rows per wave, per rect
+  int classified;      // 1: rect order = rule rects, then fast cores (no per-wave test)
+  int seg[kMaxPipeRect];  // output rows per wave, per rect
   double quarter;      // 0.25 as a kernel argument: an SGPR operand (v_fma_f64 /
                        // v_mul_f64 with s[..]) instead of a literal that forces
                        // VOP2 v_fmac + a v_mov_b64 copy per use
 };
 
 constexpr int kPipeCols = 2 * kWave;  // columns per strip
+constexpr int kPipeMaxK = 12;         // sweeps per pass (even): K = 12 keeps 2 waves per SIMD
+
+// Waves per SIMD the fast path is held to (512 VGPRs / waves).  Without the
+// bound the scheduler interleaves all K independent levels of a step and the
+// temporaries push K = 10 to 232 VGPRs (2 waves) instead of ~166 (3 waves).
+constexpr int pipe_waves(int K, int mode) { return mode != 1 || K <= 8 ? 1 : (K <= 10 ? 3 : 2); }
 
 template <int I, int N, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -76,54 +94,51 @@ __device__ __forceinline__ void pipe_strip(const PipeArgs& a, const double* __re
   const int64_t c0 = xa + 2 * lane;   // this lane's columns c0, c0 + 1
   const int64_t dx0 = a.dom[0], dx1 = a.dom[0] + a.dom[1];
   const int64_t dy0 = a.dom[2], dy1 = a.dom[2] + a.dom[3];
-  const int64_t xlim = dx1 + K, ylim = dy1 + K;  // first column / row past the stored ring
   const bool gw = a.mask & 1, ge = a.mask & 2, gs = a.mask & 4, gn = a.mask & 8;
   // per-lane column rule (!FAST only)
   const bool rx0 = (c0 >= dx0 && c0 < dx1) || (c0 < dx0 ? gw : ge);
   const bool rx1 = (c0 + 1 >= dx0 && c0 + 1 < dx1) || (c0 + 1 < dx0 ? gw : ge);
-  // load mask: whole pair, first column only, or nothing (!FAST only)
-  const int lmode = c0 + 1 < xlim ? 2 : (c0 < xlim ? 1 : 0);
   // store mask
   const bool st0 = c0 >= xs && c0 < xe, st1 = c0 + 1 >= xs && c0 + 1 < xe;
 
   const int64_t yl = ys - K;  // row loaded at step 0
   const int nload = static_cast<int>(ye - ys) + 2 * K;
   const int nsteps = static_cast<int>(ye - ys) + K + LAG;
-  const double* up = u + yl * ld + c0;
-
+  // Both paths load unconditionally (no branch around a load, see FAST).
+  // Rows past the segment's last row are clamped to it, and lanes past the
+  // array row (right-edge strips) to its last column pair: those values, and
+  // anything outside the ghost ring, only feed cells whose K-step cone ends
+  // outside the interior — never a stored output.
+  const double* up = u + yl * ld + (FAST ? c0 : (c0 < ld - 2 ? c0 : ld - 2));
   auto load = [&](int s) -> d2 {
-    if constexpr (FAST) {
-      const int sc = s < nload ? s : nload - 1;  // tail: re-read the last row (unused)
-      return ld2(up + static_cast<int64_t>(sc) * ld);
-    } else {
-      d2 v = {0.0, 0.0};
-      if (s < nload && yl + s < ylim) {
-        const double* p = up + static_cast<int64_t>(s) * ld;
-        if (lmode == 2)
-          v = ld2(p);
-        else if (lmode == 1)
-          v.x = p[0];
-      }
-      return v;
-    }
+    const int sc = s < nload ? s : nload - 1;  // tail: re-read the last row (unused)
+    return ld2(up + static_cast<int64_t>(sc) * ld);
   };
-  const uint32_t st_off = (st0 && st1) ? static_cast<uint32_t>(c0 - xs) * 8u : 0x80000000u;
+  // stores through a raw buffer descriptor spanning [xs, xe) of the row: an
+  // out-of-range offset (0x80000000) makes the store a no-op, so edge lanes
+  // need no branch either
+  constexpr uint32_t kDrop = 0x80000000u;
+  const uint32_t st_off = (st0 && st1) ? static_cast<uint32_t>(c0 - xs) * 8u : kDrop;
+  const uint32_t st_off0 = st0 ? static_cast<uint32_t>(c0 - xs) * 8u : kDrop;
+  const uint32_t st_off1 = st1 ? static_cast<uint32_t>(c0 + 1 - xs) * 8u : kDrop;
   const uint32_t st_bytes = static_cast<uint32_t>(xe - xs) * 8u;
   auto store = [&](int s, d2 v) {
     double* row = un + (yl + s - LAG) * ld;
+    // 0x00020000: raw-buffer descriptor word 3 for gfx9 (32-bit data format)
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(row + xs, 0, st_bytes, 0x00020000);
     if constexpr (FAST) {
-      // 0x00020000: raw-buffer descriptor word 3 for gfx9 (32-bit data format)
-      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(row + xs, 0, st_bytes, 0x00020000);
       typedef unsigned u4 __attribute__((ext_vector_type(4)));
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, st_off, 0, 2 /* nt */);
     } else {
-      double* q = row + c0;
-      if (st0 && st1)
-        st2_nt(q, v);
-      else if (st0)
-        q[0] = v.x;
-      else if (st1)
-        q[1] = v.y;
+      // odd rect edges leave single-column lanes: two 8-B stores
+      // (the halves are built explicitly: bit_cast of the two vector
+      // elements was folded into one register pair by clang 22)
+      typedef unsigned u2 __attribute__((ext_vector_type(2)));
+      const double vx = v.x, vy = v.y;
+      const u2 bx = {static_cast<unsigned>(__double2loint(vx)), static_cast<unsigned>(__double2hiint(vx))};
+      const u2 by = {static_cast<unsigned>(__double2loint(vy)), static_cast<unsigned>(__double2hiint(vy))};
+      __builtin_amdgcn_raw_buffer_store_b64(bx, r, st_off0, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b64(by, r, st_off1, 0, 2);
     }
   };
 
@@ -167,6 +182,9 @@ __device__ __forceinline__ void pipe_strip(const PipeArgs& a, const double* __re
           W[p][cur] = v;
         else
           out = v;
+        // K > 8: keep the levels in order (a fence for the scheduler only),
+        // else their interleaved temporaries cost a wave per SIMD
+        if constexpr (K > 8) __builtin_amdgcn_sched_barrier(0);
       }
       W[0][cur] = Q[cur];
       Q[cur] = load(s + 3);
@@ -209,15 +227,15 @@ __device__ __forceinline__ void pipe_strip(const PipeArgs& a, const double* __re
 // MODE 0: both paths in one kernel (A/B measurement), 1: fast waves only,
 // 2: the other waves only.
 template <int K, bool SKEW, int MODE>
-__global__ __launch_bounds__(kBlock)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(pipe_waves(K, MODE))))
 void jacobi5pipe_kernel(PipeArgs a, const double* __restrict__ u, double* __restrict__ un, int64_t ld,
                         int64_t nblocks) {
   const int lane = threadIdx.x & (kWave - 1);
   // readfirstlane: the wave index is uniform, so everything derived from it
   // (strip, rows, buffer descriptors) lives in SGPRs
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
-  const int64_t wid = xcd_swizzle(blockIdx.x, nblocks) * (kBlock / kWave) + wave;
-  if (wid >= a.wstart[a.n]) return;  // whole wave
+  const int64_t wid = a.wbase + xcd_swizzle(blockIdx.x, nblocks) * (kBlock / kWave) + wave;
+  if (wid >= a.wend) return;  // whole wave
   int k = 0;
   while (k + 1 < a.n && wid >= a.wstart[k + 1]) ++k;
   const int64_t lt = wid - a.wstart[k];
@@ -241,87 +259,138 @@ void jacobi5pipe_kernel(PipeArgs a, const double* __restrict__ u, double* __rest
       pipe_strip<K, false, SKEW>(a, u, un, ld, lane, xs, xe, ys, ye);
     return;
   }
-  if (fast != (MODE == 1)) return;
+  if (!a.classified && fast != (MODE == 1)) return;
   pipe_strip<K, MODE == 1, SKEW>(a, u, un, ld, lane, xs, xe, ys, ye);
 }
 
 }  // namespace gmt
 
-// nsweeps even, 2..8; seg = output rows per wave (0 = default).
+namespace {
+
+// Split rect r into the fast core (whole strips whose K-step influence cone
+// stays inside dom) and the rule bands around it: top, bottom, left, right.
+// Returns false if the core is empty; r then stays one rule rect.
+bool split_rect(const int64_t* r, const int64_t* dom, int K, int64_t wout, int64_t core[4],
+                int64_t band[4][4]) {
+  const int64_t x0 = r[0], x1 = r[0] + r[1], y0 = r[2], y1 = r[2] + r[3];
+  const int64_t fy0 = std::max(y0, dom[2] + K), fy1 = std::min(y1, dom[2] + dom[3] - K);
+  int64_t fx0 = std::max(x0, dom[0] + K);
+  fx0 += fx0 & 1;  // even: 16-B loads
+  const int64_t fx1 = std::min(x1, dom[0] + dom[1] - K);
+  if (fy1 <= fy0 || fx1 - fx0 < wout) return false;
+  const int64_t cx1 = fx0 + (fx1 - fx0) / wout * wout;
+  const int64_t c[4] = {fx0, cx1 - fx0, fy0, fy1 - fy0};
+  const int64_t b[4][4] = {{x0, x1 - x0, y0, fy0 - y0},
+                           {x0, x1 - x0, fy1, y1 - fy1},
+                           {x0, fx0 - x0, fy0, fy1 - fy0},
+                           {cx1, x1 - cx1, fy0, fy1 - fy0}};
+  for (int j = 0; j < 4; ++j) {
+    core[j] = c[j];
+    for (int i = 0; i < 4; ++i) band[i][j] = b[i][j];
+  }
+  return true;
+}
+
+}  // namespace
+
+// nsweeps even, 2..8; seg & 0xffff = output rows per fast-core wave (0 = default).
 extern "C" int gmt_jacobi5xk_pipe(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom,
                                   int halo_mask, const double* u, double* un, int64_t ld, int seg,
                                   void* stream) {
   using namespace gmt;
-  if (nsweeps < 2 || nsweeps > 8 || (nsweeps % 2) != 0) return static_cast<int>(hipErrorInvalidValue);
+  if (nsweeps < 2 || nsweeps > kPipeMaxK || (nsweeps % 2) != 0) return static_cast<int>(hipErrorInvalidValue);
   if (n_rect < 0 || n_rect > 4) return static_cast<int>(hipErrorInvalidValue);
   if (!aligned16(u) || !aligned16(un) || (ld % 2) != 0) return static_cast<int>(hipErrorInvalidValue);
   PipeArgs a{};
   const int seg_rows = seg & 0xffff;
+  const int sk = (seg >> 19) & 3;         // 0 = per-K default, 1 = skewed, 2 = chained pipeline
+  const bool single = (seg >> 21) & 1;    // one kernel for both paths (A/B)
+  const bool nosplit = (seg >> 22) & 1;   // two kernels, per-wave classification (A/B)
+  const int rule_rows = (seg >> 23) & 0x3f ? (seg >> 23) & 0x3f : (nsweeps >= 10 ? 32 : 16);
+  const bool classified = !single && !nosplit;
   a.quarter = 0.25;
   a.mask = halo_mask;
+  a.classified = classified;
   for (int j = 0; j < 4; ++j) a.dom[j] = dom[j];
-  const int wout = kPipeCols - 2 * nsweeps;
-  int64_t nfast = 0, nrule = 0;
+  const int64_t wout = kPipeCols - 2 * nsweeps;
+  // rule rects first, then the fast cores: each kernel's waves are one range
+  int64_t rl[kMaxPipeRect][4], fl[kMaxPipeRect][4];
+  int nr = 0, nf = 0;
   for (int k = 0; k < n_rect; ++k) {
     const int64_t* r = rects + 4 * k;
     if (r[1] <= 0 || r[3] <= 0) continue;
     if ((r[0] % 2) != 0) return static_cast<int>(hipErrorInvalidValue);  // 16-B loads
+    // the K-wide ring left of / above the rect must exist (relative to u)
+    if (r[0] < nsweeps || r[2] < nsweeps) return static_cast<int>(hipErrorInvalidValue);
+    int64_t core[4], band[4][4];
+    if (classified && split_rect(r, dom, nsweeps, wout, core, band)) {
+      std::copy(core, core + 4, fl[nf++]);
+      for (auto& b : band)
+        if (b[1] > 0 && b[3] > 0) std::copy(b, b + 4, rl[nr++]);
+    } else {
+      std::copy(r, r + 4, rl[nr++]);
+    }
+  }
+  auto add = [&](const int64_t* r, bool rule) {
     for (int j = 0; j < 4; ++j) a.r[a.n][j] = r[j];
     a.nstrip[a.n] = (r[1] + wout - 1) / wout;
-    // default segment: 256 rows, halved (down to 16) while the rect would
-    // give fewer than ~4096 waves — thin frame rects and small domains still
-    // fill 256 CUs (the pipeline refill costs 2K extra rows per segment)
-    int sg = seg_rows;
+    // fast core: 128 rows per wave at K = 6..10, else 256, halved (down to
+    // 16) while the rect would give fewer than ~4096 waves (small domains
+    // still fill 256 CUs; the pipeline refill costs 2K extra rows per
+    // segment).  Rule bands: 16 rows, 32 at K >= 10 (or (seg >> 23) & 63) —
+    // latency-bound waves, so many short ones (measured, profiles/r01_k12.md).
+    int sg = rule && classified ? rule_rows : seg_rows;
     if (sg <= 0) {
-      sg = 256;
+      sg = nsweeps >= 6 && nsweeps < 12 ? 128 : 256;
       while (sg > 16 && a.nstrip[a.n] * ((r[3] + sg - 1) / sg) < 4096) sg /= 2;
     }
     a.seg[a.n] = sg;
-    const int64_t nseg = (r[3] + sg - 1) / sg;
-    a.wstart[a.n + 1] = a.wstart[a.n] + a.nstrip[a.n] * nseg;
-    // waves the kernel will classify as fast (same predicate as the device)
-    int64_t fx = 0, fy = 0;
-    for (int64_t i = 0; i < a.nstrip[a.n]; ++i) {
-      const int64_t xs = r[0] + i * wout, xe = xs + wout;
-      fx += xe <= r[0] + r[1] && xs - nsweeps >= dom[0] && xe + nsweeps <= dom[0] + dom[1];
-    }
-    for (int64_t i = 0; i < nseg; ++i) {
-      const int64_t ys = r[2] + i * sg, ye = ys + sg < r[2] + r[3] ? ys + sg : r[2] + r[3];
-      fy += ys - nsweeps >= dom[2] && ye + nsweeps <= dom[2] + dom[3];
-    }
-    nfast += fx * fy;
-    nrule += a.nstrip[a.n] * nseg - fx * fy;
+    a.wstart[a.n + 1] = a.wstart[a.n] + a.nstrip[a.n] * ((r[3] + sg - 1) / sg);
     ++a.n;
-  }
-  if (a.n == 0) return 0;
-  for (int k = a.n + 1; k <= 4; ++k) a.wstart[k] = a.wstart[a.n];
+  };
+  for (int i = 0; i < nr; ++i) add(rl[i], true);
+  const int64_t nrule = a.wstart[a.n];
+  for (int i = 0; i < nf; ++i) add(fl[i], false);
   const int64_t waves = a.wstart[a.n];
-  const int64_t nb = (waves + kBlock / kWave - 1) / (kBlock / kWave);
+  if (waves == 0) return 0;
+  for (int k = a.n + 1; k <= kMaxPipeRect; ++k) a.wstart[k] = a.wstart[a.n];
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const unsigned g = grid_1d(nb);
-  const int sk = (seg >> 19) & 3;  // 0 = per-K default, 1 = skewed, 2 = chained pipeline
+  constexpr int64_t wpb = kBlock / kWave;
   // skewed (level-parallel) pipeline by default: fewer VGPRs for the fast
   // path at K = 6, 8 (measured, profiles/r01_pipe.md)
   const bool skew = sk == 0 ? nsweeps >= 6 : sk == 1;
-  const bool single = (seg >> 21) & 1;  // one kernel for both paths (A/B)
-#define GMT_PIPE(KK)                                                                        \
-  do {                                                                                      \
-    if (single) {                                                                           \
-      if (skew) jacobi5pipe_kernel<KK, true, 0><<<g, kBlock, 0, s>>>(a, u, un, ld, nb);     \
-      else jacobi5pipe_kernel<KK, false, 0><<<g, kBlock, 0, s>>>(a, u, un, ld, nb);         \
-      break;                                                                                \
-    }                                                                                       \
-    if (nrule && skew) jacobi5pipe_kernel<KK, true, 2><<<g, kBlock, 0, s>>>(a, u, un, ld, nb);   \
-    if (nrule && !skew) jacobi5pipe_kernel<KK, false, 2><<<g, kBlock, 0, s>>>(a, u, un, ld, nb); \
-    if (nfast && skew) jacobi5pipe_kernel<KK, true, 1><<<g, kBlock, 0, s>>>(a, u, un, ld, nb);    \
-    if (nfast && !skew) jacobi5pipe_kernel<KK, false, 1><<<g, kBlock, 0, s>>>(a, u, un, ld, nb);  \
-  } while (0)
+  auto launch = [&](auto KC, auto MC, int64_t w0, int64_t w1) {
+    constexpr int KK = decltype(KC)::value, MODE = decltype(MC)::value;
+    if (w1 <= w0) return;
+    a.wbase = w0;
+    a.wend = w1;
+    const int64_t nb = (w1 - w0 + wpb - 1) / wpb;
+    if (skew)
+      jacobi5pipe_kernel<KK, true, MODE><<<grid_1d(nb), kBlock, 0, s>>>(a, u, un, ld, nb);
+    else
+      jacobi5pipe_kernel<KK, false, MODE><<<grid_1d(nb), kBlock, 0, s>>>(a, u, un, ld, nb);
+  };
+  auto run = [&](auto KC) {
+    using M0 = std::integral_constant<int, 0>;
+    using M1 = std::integral_constant<int, 1>;
+    using M2 = std::integral_constant<int, 2>;
+    if (single) {
+      launch(KC, M0{}, 0, waves);
+    } else if (nosplit) {  // both kernels over every wave, each keeps its own
+      launch(KC, M2{}, 0, waves);
+      launch(KC, M1{}, 0, waves);
+    } else {
+      launch(KC, M2{}, 0, nrule);
+      launch(KC, M1{}, nrule, waves);
+    }
+  };
   switch (nsweeps) {
-    case 2: GMT_PIPE(2); break;
-    case 4: GMT_PIPE(4); break;
-    case 6: GMT_PIPE(6); break;
-    default: GMT_PIPE(8); break;
+    case 2: run(std::integral_constant<int, 2>{}); break;
+    case 4: run(std::integral_constant<int, 4>{}); break;
+    case 6: run(std::integral_constant<int, 6>{}); break;
+    case 8: run(std::integral_constant<int, 8>{}); break;
+    case 10: run(std::integral_constant<int, 10>{}); break;
+    default: run(std::integral_constant<int, 12>{}); break;
   }
-#undef GMT_PIPE
   GMT_RET_LAUNCH();
 }

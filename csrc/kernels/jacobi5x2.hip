@@ -193,7 +193,7 @@ extern "C" int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, cons
                              void* stream) {
   using namespace gmt;
   if ((tile & GMT_XK_PIPE) || (tile == 0 && nsweeps % 2 == 0))
-    return gmt_jacobi5xk_pipe(nsweeps, n_rect, rects, dom, halo_mask, u, un, ld, tile & 0xfffff, stream);
+    return gmt_jacobi5xk_pipe(nsweeps, n_rect, rects, dom, halo_mask, u, un, ld, tile & ~GMT_XK_PIPE, stream);
   if (nsweeps < 2 || nsweeps > 4) return static_cast<int>(hipErrorInvalidValue);
   if (n_rect < 0 || n_rect > 4) return static_cast<int>(hipErrorInvalidValue);
   if (!aligned16(u) || !aligned16(un) || (ld % 2) != 0) return static_cast<int>(hipErrorInvalidValue);
@@ -207,6 +207,8 @@ extern "C" int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, cons
     const int64_t* r = rects + 4 * k;
     if (r[1] <= 0 || r[3] <= 0) continue;
     if ((r[0] % 2) != 0) return static_cast<int>(hipErrorInvalidValue);  // 16-B staging
+    // the ring left of / above the rect (x side rounded up to even) must exist
+    if (r[0] < nsweeps + (nsweeps & 1) || r[2] < nsweeps) return static_cast<int>(hipErrorInvalidValue);
     for (int j = 0; j < 4; ++j) a.r[a.n][j] = r[j];
     a.ntx[a.n] = (r[1] + tl.tx - 1) / tl.tx;
     a.tstart[a.n + 1] = a.tstart[a.n] + a.ntx[a.n] * ((r[3] + tl.ty - 1) / tl.ty);

@@ -258,9 +258,26 @@ def jacobi5_rects(u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, 
 XK_PIPE = 0x40000000  # gmt_jacobi5xk tile flag: register-pipelined kernel (jacobi5pipe.hip)
 
 
+def _check_xk_bounds(k: int, u: torch.Tensor, un: torch.Tensor, rects) -> None:
+    """Host-side guard before a K-sweep launch: the kernels read each rect plus a
+    K-wide ring (K rounded up to even on the x side) and the rule path may read up
+    to the last column of a row, so both tensors must be whole row-major arrays
+    holding that ring."""
+    if u.dim() != 2 or u.shape != un.shape or not (u.is_contiguous() and un.is_contiguous()):
+        raise ValueError("jacobi5xk: u and un must be contiguous 2-D tensors of one shape")
+    if u.dtype != torch.float64 or un.dtype != torch.float64:
+        raise ValueError("jacobi5xk: fp64 only")
+    kx = k + (k & 1)
+    rows, cols = u.shape
+    for x0, nx, y0, ny in rects:
+        if x0 % 2 or x0 - kx < 0 or y0 - k < 0 or x0 + nx + k > cols or y0 + ny + k > rows:
+            raise ValueError(f"jacobi5xk: rect {(x0, nx, y0, ny)} with its {k}-cell ring does not fit "
+                             f"a {rows}x{cols} array (x0 must be even)")
+
+
 def jacobi5xk(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, int, int, int]],
               dom: tuple[int, int, int, int], halo_mask: int = 0, tile: int = 0) -> None:
-    """``k`` (2-8) fused Laplace Jacobi sweeps (temporal blocking): ``un = J^k(u)`` on
+    """``k`` (2-12) fused Laplace Jacobi sweeps (temporal blocking): ``un = J^k(u)`` on
     each output rect (absolute coordinates, x0 even).  ``dom`` is the interior; bits
     of ``halo_mask`` (1 W, 2 E, 4 S, 8 N) mark ghost sides owned by a neighbour.
     ``tile``: 0 = default (register-pipelined kernel for even k, LDS tiles for k = 3),
@@ -273,6 +290,7 @@ def jacobi5xk(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[i
         ref.jacobi5xk(k, u, un, rects, dom, halo_mask)
         return
     assert len(rects) <= 4 and u.stride(0) == un.stride(0)
+    _check_xk_bounds(k, u, un, rects)
     L = _native.lib()
     arr = (ctypes.c_int64 * (4 * len(rects)))(*[v for r in rects for v in r])
     d = (ctypes.c_int64 * 4)(*[int(v) for v in dom])

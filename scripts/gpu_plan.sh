@@ -1,0 +1,19 @@
+#!/bin/bash
+# Default K=12 + pass planner: all GPU tests, smoke, bench (driver defaults), rocprof.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+export TMPDIR=/tmp
+OUT=gpurun_out/plan${TAG:-}
+mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; exit 1; }
+tail -2 $OUT/pytest_gpu.log
+timeout -k 10 300 python __graft_entry__.py smoke > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
+tail -1 $OUT/smoke.log
+timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+timeout -k 10 300 python bench.py --steps 50 --warmup 5 --skip-extras > $OUT/bench50.json 2>> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
+cat $OUT/bench50.json
+timeout -k 10 300 python bench.py --size 8192 --steps 500 --skip-extras > $OUT/bench8192.json 2>> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
+cat $OUT/bench8192.json
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$OUT/prof -o bench -- python3 $GRAFT_REPO_ROOT/bench.py --steps 100 --warmup 2 --graph off > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/$OUT/prof.log; exit 1; }
+echo PROF_OK

@@ -326,16 +326,19 @@ def test_jacobi5xk_fused_k_sweeps(k, tile, ny, nx, mask):
     assert torch.equal(un[g:g + ny, xo:xo + nx].cpu(), exp[g:g + ny, xo:xo + nx])
 
 
-@pytest.mark.parametrize("k", [2, 4, 6, 8])
-@pytest.mark.parametrize("seg", [0, 1, 5, 64, (1 << 19) | 7, (1 << 19) | 64, (2 << 19) | 33, (2 << 19) | 3])
-@pytest.mark.parametrize("ny,nx", [(1, 2), (7, 9), (40, 126), (33, 130), (70, 515)])
+@pytest.mark.parametrize("k", [2, 4, 6, 8, 10, 12])
+@pytest.mark.parametrize("seg", [0, 1, 5, 64, (1 << 19) | 7, (1 << 19) | 64, (2 << 19) | 33, (2 << 19) | 3,
+                                 (1 << 21) | 16, (1 << 22) | 24])
+@pytest.mark.parametrize("ny,nx", [(1, 2), (7, 9), (40, 126), (33, 130), (70, 515), (301, 700)])
 @pytest.mark.parametrize("mask", [0, 15, 6, 9])
 def test_jacobi5xk_pipelined(k, seg, ny, nx, mask):
     """Register-pipelined K-sweep kernel (jacobi5pipe.hip): bitwise equal to k
     fp64 reference sweeps — partial strips (128 - 2k output columns per wave),
-    segments shorter than the pipeline depth, every ghost-side pattern."""
-    g, xo = k, 8
-    u = _rand(ny + 2 * g, (xo + nx + 9) // 2 * 2, seed=71)
+    segments shorter than the pipeline depth, every ghost-side pattern; the
+    default launch (rule bands split off the fast core), the per-wave split
+    (bit 22) and the single-kernel launch (bit 21)."""
+    g, xo = k, max(8, k)  # the K-wide ghost ring fits left of the interior
+    u = _rand(ny + 2 * g, (xo + nx + max(9, k + 1)) // 2 * 2, seed=71)
     dom = (xo, nx, g, ny)
     un = torch.zeros_like(u)
     ops.jacobi5xk(k, u, un, [(xo, nx, g, ny)], dom, mask, ops.XK_PIPE | seg)
@@ -345,12 +348,12 @@ def test_jacobi5xk_pipelined(k, seg, ny, nx, mask):
     assert torch.equal(un[g:g + ny, xo:xo + nx].cpu(), exp[g:g + ny, xo:xo + nx])
 
 
-@pytest.mark.parametrize("k", [4, 8])
+@pytest.mark.parametrize("k", [4, 8, 12])
 def test_jacobi5xk_pipelined_frame_rects(k):
     """core + 4 frame rects (the engine's overlapped block step) == full launch,
     and the output never touches cells outside the rects."""
-    g, xo, ny, nx = k, 8, 90, 400
-    u = _rand(ny + 2 * g, xo + nx + 8, seed=72)
+    g, xo, ny, nx = k, max(8, k), 90, 400
+    u = _rand(ny + 2 * g, xo + nx + max(8, k), seed=72)
     dom = (xo, nx, g, ny)
     full = torch.zeros_like(u)
     ops.jacobi5xk(k, u, full, [dom], dom, 15)

@@ -241,6 +241,10 @@ def test_mpi_stencil2d_sycl_oo_strong_scaling_and_debug():
     (["70", "13", "--tblock", "--tsteps=6", "--periodic"], 1),
     (["75", "17", "--tblock", "--tsteps=8", "--dims=2x2", "--periodic", "--transport=ipc"], 4),
     (["80", "12", "--tblock", "--tsteps=6", "--dims=1x2"], 2),
+    # 10 and 12 sweeps per pass: 10/12-wide halos and corners
+    (["90", "25", "--tblock", "--tsteps=12"], 1),
+    (["96", "23", "--tblock", "--tsteps=10", "--dims=2x2", "--periodic", "--transport=ipc"], 4),
+    (["100", "26", "--tblock", "--tsteps=12", "--dims=1x2"], 2),
 ])
 def test_mpi_jacobi2d_matches_serial(args, np_):
     out = run_app("mpi_jacobi2d", *args, "--check", "--warmup=2", "--halo-iters=3", np=np_).stdout
