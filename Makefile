@@ -44,7 +44,7 @@ KERNEL_HDRS := $(wildcard csrc/kernels/*.hpp) csrc/include/gmt/kernels.h
 RT_OBJ      := $(OBJ)/runtime/rt_hip.o
 CCL_OBJ     := $(OBJ)/runtime/ccl_rccl.o
 HOST_OBJS   := $(OBJ)/host/kernels_host.o $(OBJ)/host/rt_host.o
-HOSTCCL_OBJ := $(OBJ)/host/ccl_stub.o
+HOSTCCL_OBJ := $(OBJ)/host/ccl_host.o
 COMM_OBJS   := $(OBJ)/comm/transport_mpi.o $(OBJ)/comm/transport_core.o $(OBJ)/engine/jacobi.o
 ENG_OBJS    := $(OBJ)/comm/transport_core.o $(OBJ)/engine/jacobi.o $(OBJ)/engine/engine_capi.o
 APP_HDRS    := $(wildcard csrc/include/gmt/*.hpp csrc/include/gmt/*.h csrc/apps/*.hpp)

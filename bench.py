@@ -166,8 +166,6 @@ def main(argv=None):
     dims = tuple(int(v) for v in args.dims.lower().split("x")) if args.dims else None
     overlap = not args.no_overlap
     engine = args.engine
-    if engine == "native" and env.world_size > 1 and not env.is_gpu:
-        engine = "torch"  # the native engine's multi-rank data plane is RCCL (GPU only)
     graph = args.graph == "on" or (args.graph == "auto" and env.world_size == 1)
     if engine == "native":
         solver, dt, info = bench_native(env, args.size, args.steps, args.warmup, overlap, dims,

@@ -69,23 +69,43 @@ struct DerivConfig {
   bool debug_dump = false;        // rank-serialised halo-row dumps (sycl_oo DEBUG build)
 };
 
-// Print rows [r0, r0+nr) of a column-major field (first <= 20 columns) on
-// every rank in turn (mpi_stencil2d_sycl_oo.cc:636-659).
+// Print rows [r0, r0+nr) of a column-major field (first <= 20 columns) for
+// every rank in rank order (mpi_stencil2d_sycl_oo.cc:636-659 serialises the
+// ranks with MPI_Barrier; here rank 0 gathers the formatted lines and prints
+// them, so the forwarded stdout of several ranks cannot interleave).
 inline void dump_rows(MPI_Comm comm, int rank, int ws, const char* what, const double* dev,
                       size_t nrows, size_t ncols, size_t r0, size_t nr) {
   const size_t nc = ncols < 20 ? ncols : 20;
   std::vector<double> h(nrows * nc);
   GMT_CHECK("dump D2H", gmt_rt_memcpy(h.data(), dev, h.size() * sizeof(double)));
-  for (int r = 0; r < ws; ++r) {
-    if (r == rank) {
-      for (size_t i = r0; i < r0 + nr; ++i) {
-        std::printf("%d: %s [%zu, :]", rank, what, i);
-        for (size_t j = 0; j < nc; ++j) std::printf(" %f", h[i + j * nrows]);
-        std::printf("\n");
-      }
-      std::fflush(stdout);
+  std::string text;
+  char buf[64];
+  for (size_t i = r0; i < r0 + nr; ++i) {
+    std::snprintf(buf, sizeof(buf), "%d: %s [%zu, :]", rank, what, i);
+    text += buf;
+    for (size_t j = 0; j < nc; ++j) {
+      std::snprintf(buf, sizeof(buf), " %f", h[i + j * nrows]);
+      text += buf;
     }
-    MPI_Barrier(comm);
+    text += "\n";
+  }
+  int len = static_cast<int>(text.size());
+  std::vector<int> lens(ws), offs(ws);
+  GMT_MPI_CHECK(MPI_Gather(&len, 1, MPI_INT, lens.data(), 1, MPI_INT, 0, comm));
+  std::string all;
+  if (rank == 0) {
+    int tot = 0;
+    for (int r = 0; r < ws; ++r) {
+      offs[r] = tot;
+      tot += lens[r];
+    }
+    all.resize(tot);
+  }
+  GMT_MPI_CHECK(MPI_Gatherv(text.data(), len, MPI_CHAR, rank == 0 ? &all[0] : nullptr, lens.data(),
+                            offs.data(), MPI_CHAR, 0, comm));
+  if (rank == 0) {
+    std::fwrite(all.data(), 1, all.size(), stdout);
+    std::fflush(stdout);
   }
 }
 

@@ -42,7 +42,11 @@ int main(int argc, char** argv) {
   if (n_global % world_size != 0) {
     std::printf("%d nmpi (%d) must be divisor of domain size (%lld), exiting\n", world_rank,
                 world_size, n_global);
-    MPI_Abort(MPI_COMM_WORLD, 1);
+    // every rank sees the same condition: leave collectively (an MPI_Abort
+    // can kill the job before the forwarded message reaches the terminal)
+    std::fflush(stdout);
+    MPI_Finalize();
+    return 1;
   }
   const size_t n_local = static_cast<size_t>(n_global / world_size);
   const size_t n_ghost = n_local + 2 * n_bnd;

@@ -42,7 +42,7 @@ class RcclExchange : public Exchange {
 class RcclTransport : public Transport {
  public:
   RcclTransport(int rank, int size, const gmt_ccl_id& id) : Transport(rank, size) {
-    if (!gmt_ccl_available()) {
+    if (!gmt_ccl_available() && !gmt_ccl_emulated()) {
       std::printf("ERROR: transport rccl requested but this build has no RCCL (%s backend)\n",
                   gmt_rt_backend_name());
       abort_job(EXIT_FAILURE);

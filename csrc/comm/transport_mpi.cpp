@@ -437,14 +437,14 @@ std::unique_ptr<Transport> make_transport(Kind k, MPI_Comm comm, const RankBindi
     case Kind::MpiHost: return std::make_unique<MpiHostTransport>(comm);
     case Kind::MpiDirect: return std::make_unique<MpiDirectTransport>(comm);
     case Kind::Rccl: {
-      if (!gmt_ccl_available()) {
+      if (!gmt_ccl_available() && !gmt_ccl_emulated()) {
         std::printf("ERROR: transport rccl requested but this build has no RCCL (%s backend)\n",
                     gmt_rt_backend_name());
         abort_job(EXIT_FAILURE);
       }
       int worst = b.ranks_per_device;
       MPI_Allreduce(MPI_IN_PLACE, &worst, 1, MPI_INT, MPI_MAX, comm);
-      if (worst > 1) {
+      if (worst > 1 && !gmt_ccl_emulated()) {  // the host emulation has no devices to share
         std::printf("ERROR: transport rccl needs one rank per GPU (%d ranks share a GPU); "
                     "use --transport=ipc or mpi-host\n", worst);
         abort_job(EXIT_FAILURE);

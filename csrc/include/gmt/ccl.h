@@ -1,8 +1,11 @@
 /*
  * gmt/ccl.h — collective / point-to-point device communication C ABI.
  *
- * HIP build: RCCL over xGMI (csrc/runtime/ccl_rccl.cpp).  Host build: not
- * available (gmt_ccl_available() == 0; every call returns GMT_CCL_UNAVAILABLE).
+ * HIP build: RCCL over xGMI (csrc/runtime/ccl_rccl.cpp).  Host build: the
+ * same semantics emulated over Unix-domain sockets between the processes of
+ * one node (csrc/host/ccl_host.cpp): gmt_ccl_available() == 0 (automatic
+ * transport selection never picks it) and gmt_ccl_emulated() == 1 (an
+ * explicit "rccl" request runs on it).
  *
  * The reference passes device pointers straight to GPU-aware MPI
  * (MPI_Isend/Irecv: mpi_stencil2d_gt.cc:186-225, MPI_Allreduce :615,
@@ -29,6 +32,7 @@ typedef struct gmt_ccl_id {
 } gmt_ccl_id;
 
 int gmt_ccl_available(void);
+int gmt_ccl_emulated(void);
 const char* gmt_ccl_error_string(int err);
 int gmt_ccl_version(int* v);
 int gmt_ccl_get_unique_id(gmt_ccl_id* id);

@@ -9,6 +9,7 @@
 #pragma once
 
 #include <mpi.h>
+#include <unistd.h>
 
 #include <cstdio>
 
@@ -20,7 +21,12 @@ inline void mpi_abort_hook(int code) {
   int init = 0, fin = 0;
   MPI_Initialized(&init);
   MPI_Finalized(&fin);
-  if (init && !fin) MPI_Abort(MPI_COMM_WORLD, code);
+  if (init && !fin) {
+    // give the launcher's stdout forwarding a moment: MPI_Abort tears the job
+    // down at once and can drop the error message just printed
+    usleep(300000);
+    MPI_Abort(MPI_COMM_WORLD, code);
+  }
 }
 
 inline void install_mpi_abort() { abort_hook() = &mpi_abort_hook; }

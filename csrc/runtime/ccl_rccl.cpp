@@ -20,6 +20,7 @@ inline ncclComm_t C(gmt_ccl_comm_t c) { return reinterpret_cast<ncclComm_t>(c); 
 extern "C" {
 
 int gmt_ccl_available(void) { return 1; }
+int gmt_ccl_emulated(void) { return 0; }
 const char* gmt_ccl_error_string(int err) {
   if (err == GMT_CCL_UNAVAILABLE) return "RCCL not available in this build";
   return ncclGetErrorString(static_cast<ncclResult_t>(err));

@@ -111,9 +111,9 @@ class NativeJacobi:
         if e.world_size == 1:
             transport, cid = LOCAL, None
         else:
-            if not e.is_gpu:
-                raise EngineError("multi-rank native engine needs GPUs (RCCL); "
-                                  "use the mpi_jacobi2d app or the torch engine on CPU")
+            # GPU: RCCL over xGMI.  CPU: the host backend's emulation of the same
+            # RCCL semantics over Unix sockets (csrc/host/ccl_host.cpp), so the
+            # multi-rank engine path runs and is checked without GPUs.
             transport = RCCL
             cid = ctypes.create_string_buffer(_broadcast_unique_id(self.lib, e), 128)
         ks = 0 if not tblock else (2 if tblock is True else int(tblock))
@@ -131,7 +131,7 @@ class NativeJacobi:
         self.tblock = self.tsteps > 1
         self.graph = bool(graph_on)
         self.overlap = bool(overlap_on)
-        self.transport = "rccl" if transport == RCCL else "local"
+        self.transport = ("rccl" if e.is_gpu else "rccl-host") if transport == RCCL else "local"
 
     # ------------------------------------------------------------------
     def run(self, steps: int) -> None:

@@ -45,5 +45,17 @@ def test_bench_two_ranks_torchrun_cpu():
                 "--device", "cpu", "--size", "256", "--steps", "3", "--warmup", "1",
                 "--daxpy-n", "20000"])
     _check(rec, 2, 3, 1)
-    assert rec["config"]["engine"] == "torch"  # multi-rank CPU runs use torch.distributed (gloo)
+    # the GPU run's path: native engine, RCCL semantics (host emulation on CPU)
+    assert rec["config"]["engine"] == "native" and rec["config"]["transport"] == "rccl-host"
+    assert rec["halo_exchange_us"] is not None and rec["halo_exchange_us"] > 0
+
+
+def test_bench_two_ranks_torch_engine_cpu():
+    port = str(random.randint(20000, 40000))
+    rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
+                "--device", "cpu", "--size", "256", "--steps", "3", "--warmup", "1",
+                "--daxpy-n", "20000", "--engine", "torch"])
+    _check(rec, 2, 3, 1)
+    assert rec["config"]["engine"] == "torch"  # torch.distributed (gloo) P2P from Python
     assert rec["halo_exchange_us"] is not None and rec["halo_exchange_us"] > 0

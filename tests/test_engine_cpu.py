@@ -5,6 +5,7 @@ the libgmt.so SONAME, so one process may only ever bind one backend.
 """
 import json
 import os
+import random
 import subprocess
 import sys
 
@@ -71,3 +72,33 @@ def test_native_engine_temporal_blocking(steps, periodic):
 def test_native_engine_k_sweeps(k):
     r = _run(ny=41, nx=66, steps=11, periodic=True, overlap=True, tblock=k)
     assert r["diff"] < 1e-13
+
+
+@pytest.mark.parametrize("np_,ny,nx,steps,periodic,overlap,tblock,dims", [
+    (2, 40, 70, 7, False, True, 0, None),
+    (2, 41, 66, 9, True, True, 2, "1x2"),
+    (4, 61, 75, 13, True, True, 4, "2x2"),
+    (4, 60, 64, 25, False, True, 12, "2x2"),
+    (3, 50, 90, 11, True, False, 8, "1x3"),
+    (6, 66, 70, 10, True, True, 6, "2x3"),
+])
+def test_native_engine_multirank_rccl_semantics(np_, ny, nx, steps, periodic, overlap, tblock, dims):
+    """The multi-GPU data plane of bench.py (native engine, RCCL grouped
+    send/recv, temporal-blocking halos with corners, residual all-reduce) at
+    np_ ranks on the CPU backend: the result equals the serial sweep."""
+    ensure_host_build()
+    port = str(random.randint(20000, 45000))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(np_),
+           "--master-addr", "127.0.0.1", "--master-port", port,
+           os.path.join(ROOT, "tests", "engine_mp_worker.py"), str(ny), str(nx), str(steps),
+           "1" if periodic else "0", "1" if overlap else "0", str(tblock)] + ([dims] if dims else [])
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+                                OMP_NUM_THREADS="1"))
+    assert p.returncode == 0, p.stdout + p.stderr
+    r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert r["transport"] == "rccl-host"
+    assert r["diff"] < 1e-13, r
+    assert r["resid_same"]
+    if dims:
+        assert r["dims"] == [int(v) for v in dims.split("x")]

@@ -53,12 +53,13 @@ def test_mpi_daxpy_memory_per_core_env():
     assert "MEMORY_PER_CORE=4096" in out
 
 
-@pytest.mark.parametrize("np_", [1, 3])
-def test_mpi_daxpy_bench_allreduce(np_, tmp_path):
+@pytest.mark.parametrize("np_,transport", [(1, "auto"), (3, "auto"), (3, "rccl")])
+def test_mpi_daxpy_bench_allreduce(np_, transport, tmp_path):
     """BASELINE config "mpi_daxpy N ranks x 1 GPU, allreduce of partial sums":
     timed DAXPY + device partial sum + transport all-reduce, ALLSUM checked."""
     j = tmp_path / "d.jsonl"
-    out = run_app("mpi_daxpy", "--bench=50000", "--iters=4", f"--json={j}", np=np_).stdout
+    out = run_app("mpi_daxpy", "--bench=50000", "--iters=4", f"--json={j}", f"--transport={transport}",
+                  np=np_).stdout
     assert re.search(r"BENCH daxpy n=50000 per rank x %d ranks: [\d.]+ ms/call" % np_, out)
     m = re.search(r"ALLSUM = (\S+) \(expected (\S+), rel err \S+\) OK", out)
     assert m and abs(float(m.group(1)) - 9 * 50001 / 2 * np_) < 1e-6 * np_ * 50001 * 9
@@ -79,10 +80,11 @@ def test_mpi_daxpy_gt_every_rank():
 
 
 @pytest.mark.parametrize("variant", ["mpi_daxpy_nvtx_managed", "mpi_daxpy_nvtx_unmanaged"])
-@pytest.mark.parametrize("np_", [1, 2, 3])
-def test_mpi_daxpy_nvtx_sums_and_times(variant, np_):
+@pytest.mark.parametrize("np_,transport", [(1, "auto"), (2, "auto"), (3, "auto"), (3, "rccl")])
+def test_mpi_daxpy_nvtx_sums_and_times(variant, np_, transport):
     per_node = 1200
-    out = run_app(variant, f"--n-per-node={per_node}", "--iters=2", np=np_).stdout
+    out = run_app(variant, f"--n-per-node={per_node}", "--iters=2", f"--transport={transport}",
+                  np=np_).stdout
     n = per_node // np_
     assert f"1 nodes, {np_} ranks, {n} elements each, total {per_node}" in out
     for r in range(np_):
@@ -156,7 +158,7 @@ def test_mpi_stencil2d_gt_all_variants(np_):
     assert "WARNING" not in out  # all-reduce values checked against PI*n_other
 
 
-@pytest.mark.parametrize("transport", ["mpi-host", "mpi-direct", "ipc"])
+@pytest.mark.parametrize("transport", ["mpi-host", "mpi-direct", "ipc", "rccl"])
 def test_mpi_stencil2d_gt_transport_parity(transport):
     out = run_app("mpi_stencil2d_gt", "40", "4", "--n-other=256", "--no-managed",
                   f"--transport={transport}", "--host-init", "--host-verify", np=3).stdout
@@ -241,6 +243,13 @@ def test_mpi_stencil2d_sycl_oo_strong_scaling_and_debug():
     (["70", "13", "--tblock", "--tsteps=6", "--periodic"], 1),
     (["75", "17", "--tblock", "--tsteps=8", "--dims=2x2", "--periodic", "--transport=ipc"], 4),
     (["80", "12", "--tblock", "--tsteps=6", "--dims=1x2"], 2),
+    # rccl transport (host backend: the RCCL semantics over Unix sockets,
+    # csrc/host/ccl_host.cpp) — the data plane of the multi-GPU runs
+    (["50", "10", "--tblock", "--transport=rccl"], 2),
+    (["41", "7", "--dims=2x2", "--transport=rccl"], 4),
+    (["41", "7", "--dims=1x2", "--periodic", "--transport=rccl"], 2),
+    (["61", "11", "--tblock", "--tsteps=12", "--dims=2x2", "--periodic", "--transport=rccl"], 4),
+    (["45", "8", "--tblock=8", "--dims=2x3", "--periodic", "--transport=rccl"], 6),
     # 10 and 12 sweeps per pass: 10/12-wide halos and corners
     (["90", "25", "--tblock", "--tsteps=12"], 1),
     (["96", "23", "--tblock", "--tsteps=10", "--dims=2x2", "--periodic", "--transport=ipc"], 4),
@@ -253,7 +262,8 @@ def test_mpi_jacobi2d_matches_serial(args, np_):
     assert re.search(r"MLUPS     : [\d.]+", out)
 
 
-@pytest.mark.parametrize("transport,np_", [("ipc", 2), ("mpi-host", 2), ("mpi-direct", 3), ("local", 1)])
+@pytest.mark.parametrize("transport,np_", [("ipc", 2), ("mpi-host", 2), ("mpi-direct", 3), ("local", 1),
+                                           ("rccl", 3)])
 def test_mpi_halo_bench_data(transport, np_):
     out = run_app("mpi_halo_bench", "8", "65536", "3", f"--transport={transport}", np=np_).stdout
     rows = re.findall(r"^\s+(\d+)\s+2\s+[\d.]+\s+[\d.]+\s+[\d.]+$", out, re.M)
@@ -262,8 +272,9 @@ def test_mpi_halo_bench_data(transport, np_):
 
 
 def test_transport_errors_are_loud():
-    p = run_app("mpi_jacobi2d", "32", "2", "--transport=rccl", np=1, check=False)
-    assert p.returncode != 0 and "no RCCL" in p.stdout
+    # a single-process transport in a 2-rank job
+    p = run_app("mpi_jacobi2d", "32", "2", "--transport=local", np=2, check=False)
+    assert p.returncode != 0 and "!= world size" in p.stdout
     p = run_app("mpi_jacobi2d", "32", "2", "--transport=bogus", np=1, check=False)
     assert p.returncode != 0 and "unknown transport" in p.stdout
 
