@@ -10,10 +10,18 @@
 // The reference prints PCI BDF + UUID only for Intel GPUs
 // (ext_intel_pci_address) and leaves device_id/vendor_id uninitialised
 // (:403-404); here both come from the HIP device.
+//
+// --test-buf-view[=N] runs the reference's pack/unpack self-test
+// (test_buf_view, mpi_stencil2d_sycl.cc:118-159, wired in but commented out
+// of its main at :379-381) on an N x N field (default 6) through the gfx950
+// halo copy kernel (gmt_copy2d_batched): print the field and a second
+// buffer, pack ghost-side rows [0, n_bnd) into a buffer, unpack the second
+// buffer into rows [N-n_bnd, N), print again.  No MPI.
 #include <mpi.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "deriv_common.hpp"
 #include "gmt/device.hpp"
@@ -21,8 +29,75 @@
 using namespace gmt;
 using namespace gmt::apps;
 
+namespace {
+
+// Copy rows [start, end) of a col-major nrows x ncols field to/from a
+// contiguous (end-start) x ncols buffer on `stream` (nullptr = default).
+void buf_view_copy(bool to_buf, int ncols, int buf_nrows, double* buf, int nrows, double* data,
+                   int start, int end) {
+  gmt_copy2d_desc d;
+  d.width = end - start;
+  d.height = ncols;
+  if (to_buf) {
+    d.src = data + start, d.src_ld = nrows, d.dst = buf, d.dst_ld = buf_nrows;
+  } else {
+    d.src = buf, d.src_ld = buf_nrows, d.dst = data + start, d.dst_ld = nrows;
+  }
+  GMT_CHECK("copy2d", gmt_copy2d_batched(1, &d, sizeof(double), nullptr));
+  GMT_CHECK("sync", gmt_rt_device_synchronize());
+}
+
+int test_buf_view(int n) {
+  const int n_bnd = 2, n_with_ghost = n + 2 * n_bnd;
+  std::vector<double> data(size_t(n_with_ghost) * n), buf(size_t(n_bnd) * n),
+      buf2(size_t(n_bnd) * n);
+  for (int j = 0; j < n; j++) {
+    for (int i = 0; i < n_with_ghost; i++) data[i + size_t(j) * n_with_ghost] = (i - n_bnd) + j / 1000.0;
+    buf2[0 + size_t(j) * n_bnd] = 100.0 + j;
+    buf2[1 + size_t(j) * n_bnd] = 100.0 + j + 0.1;
+  }
+  auto print_data = [&] {
+    for (int j = 0; j < n; j++)
+      for (int i = 0; i < n; i++)
+        std::printf("data[%d, %d] = %f\n", i, j, data[i + size_t(j) * n_with_ghost]);
+  };
+  auto print_buf = [&](const char* name, const std::vector<double>& b) {
+    for (int j = 0; j < n; j++)
+      for (int i = 0; i < n_bnd; i++) std::printf("%s[%d, %d] = %f\n", name, i, j, b[i + size_t(j) * n_bnd]);
+  };
+  print_data();
+  print_buf("buf2", buf2);
+  Buffer<double> d_data(data.size(), GMT_SPACE_DEVICE), d_buf(buf.size(), GMT_SPACE_DEVICE),
+      d_buf2(buf2.size(), GMT_SPACE_DEVICE);
+  GMT_CHECK("H2D", gmt_rt_memcpy(d_data.data(), data.data(), d_data.bytes()));
+  GMT_CHECK("H2D", gmt_rt_memcpy(d_buf2.data(), buf2.data(), d_buf2.bytes()));
+  buf_view_copy(true, n, n_bnd, d_buf.data(), n_with_ghost, d_data.data(), 0, n_bnd);
+  GMT_CHECK("D2H", gmt_rt_memcpy(buf.data(), d_buf.data(), d_buf.bytes()));
+  print_buf("buf", buf);
+  buf_view_copy(false, n, n_bnd, d_buf2.data(), n_with_ghost, d_data.data(), n - n_bnd, n);
+  GMT_CHECK("D2H", gmt_rt_memcpy(data.data(), d_data.data(), d_data.bytes()));
+  print_data();
+  // self-check (the reference only prints): packed rows are rows 0..1 of the
+  // field, unpacked rows n-2..n-1 now hold buf2
+  int bad = 0;
+  for (int j = 0; j < n; j++)
+    for (int i = 0; i < n_bnd; i++) {
+      bad += buf[i + size_t(j) * n_bnd] != (i - n_bnd) + j / 1000.0;
+      bad += data[n - n_bnd + i + size_t(j) * n_with_ghost] != buf2[i + size_t(j) * n_bnd];
+    }
+  std::printf("test_buf_view %s\n", bad ? "FAILED" : "OK");
+  return bad ? EXIT_FAILURE : EXIT_SUCCESS;
+}
+
+}  // namespace
+
 int main(int argc, char** argv) {
   Cli cli(argc, argv);
+  if (cli.has("test-buf-view")) {
+    GMT_CHECK("set device", gmt_rt_set_device(0));
+    const long long n = cli.geti("test-buf-view", 6);  // bare flag = "1" -> default 6
+    return test_buf_view(n >= 4 ? static_cast<int>(n) : 6);
+  }
   size_t nx_local = 1024;
   bool stage_host = false;
   int n_iter = 100;

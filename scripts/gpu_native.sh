@@ -46,6 +46,7 @@ run 120 halo_host2       $MPIRUN -np 2 $B/mpi_halo_bench 16 16777216 20 --transp
 run 60  stencil1d        $MPIRUN -np 2 $B/mpi_stencil_gt 32 --iters=100 $J
 run 300 stencil2d_gt1    $MPIRUN -np 1 $B/mpi_stencil2d_gt 1024 50 $J
 run 300 stencil2d_gt2    $MPIRUN -np 2 $B/mpi_stencil2d_gt 1024 30 --no-managed $J
+run 60  buf_view         $B/mpi_stencil2d_sycl --test-buf-view=64
 run 120 stencil2d_sycl   $MPIRUN -np 2 $B/mpi_stencil2d_sycl 1024 0 50 $J
 run 120 stencil2d_sycl_h $MPIRUN -np 2 $B/mpi_stencil2d_sycl 1024 1 50 $J
 run 120 stencil2d_oo     $MPIRUN -np 2 $B/mpi_stencil2d_sycl_oo 8 0 100 $J

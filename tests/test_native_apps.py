@@ -198,6 +198,20 @@ def test_mpi_stencil2d_sycl(stage):
     assert len(errs) == 2 and max(errs) < 1e-6
 
 
+@pytest.mark.parametrize("n", [None, "9"])
+def test_mpi_stencil2d_sycl_buf_view_selftest(n):
+    """Reference test_buf_view (mpi_stencil2d_sycl.cc:118-159): pack rows
+    [0,2) of an n x n field, unpack a buffer into rows [n-2,n)."""
+    flag = "--test-buf-view" if n is None else f"--test-buf-view={n}"
+    out = run_app("mpi_stencil2d_sycl", flag).stdout
+    k = 6 if n is None else int(n)
+    assert out.rstrip().endswith("test_buf_view OK")
+    assert len(re.findall(r"^data\[", out, re.M)) == 2 * k * k
+    assert len(re.findall(r"^buf2\[", out, re.M)) == 2 * k
+    assert "buf[1, 0] = -1.000000" in out
+    assert f"data[{k - 1}, {k - 1}] = {100 + k - 1 + 0.1:f}" in out
+
+
 def test_mpi_stencil2d_sycl_oo_strong_scaling_and_debug():
     out = run_app("mpi_stencil2d_sycl_oo", "1", "0", "5", np=2).stdout
     assert "n_global   = 1024" in out and "n_local    = 512" in out
