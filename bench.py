@@ -11,7 +11,7 @@ carries the single-GPU-per-rank DAXPY bandwidth (BASELINE config "daxpy
 N=2^28 fp64 on one MI355X") and the measured halo-exchange latency.
 
 One step = one full Jacobi sweep of the global domain (every point updated
-once).  The native engine (C++ + hipGraph replay, ``csrc/engine/jacobi.cpp``)
+once).  The native engine (C++, ``csrc/engine/jacobi.cpp``)
 runs the steps in fused passes of up to 12 sweeps by default (temporal
 blocking, ``--tblock on --tsteps 12``): one 12-wide halo exchange (RCCL over
 xGMI on a high-priority stream, overlapped with the interior update) and one
@@ -146,8 +146,10 @@ def main(argv=None):
     ap.add_argument("--engine", choices=("native", "torch"), default="native")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
-                    help="hipGraph replay of the step (auto: on for 1 GPU; eager RCCL steps "
-                         "for N>1, where a step is >100 us of GPU work and launches hide)")
+                    help="hipGraph replay of the fused passes (auto = off: a 12-sweep pass is "
+                         ">0.5 ms of GPU work, its 2-3 launches hide, and replaying the captured "
+                         "graph measured 2-6%% slower than eager launches at every domain size, "
+                         "profiles/r01_frame.md)")
     ap.add_argument("--tblock", choices=("on", "off"), default="on",
                     help="temporal blocking (native engine): --tsteps sweeps per memory pass and "
                          "per halo exchange; bitwise the same result as single sweeps")
@@ -166,7 +168,7 @@ def main(argv=None):
     dims = tuple(int(v) for v in args.dims.lower().split("x")) if args.dims else None
     overlap = not args.no_overlap
     engine = args.engine
-    graph = args.graph == "on" or (args.graph == "auto" and env.world_size == 1)
+    graph = args.graph == "on"
     if engine == "native":
         solver, dt, info = bench_native(env, args.size, args.steps, args.warmup, overlap, dims,
                                         graph, args.variant,

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 namespace gmt {
@@ -48,6 +49,26 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   nb_.east = cx < c.px - 1 ? at(cy, cx + 1) : (c.periodic ? at(cy, 0) : -1);
   nb_.south = cy > 0 ? at(cy - 1, cx) : (c.periodic ? at(c.py - 1, cx) : -1);
   nb_.north = cy < c.py - 1 ? at(cy + 1, cx) : (c.periodic ? at(0, cx) : -1);
+  // diagonal neighbours: the K-wide corner ghosts travel in the same single
+  // exchange phase as the faces (gmt/halo.hpp one-phase corner mode);
+  // GMT_HALO_TWO_PHASE=1 restores the two-phase exchange (A/B)
+  auto wrap = [&](int v, int n, bool& ok) {
+    if (v >= 0 && v < n) return v;
+    if (!c.periodic) ok = false;
+    return (v + n) % n;
+  };
+  auto diag = [&](int dy, int dx) {
+    bool ok = true;
+    const int y = wrap(cy + dy, c.py, ok), x = wrap(cx + dx, c.px, ok);
+    return ok ? at(y, x) : -1;
+  };
+  const char* tp = std::getenv("GMT_HALO_TWO_PHASE");
+  if (!(tp && tp[0] == '1')) {
+    nb_.sw = diag(-1, -1);
+    nb_.se = diag(-1, 1);
+    nb_.nw = diag(1, -1);
+    nb_.ne = diag(1, 1);
+  }
 
   ks_ = c.tsteps > 1 ? c.tsteps : (c.tblock ? 2 : 1);
   if (ks_ > 12) ks_ = 12;
@@ -58,9 +79,14 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   ld_ = round_up(xo_ + nx_ + g_, 64);
   const size_t elems = static_cast<size_t>(ld_) * (ny_ + 2 * g_);
   GMT_CHECK("stream", gmt_rt_stream_create(&s_, 0));
-  GMT_CHECK("comm stream", gmt_rt_stream_create(&cs_, 1));
+  // exchange stream priority: high by default; GMT_COMM_PRIORITY=0 for A/B
+  const char* cp = std::getenv("GMT_COMM_PRIORITY");
+  GMT_CHECK("comm stream", gmt_rt_stream_create(&cs_, cp && cp[0] == '0' ? 0 : 1));
   GMT_CHECK("event", gmt_rt_event_create(&ev_start_, 0));
   GMT_CHECK("event", gmt_rt_event_create(&ev_halo_, 0));
+  GMT_CHECK("event", gmt_rt_event_create(&ev_packed_, 0));
+  const char* cap = std::getenv("GMT_CORE_AFTER_PACK");
+  core_after_pack_ = !(cap && cap[0] == '0');
   if (c.variant) gmt_jacobi5_set_variant(c.variant);
 
   // deterministic, decomposition-independent initial field and Dirichlet
@@ -88,6 +114,7 @@ JacobiSolver::~JacobiSolver() {
   for (auto& g : graph2_) gmt_rt_graph_destroy(g);
   gmt_rt_event_destroy(ev_start_);
   gmt_rt_event_destroy(ev_halo_);
+  gmt_rt_event_destroy(ev_packed_);
   halo_[0].reset();
   halo_[1].reset();
   gmt_rt_stream_destroy(cs_);
@@ -160,19 +187,45 @@ void JacobiSolver::enqueue_block(int parity, int K) {
     GMT_CHECK("jacobi xk", gmt_jacobi5xk(K, 1, dom, dom, mask, u, un, ld_, tr, s_));
     return;
   }
-  // right frame starts at an even column: KA or KA+1 columns wide
+  // The core is inset only on the sides whose ghost ring is a neighbour's
+  // halo (a Dirichlet side does not wait for the exchange; the kernel's rule
+  // band handles it).  The frame — the K-wide bands along the halo sides —
+  // follows once the halo has landed.  The right band starts at an even
+  // column: KA or KA+1 columns wide.
+  const bool hw = mask & 1, he = mask & 2, hs = mask & 4, hn = mask & 8;
   const int64_t xr = (xo_ + nx_ - K) & ~int64_t(1);
-  const int64_t core[4] = {xo_ + KA, xr - xo_ - KA, yo_ + K, ny_ - 2 * K};
+  const int64_t cx0 = hw ? xo_ + KA : xo_, cx1 = he ? xr : xo_ + nx_;
+  const int64_t cy0 = hs ? yo_ + K : yo_, cy1 = hn ? yo_ + ny_ - K : yo_ + ny_;
+  const int64_t core[4] = {cx0, cx1 - cx0, cy0, cy1 - cy0};
   GMT_CHECK("event", gmt_rt_event_record(ev_start_, s_));
-  GMT_CHECK("core xk", gmt_jacobi5xk(K, 1, core, dom, mask, u, un, ld_, tr, s_));
   GMT_CHECK("wait", gmt_rt_stream_wait_event(cs_, ev_start_));
-  h.start(cs_);
+  // the core waits for the (few-us) halo pack: the transfer kernels are then
+  // dispatched together with the core's first waves and find free CUs —
+  // queued behind a GPU-filling core they waited ~1/3 of it for a slot and
+  // their late start stalled the core's dispatch (rocprofv3, profiles/r01_frame.md).
+  // GMT_CORE_AFTER_PACK=0 launches the core at once (A/B).
+  h.start(cs_, core_after_pack_ ? ev_packed_ : nullptr);
+  if (core_after_pack_) GMT_CHECK("wait", gmt_rt_stream_wait_event(s_, ev_packed_));
+  GMT_CHECK("core xk", gmt_jacobi5xk(K, 1, core, dom, mask, u, un, ld_, tr, s_));
   h.finish(cs_);
   GMT_CHECK("event", gmt_rt_event_record(ev_halo_, cs_));
   GMT_CHECK("wait", gmt_rt_stream_wait_event(s_, ev_halo_));
-  const int64_t frame[16] = {xo_, nx_, yo_,            K,          xo_, nx_,            yo_ + ny_ - K, K,
-                             xo_, KA,  yo_ + K,        ny_ - 2 * K, xr, xo_ + nx_ - xr, yo_ + K,       ny_ - 2 * K};
-  GMT_CHECK("frame xk", gmt_jacobi5xk(K, 4, frame, dom, mask, u, un, ld_, tr, s_));
+  int64_t frame[16];
+  int nf = 0;
+  auto add = [&](int64_t x0, int64_t nx, int64_t y0, int64_t ny) {
+    if (nx <= 0 || ny <= 0) return;
+    const int64_t r[4] = {x0, nx, y0, ny};
+    std::copy(r, r + 4, frame + 4 * nf++);
+  };
+  if (hs) add(xo_, nx_, yo_, K);
+  if (hn) add(xo_, nx_, yo_ + ny_ - K, K);
+  if (hw) add(xo_, KA, cy0, cy1 - cy0);
+  if (he) add(xr, xo_ + nx_ - xr, cy0, cy1 - cy0);
+  // the pipelined kernel may cover the narrow bands with whole strips that
+  // reach into the finished core (same values rewritten): branch-free path
+  const bool pipe = (tr == 0 && K % 2 == 0) || (tr & GMT_XK_PIPE);
+  const int tf = pipe ? (tr | GMT_XK_PIPE | GMT_XK_EXT) : tr;
+  GMT_CHECK("frame xk", gmt_jacobi5xk(K, nf, frame, dom, mask, u, un, ld_, tf, s_));
 }
 
 void JacobiSolver::step_block() {

@@ -30,24 +30,38 @@ namespace gmt {
 struct Neighbors {
   int west = -1, east = -1;    // x / dim 0 (contiguous axis) lower / upper
   int south = -1, north = -1;  // y / dim 1 (strided axis) lower / upper
+  // diagonal neighbours (corner mode): known -> one-phase exchange with four
+  // gx x gy corner messages; unknown (-2) -> two-phase (y faces, then x faces
+  // spanning the fresh y ghosts)
+  int sw = -2, se = -2, nw = -2, ne = -2;
+  bool diagonals_known() const { return sw != -2 && se != -2 && nw != -2 && ne != -2; }
 };
 
 class Halo2D {
  public:
   static constexpr int kTagLow = 456, kTagHigh = 123, kTagY = 1000;
+  // corner message sent toward SW/SE/NW/NE; it arrives from the opposite side
+  static constexpr int kTagSW = 2000, kTagSE = 2001, kTagNW = 2002, kTagNE = 2003;
 
   // field: the whole ghosted array, nrows = nx + 2*gx (contiguous), ncols = ny + 2*gy.
-  // corners: two-phase exchange (y faces first, then x faces that include the
-  // freshly received y-ghost rows) so diagonal ghost cells are valid too — the
-  // temporal-blocking kernel (two sweeps per exchange) reads them.
+  // corners: diagonal ghost cells must be valid too — the temporal-blocking
+  // kernels (K sweeps per exchange) read them.  With the diagonal neighbours
+  // known: ONE phase — x faces over the interior rows, y faces (whole
+  // columns), and a gx x gy block to each diagonal neighbour, all in one
+  // transport group, packed and unpacked by one fused copy launch each (the
+  // corner unpack runs after the y faces landed, so it overwrites the
+  // sender's stale corner ghosts they carry).  Otherwise two phases: y faces
+  // first, then x faces that include the freshly received y-ghost rows.
   Halo2D(comm::Transport& t, Span2D<double> field, int gx, int gy, Neighbors nb, bool pack_y,
          int buf_space, bool corners = false)
       : t_(t), f_(field), gx_(gx), gy_(gy), nb_(nb) {
     nx_ = f_.nrows - 2 * gx;
     ny_ = f_.ncols - 2 * gy;
-    corners_ = corners && gx > 0 && gy > 0 && (nb.west >= 0 || nb.east >= 0) &&
-               (nb.south >= 0 || nb.north >= 0);
-    // x faces span the y ghosts too in corner mode
+    const bool corner_cells = corners && gx > 0 && gy > 0 && (nb.west >= 0 || nb.east >= 0) &&
+                              (nb.south >= 0 || nb.north >= 0);
+    one_phase_ = corner_cells && nb.diagonals_known();
+    corners_ = corner_cells && !one_phase_;  // two-phase mode
+    // x faces span the y ghosts too in two-phase corner mode
     const size_t xrow0 = corners_ ? 0 : gy, xrows = corners_ ? ny_ + 2 * gy : ny_;
     std::vector<comm::Msg> recvs, sends;
     auto x_face = [&](int peer, size_t send_row, size_t recv_row, int send_tag, int recv_tag) {
@@ -63,6 +77,27 @@ class Halo2D {
     if (gx > 0) {
       if (nb.west >= 0) x_face(nb.west, gx, 0, kTagLow, kTagHigh);
       if (nb.east >= 0) x_face(nb.east, nx_, gx + nx_, kTagHigh, kTagLow);
+    }
+    if (one_phase_) {
+      // gx x gy blocks: send rows/cols are the interior corner, recv the ghost corner
+      auto corner = [&](int peer, size_t srow, size_t scol, size_t rrow, size_t rcol, int stag,
+                        int rtag) {
+        if (peer < 0) return;
+        Face fc;
+        fc.sbuf = Buffer<double>(static_cast<size_t>(gx) * gy, buf_space);
+        fc.rbuf = Buffer<double>(static_cast<size_t>(gx) * gy, buf_space);
+        fc.send = f_.sub(srow, gx, scol, gy);
+        fc.recv = f_.sub(rrow, gx, rcol, gy);
+        sends.push_back({fc.sbuf.data(), fc.sbuf.bytes(), peer, stag});
+        recvs.push_back({fc.rbuf.data(), fc.rbuf.bytes(), peer, rtag});
+        xfaces_.push_back(std::move(fc));
+      };
+      const size_t lo = gx, hi = nx_, glo = 0, ghi = gx + nx_;  // rows (x)
+      const size_t clo = gy, chi = ny_, gclo = 0, gchi = gy + ny_;  // cols (y)
+      corner(nb.sw, lo, clo, glo, gclo, kTagSW, kTagNE);
+      corner(nb.se, hi, clo, ghi, gclo, kTagSE, kTagNW);
+      corner(nb.nw, lo, chi, glo, gchi, kTagNW, kTagSE);
+      corner(nb.ne, hi, chi, ghi, gchi, kTagNE, kTagSW);
     }
     auto y_face = [&](int peer, size_t send_col, size_t recv_col, int send_tag, int recv_tag) {
       // whole columns: contiguous from the first row of column c to the last
@@ -105,7 +140,8 @@ class Halo2D {
   }
 
   bool active() const { return ex_ != nullptr; }
-  bool corners() const { return corners_; }
+  bool corners() const { return corners_ || one_phase_; }
+  bool one_phase() const { return one_phase_; }
   // the whole exchange is stream-ordered (capturable into a hipGraph)
   bool capturable() const {
     return (!ex_ || ex_->graph_capturable()) && (!ex_x_ || ex_x_->graph_capturable());
@@ -113,7 +149,10 @@ class Halo2D {
   size_t bytes_sent() const { return bytes_; }
   size_t messages() const { return nmsg_; }
 
-  void start(gmt_stream_t s) {
+  // packed: optional event recorded once the send buffers are packed, just
+  // before the transport launches (a caller can hold its compute launch on
+  // it so the transfer kernels are dispatched first and get CUs)
+  void start(gmt_stream_t s, gmt_event_t packed = nullptr) {
     if (!ex_) return;
     fault_point_exchange(t_.rank());
     if (corners_) {  // y faces complete before the x faces (with their corners) are packed
@@ -122,10 +161,12 @@ class Halo2D {
       ex_->wait(s);
       unpack_y_faces(s);
       pack_x_faces(s);
+      if (packed) GMT_CHECK("event", gmt_rt_event_record(packed, s));
       ex_x_->start(s);
       return;
     }
     pack(s);
+    if (packed) GMT_CHECK("event", gmt_rt_event_record(packed, s));
     ex_->start(s);
   }
   void finish(gmt_stream_t s) {
@@ -161,8 +202,8 @@ class Halo2D {
     pack_y_faces(s);
   }
   void unpack(gmt_stream_t s) {
-    unpack_x_faces(s);
-    unpack_y_faces(s);
+    unpack_y_faces(s);  // first: packed y faces carry stale corner ghosts
+    unpack_x_faces(s);  // x faces and (one-phase mode) the corner blocks
   }
   void pack_x_faces(gmt_stream_t s) {
     if (xfaces_.empty()) return;
@@ -197,7 +238,8 @@ class Halo2D {
   size_t nx_ = 0, ny_ = 0;
   Neighbors nb_;
   std::vector<Face> xfaces_, yfaces_;
-  bool corners_ = false;
+  bool corners_ = false;    // two-phase corner mode
+  bool one_phase_ = false;  // corner blocks to the diagonal neighbours
   std::unique_ptr<comm::Exchange> ex_;    // all faces, or the y faces in corner mode
   std::unique_ptr<comm::Exchange> ex_x_;  // x faces in corner mode
   size_t bytes_ = 0, nmsg_ = 0;

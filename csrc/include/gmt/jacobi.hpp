@@ -104,7 +104,8 @@ class JacobiSolver {
   std::unique_ptr<Halo2D> halo_[2];
   Buffer<double> resid_ws_;
   gmt_stream_t s_ = nullptr, cs_ = nullptr;
-  gmt_event_t ev_start_ = nullptr, ev_halo_ = nullptr;
+  gmt_event_t ev_start_ = nullptr, ev_halo_ = nullptr, ev_packed_ = nullptr;
+  bool core_after_pack_ = true;
   gmt_graph_t graph_[2] = {nullptr, nullptr};   // single sweep, per parity
   gmt_graph_t graph2_[2] = {nullptr, nullptr};  // fused ks_-sweep block, per parity
   int parity_ = 0;  // buf_[parity_] holds the current u

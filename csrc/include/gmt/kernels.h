@@ -120,6 +120,11 @@ int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int halo
  * the LDS-tiled one (jacobi5x2.hip, nsweeps 2..4; tile = (TX << 16) | TY,
  * or tile = 0 with nsweeps = 3). */
 #define GMT_XK_PIPE 0x40000000
+/* With GMT_XK_PIPE: the caller allows interior cells outside the rects to be
+ * rewritten with their own K-sweep values (e.g. a frame pass after the core
+ * pass), so rects narrower than a 128 - 2K column strip still take the
+ * branch-free path. */
+#define GMT_XK_EXT 0x20000000
 int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
                   const double* u, double* un, int64_t ld, int tile, void* stream);
 /* Register-pipelined K-sweep kernel: one wave per 128-column strip and

@@ -40,7 +40,7 @@ namespace gmt {
 // one HBM latency per step) finish in tens of microseconds instead of one
 // long segment's worth (0.68 ms of a 4.2 ms pass at 256 rows per wave,
 // profiles/r01_pipe.md).
-constexpr int kMaxPipeRect = 20;
+constexpr int kMaxPipeRect = 24;  // 4 input rects x (2 fast + 4 rule bands)
 
 struct PipeArgs {
   int64_t r[kMaxPipeRect][4];        // output rects: x0, nx, y0, ny (absolute array coordinates, x0 even)
@@ -267,28 +267,64 @@ void jacobi5pipe_kernel(PipeArgs a, const double* __restrict__ u, double* __rest
 
 namespace {
 
-// Split rect r into the fast core (whole strips whose K-step influence cone
-// stays inside dom) and the rule bands around it: top, bottom, left, right.
-// Returns false if the core is empty; r then stays one rule rect.
-bool split_rect(const int64_t* r, const int64_t* dom, int K, int64_t wout, int64_t core[4],
-                int64_t band[4][4]) {
+// Split rect r into fast rects (whole strips, branch-free path) and rule
+// bands (ghost rule / partial strips).  A cell may take the fast path when
+// every load of its K-step cone is valid data that the kernel may update:
+// interior cells, and ghost cells of sides whose ring belongs to a neighbour
+// (halo_mask bit set: the caller exchanged a K-wide halo, corners included,
+// and the rule would update those cells anyway).  So the fast limits are the
+// interior inset by K on Dirichlet sides only.
+//
+// Columns: full strips of wout outputs from fx0; a leftover narrower than a
+// strip becomes one more full strip shifted left to end at fx1 (its overlap
+// with the previous strip is recomputed — the same operations on the same
+// inputs, so the same bits, written twice).  With `ext`, a rect narrower
+// than a strip may also be covered by a strip reaching outside the rect
+// (still within the fast limits): the caller allows cells of the interior
+// outside its rects to be rewritten with their own values, e.g. the frame
+// pass after the core pass has written them.  An odd leftover column the
+// shifted strip cannot reach (16-B aligned starts) goes to the rule band.
+// Returns the number of fast rects (0: the whole rect is one rule band).
+int split_rect(const int64_t* r, const int64_t* dom, int mask, bool ext, int K, int64_t wout,
+               int64_t fast[2][4], int64_t band[4][4]) {
   const int64_t x0 = r[0], x1 = r[0] + r[1], y0 = r[2], y1 = r[2] + r[3];
-  const int64_t fy0 = std::max(y0, dom[2] + K), fy1 = std::min(y1, dom[2] + dom[3] - K);
-  int64_t fx0 = std::max(x0, dom[0] + K);
+  const int64_t lx = dom[0] + ((mask & 1) ? 0 : K), ux = dom[0] + dom[1] - ((mask & 2) ? 0 : K);
+  const int64_t ly = dom[2] + ((mask & 4) ? 0 : K), uy = dom[2] + dom[3] - ((mask & 8) ? 0 : K);
+  const int64_t fy0 = std::max(y0, ly), fy1 = std::min(y1, uy);
+  int64_t fx0 = std::max(x0, lx);
   fx0 += fx0 & 1;  // even: 16-B loads
-  const int64_t fx1 = std::min(x1, dom[0] + dom[1] - K);
-  if (fy1 <= fy0 || fx1 - fx0 < wout) return false;
-  const int64_t cx1 = fx0 + (fx1 - fx0) / wout * wout;
-  const int64_t c[4] = {fx0, cx1 - fx0, fy0, fy1 - fy0};
+  const int64_t fx1 = std::min(x1, ux);
+  if (fy1 <= fy0 || fx1 <= fx0) return 0;
+  const int64_t cx1 = fx0 + (fx1 - fx0) / wout * wout;  // end of the whole strips
+  // the shifted strip goes first: waves run in rect order, and its few long
+  // segments must not be the launch's tail
+  int nf = 0;
+  int64_t xend = cx1;  // first column not covered by a fast rect
+  if (cx1 < fx1) {
+    // one more strip [sx, sx + wout): even start, inside the fast limits,
+    // starting at or before cx1 (inside the rect unless ext)
+    int64_t sx = (fx1 - wout) & ~int64_t(1);
+    const int64_t lo = ext ? lx : fx0;
+    if (sx < lo) sx = lo + (lo & 1);
+    if (sx <= cx1 && sx + wout <= ux && sx + wout > cx1 && (ext || sx + wout <= fx1)) {
+      const int64_t c[4] = {sx, wout, fy0, fy1 - fy0};
+      std::copy(c, c + 4, fast[nf++]);
+      xend = sx + wout;
+    }
+  }
+  if (cx1 > fx0) {
+    const int64_t c[4] = {fx0, cx1 - fx0, fy0, fy1 - fy0};
+    std::copy(c, c + 4, fast[nf++]);
+  }
+  if (nf == 0) return 0;
+  xend = std::min(xend, x1);
   const int64_t b[4][4] = {{x0, x1 - x0, y0, fy0 - y0},
                            {x0, x1 - x0, fy1, y1 - fy1},
                            {x0, fx0 - x0, fy0, fy1 - fy0},
-                           {cx1, x1 - cx1, fy0, fy1 - fy0}};
-  for (int j = 0; j < 4; ++j) {
-    core[j] = c[j];
-    for (int i = 0; i < 4; ++i) band[i][j] = b[i][j];
-  }
-  return true;
+                           {xend, x1 - xend, fy0, fy1 - fy0}};
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) band[i][j] = b[i][j];
+  return nf;
 }
 
 }  // namespace
@@ -307,6 +343,7 @@ extern "C" int gmt_jacobi5xk_pipe(int nsweeps, int n_rect, const int64_t* rects,
   const bool single = (seg >> 21) & 1;    // one kernel for both paths (A/B)
   const bool nosplit = (seg >> 22) & 1;   // two kernels, per-wave classification (A/B)
   const int rule_rows = (seg >> 23) & 0x3f ? (seg >> 23) & 0x3f : (nsweeps >= 10 ? 32 : 16);
+  const bool ext = (seg >> 29) & 1;       // GMT_XK_EXT: may rewrite interior cells outside the rects
   const bool classified = !single && !nosplit;
   a.quarter = 0.25;
   a.mask = halo_mask;
@@ -316,22 +353,35 @@ extern "C" int gmt_jacobi5xk_pipe(int nsweeps, int n_rect, const int64_t* rects,
   // rule rects first, then the fast cores: each kernel's waves are one range
   int64_t rl[kMaxPipeRect][4], fl[kMaxPipeRect][4];
   int nr = 0, nf = 0;
+  int fgroup[kMaxPipeRect];  // fast rect -> index of the widest fast rect of its input rect
   for (int k = 0; k < n_rect; ++k) {
     const int64_t* r = rects + 4 * k;
     if (r[1] <= 0 || r[3] <= 0) continue;
     if ((r[0] % 2) != 0) return static_cast<int>(hipErrorInvalidValue);  // 16-B loads
     // the K-wide ring left of / above the rect must exist (relative to u)
     if (r[0] < nsweeps || r[2] < nsweeps) return static_cast<int>(hipErrorInvalidValue);
-    int64_t core[4], band[4][4];
-    if (classified && split_rect(r, dom, nsweeps, wout, core, band)) {
-      std::copy(core, core + 4, fl[nf++]);
+    int64_t core[2][4], band[4][4];
+    const int ncore = classified ? split_rect(r, dom, halo_mask, ext, nsweeps, wout, core, band) : 0;
+    if (ncore > 0) {
+      const int widest = nf + (ncore == 2 && core[1][1] > core[0][1] ? 1 : 0);
+      for (int c = 0; c < ncore; ++c) {
+        fgroup[nf] = widest;
+        std::copy(core[c], core[c] + 4, fl[nf++]);
+      }
       for (auto& b : band)
         if (b[1] > 0 && b[3] > 0) std::copy(b, b + 4, rl[nr++]);
     } else {
       std::copy(r, r + 4, rl[nr++]);
     }
   }
-  auto add = [&](const int64_t* r, bool rule) {
+  // default rows per wave of a rect (see add)
+  auto auto_seg = [&](const int64_t* r) {
+    const int64_t ns = (r[1] + wout - 1) / wout;
+    int sg = nsweeps >= 6 && nsweeps < 12 ? 128 : 256;
+    while (sg > 16 && ns * ((r[3] + sg - 1) / sg) < 4096) sg /= 2;
+    return sg;
+  };
+  auto add = [&](const int64_t* r, bool rule, int sg_fast) {
     for (int j = 0; j < 4; ++j) a.r[a.n][j] = r[j];
     a.nstrip[a.n] = (r[1] + wout - 1) / wout;
     // fast core: 128 rows per wave at K = 6..10, else 256, halved (down to
@@ -339,18 +389,18 @@ extern "C" int gmt_jacobi5xk_pipe(int nsweeps, int n_rect, const int64_t* rects,
     // still fill 256 CUs; the pipeline refill costs 2K extra rows per
     // segment).  Rule bands: 16 rows, 32 at K >= 10 (or (seg >> 23) & 63) —
     // latency-bound waves, so many short ones (measured, profiles/r01_k12.md).
+    // A shifted last strip takes its main core's length: the XCD swizzle
+    // gives every XCD the same NUMBER of blocks, so a run of short-segment
+    // blocks (all on one XCD) would leave the other seven a longer tail.
     int sg = rule && classified ? rule_rows : seg_rows;
-    if (sg <= 0) {
-      sg = nsweeps >= 6 && nsweeps < 12 ? 128 : 256;
-      while (sg > 16 && a.nstrip[a.n] * ((r[3] + sg - 1) / sg) < 4096) sg /= 2;
-    }
+    if (sg <= 0) sg = rule ? auto_seg(r) : sg_fast;
     a.seg[a.n] = sg;
     a.wstart[a.n + 1] = a.wstart[a.n] + a.nstrip[a.n] * ((r[3] + sg - 1) / sg);
     ++a.n;
   };
-  for (int i = 0; i < nr; ++i) add(rl[i], true);
+  for (int i = 0; i < nr; ++i) add(rl[i], true, 0);
   const int64_t nrule = a.wstart[a.n];
-  for (int i = 0; i < nf; ++i) add(fl[i], false);
+  for (int i = 0; i < nf; ++i) add(fl[i], false, auto_seg(fl[fgroup[i]]));
   const int64_t waves = a.wstart[a.n];
   if (waves == 0) return 0;
   for (int k = a.n + 1; k <= kMaxPipeRect; ++k) a.wstart[k] = a.wstart[a.n];

@@ -256,6 +256,7 @@ def jacobi5_rects(u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, 
 
 
 XK_PIPE = 0x40000000  # gmt_jacobi5xk tile flag: register-pipelined kernel (jacobi5pipe.hip)
+XK_EXT = 0x20000000   # with XK_PIPE: interior cells outside the rects may be rewritten (own values)
 
 
 def _check_xk_bounds(k: int, u: torch.Tensor, un: torch.Tensor, rects) -> None:

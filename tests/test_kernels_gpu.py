@@ -366,3 +366,50 @@ def test_jacobi5xk_pipelined_frame_rects(k):
     outside = torch.ones_like(u, dtype=torch.bool)
     outside[g:g + ny, xo:xo + nx] = False
     assert bool((split[outside] == 7.0).all())
+
+
+def _engine_frame(k, xo, nx, g, ny, mask):
+    """The engine's overlapped block step (csrc/engine/jacobi.cpp
+    enqueue_block): core inset only on halo sides, K-wide frame bands along
+    the halo sides."""
+    ka = (k + 1) & ~1
+    hw, he, hs, hn = mask & 1, mask & 2, mask & 4, mask & 8
+    xr = (xo + nx - k) & ~1
+    cx0, cx1 = (xo + ka if hw else xo), (xr if he else xo + nx)
+    cy0, cy1 = (g + k if hs else g), (g + ny - k if hn else g + ny)
+    frame = []
+    if hs:
+        frame.append((xo, nx, g, k))
+    if hn:
+        frame.append((xo, nx, g + ny - k, k))
+    if hw:
+        frame.append((xo, ka, cy0, cy1 - cy0))
+    if he:
+        frame.append((xr, xo + nx - xr, cy0, cy1 - cy0))
+    return (cx0, cx1 - cx0, cy0, cy1 - cy0), frame
+
+
+@pytest.mark.parametrize("k", [2, 8, 12])
+@pytest.mark.parametrize("mask", [15, 0, 1, 2, 5, 10, 12, 3])
+@pytest.mark.parametrize("ny,nx", [(90, 400), (130, 233), (64, 1031)])
+def test_jacobi5xk_pipelined_engine_frame_ext(k, mask, ny, nx):
+    """Mask-aware fast path + shifted last strips + GMT_XK_EXT frame bands
+    (strips reaching into the finished core) == one full launch, bitwise, and
+    nothing outside the interior is written."""
+    g, xo = k, max(8, k)
+    u = _rand(ny + 2 * g, (xo + nx + max(8, k) + 1) // 2 * 2, seed=73)
+    dom = (xo, nx, g, ny)
+    full = torch.zeros_like(u)
+    ops.jacobi5xk(k, u, full, [dom], dom, mask)
+    exp = torch.zeros(u.shape, dtype=torch.float64)
+    ref.jacobi5xk(k, u.cpu(), exp, [dom], dom, mask)
+    split = torch.full_like(u, 7.0)
+    core, frame = _engine_frame(k, xo, nx, g, ny, mask)
+    ops.jacobi5xk(k, u, split, [core], dom, mask)
+    ops.jacobi5xk(k, u, split, frame, dom, mask, ops.XK_PIPE | ops.XK_EXT)
+    torch.cuda.synchronize()
+    assert torch.equal(full[g:g + ny, xo:xo + nx].cpu(), exp[g:g + ny, xo:xo + nx])
+    assert torch.equal(split[g:g + ny, xo:xo + nx], full[g:g + ny, xo:xo + nx])
+    outside = torch.ones_like(u, dtype=torch.bool)
+    outside[g:g + ny, xo:xo + nx] = False
+    assert bool((split[outside] == 7.0).all())

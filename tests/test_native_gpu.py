@@ -1,0 +1,114 @@
+"""Native layer on a real MI355X: the Jacobi engine (libgmt_engine.so +
+libgmt_ccl.so, hipGraphs, high-priority exchange stream, RCCL) loaded into
+this process, and the HIP builds of the reference apps (build/bin) under
+MPICH with the transports a one-GPU box can run (RCCL with a single
+periodic rank, HIP IPC and host staging with oversubscribed ranks).
+
+Every check is against an independent reference: the NumPy serial Jacobi
+(engine), the analytic derivative / closed-form sums (apps, the reference's
+own self-checks), or a serial run of the whole problem
+(mpi_jacobi2d --check).
+"""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, gpu_available
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")]
+
+BIN = os.path.join(ROOT, "build", "bin")
+MPIRUN = "/opt/conda/bin/mpirun"
+
+
+@pytest.fixture(scope="module")
+def env():
+    from gpu_mpi_tests_amd.parallel import dist as gd
+
+    return gd.init(device="cuda")
+
+
+@pytest.mark.parametrize("ny,nx,steps", [(96, 130, 5), (255, 517, 27)])
+@pytest.mark.parametrize("tblock", [0, 2, 8, 12])
+@pytest.mark.parametrize("graph", [False, True])
+def test_engine_periodic_matches_serial(env, ny, nx, steps, tblock, graph):
+    from gpu_mpi_tests_amd import engine
+
+    e = engine.NativeJacobi(ny, nx, env, periodic=True, overlap=True, graph=graph, tblock=tblock)
+    try:
+        assert e.graph == graph and e.overlap
+        assert e.tsteps == (tblock if tblock else 1) or (tblock == 0 and not e.tblock)
+        e.run(steps)
+        e.synchronize()
+        got = e.interior()
+        assert e.halo_bytes > 0  # the periodic single rank exchanges with itself
+        assert e.residual() >= 0.0
+    finally:
+        e.close()
+    ref = engine.serial_jacobi(ny, nx, steps, True)
+    assert float(np.abs(got - ref).max()) < 1e-13
+
+
+@pytest.mark.parametrize("tblock", [0, 12])
+def test_engine_dirichlet_repeated_runs(env, tblock):
+    """run() called several times (graph replays of both parities) == one serial run."""
+    from gpu_mpi_tests_amd import engine
+
+    e = engine.NativeJacobi(200, 333, env, periodic=False, overlap=True, graph=True, tblock=tblock)
+    try:
+        for k in (1, 12, 7, 25):
+            e.run(k)
+        e.synchronize()
+        got = e.interior()
+    finally:
+        e.close()
+    ref = engine.serial_jacobi(200, 333, 45, False)
+    assert float(np.abs(got - ref).max()) < 1e-13
+
+
+def _app(args, np_=None, timeout=120):
+    exe = os.path.join(BIN, args[0])
+    if not os.path.exists(exe):
+        pytest.fail(f"{exe} not built (run make all / __graft_entry__.build())")
+    cmd = [exe, *args[1:]] if np_ is None else [MPIRUN, "-np", str(np_), exe, *args[1:]]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd="/tmp")
+    assert p.returncode == 0, f"{' '.join(cmd)} rc={p.returncode}\n{p.stdout[-3000:]}\n{p.stderr[-3000:]}"
+    return p.stdout
+
+
+def test_app_daxpy_reference_sum():
+    assert "SUM = 524800.000000" in _app(["daxpy", "--print=0"])
+
+
+def test_app_buf_view_selftest_on_gpu():
+    assert _app(["mpi_stencil2d_sycl", "--test-buf-view=33"]).rstrip().endswith("test_buf_view OK")
+
+
+@pytest.mark.parametrize("np_,transport", [(1, "rccl"), (2, "ipc"), (2, "mpi-host"), (3, "ipc")])
+def test_app_jacobi_check(np_, transport):
+    periodic = ["--periodic"] if np_ == 1 else []
+    out = _app(["mpi_jacobi2d", "301", "19", "--check", "--tblock", "--tsteps=4", "--warmup=2",
+                f"--transport={transport}", *periodic], np_=np_)
+    m = re.search(r"check\s*: max\|diff\| vs serial = ([0-9.eE+-]+) OK", out)
+    assert m, out
+    assert float(m.group(1)) < 1e-12, out
+
+
+@pytest.mark.parametrize("transport", ["ipc", "mpi-host"])
+def test_app_stencil2d_gt_err_norm(transport):
+    # both dims share the reference's spacing 8/n_global_deriv, so the
+    # non-decomposed extent stays small to keep the round-off of x^3 + y^2 low
+    out = _app(["mpi_stencil2d_gt", "64", "5", "--no-managed", "--n-other=300",
+                f"--transport={transport}"], np_=2)
+    errs = [float(v) for v in re.findall(r"err=([0-9.]+)", out)]
+    assert len(errs) == 4 and max(errs) < 1e-5, out
+    assert len(re.findall(r"allreduce=", out)) >= 2
+
+
+def test_app_mpi_daxpy_nvtx_sums():
+    out = _app(["mpi_daxpy_nvtx_unmanaged", "--iters=2"], np_=2)
+    assert len(re.findall(r"\d/2 ALLSUM", out)) == 2
