@@ -67,10 +67,10 @@ def _timed(env, fn_run, fn_sync, steps, warmup):
     return gdist.allreduce_max(dt, env)
 
 
-def bench_native(env, n, steps, warmup, overlap, dims, graph, variant, tblock):
+def bench_native(env, shape, steps, warmup, overlap, dims, graph, variant, tblock):
     from gpu_mpi_tests_amd.engine import NativeJacobi
 
-    eng = NativeJacobi(n, n, env, dims=dims, overlap=overlap, graph=graph, variant=variant,
+    eng = NativeJacobi(shape[0], shape[1], env, dims=dims, overlap=overlap, graph=graph, variant=variant,
                        tblock=tblock)
     dt = _timed(env, eng.run, eng.synchronize, steps, warmup)
     info = {"engine": "native", "graph": eng.graph, "overlap": eng.overlap, "tblock": eng.tblock,
@@ -80,10 +80,10 @@ def bench_native(env, n, steps, warmup, overlap, dims, graph, variant, tblock):
     return eng, dt, info
 
 
-def bench_torch(env, n, steps, warmup, overlap, dims):
+def bench_torch(env, shape, steps, warmup, overlap, dims):
     from gpu_mpi_tests_amd.models.jacobi import Jacobi2D
 
-    solver = Jacobi2D(n, n, env=env, dims=dims, overlap=overlap)
+    solver = Jacobi2D(shape[0], shape[1], env=env, dims=dims, overlap=overlap)
     dt = _timed(env, solver.run, lambda: _sync(env), steps, warmup)
     ex = solver.ex[id(solver.u)]
     info = {"engine": "torch", "graph": False, "overlap": overlap, "tblock": False,
@@ -143,6 +143,9 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--size", type=int, default=32768, help="global domain is size x size (default 32768)")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong (default): the global domain is size x size for every N (the BASELINE "
+                         "config); weak: size x size PER GPU, global (py*size) x (px*size)"),
     ap.add_argument("--engine", choices=("native", "torch"), default="native")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
@@ -167,17 +170,23 @@ def main(argv=None):
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
     dims = tuple(int(v) for v in args.dims.lower().split("x")) if args.dims else None
     overlap = not args.no_overlap
+    gdims = dims if dims else choose_dims(env.world_size, args.size, args.size)
+    if args.scaling == "weak":
+        dims = gdims  # the per-GPU block stays size x size
+        shape = (args.size * gdims[0], args.size * gdims[1])
+    else:
+        shape = (args.size, args.size)
     engine = args.engine
     graph = args.graph == "on"
     if engine == "native":
-        solver, dt, info = bench_native(env, args.size, args.steps, args.warmup, overlap, dims,
+        solver, dt, info = bench_native(env, shape, args.steps, args.warmup, overlap, dims,
                                         graph, args.variant,
                                         (args.tsteps or DEFAULT_TSTEPS) if args.tblock == "on" else False)
     else:
         if env.is_gpu and args.variant:
             ops.set_jacobi_variant(args.variant)
-        solver, dt, info = bench_torch(env, args.size, args.steps, args.warmup, overlap, dims)
-    points = args.size * args.size
+        solver, dt, info = bench_torch(env, shape, args.steps, args.warmup, overlap, dims)
+    points = shape[0] * shape[1]
     mlups = points * args.steps / dt / 1e6
     ms_per_step = dt / args.steps * 1e3
     extras = {}
@@ -196,7 +205,7 @@ def main(argv=None):
         extras["daxpy_GBps_per_gpu"] = round(gbps / env.world_size, 1)
         extras["daxpy_n"] = args.daxpy_n
         extras["daxpy_ms"] = round(ddt * 1e3, 4)
-    py, px = info["dims"] if info.get("dims") else choose_dims(env.world_size, args.size, args.size)
+    py, px = info["dims"] if info.get("dims") else gdims
     if env.rank == 0:
         rec = {
             "metric": "2D 5-pt Jacobi stencil MLUPS (fp64, halo exchange overlapped)",
@@ -207,12 +216,12 @@ def main(argv=None):
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "fp64",
             "data": "synthetic (analytic x^3+y^2 initial field, Dirichlet boundary)",
             "config": {
-                "model": f"mpi_stencil2d jacobi5 {args.size}x{args.size} fp64",
+                "model": f"mpi_stencil2d jacobi5 {shape[0]}x{shape[1]} fp64",
                 "global_batch": points,
                 "seq_len": None,
                 "parallelism": f"spatial2d py{py} x px{px}, "

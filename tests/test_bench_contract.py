@@ -3,9 +3,10 @@ required keys, for 1 process and for 2 processes under torch.distributed.run
 (gloo; the GPU run uses RCCL through the native engine)."""
 import json
 import os
-import random
 import subprocess
 import sys
+
+from conftest import free_port
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
@@ -21,13 +22,13 @@ def _run(cmd, timeout=600):
     return json.loads(lines[0])
 
 
-def _check(rec, n, steps, warmup):
+def _check(rec, n, steps, warmup, scaling="strong", points=256 * 256):
     assert KEYS <= set(rec)
     assert rec["n_gpus"] == n and rec["steps"] == steps and rec["warmup"] == warmup
     assert rec["value"] > 0 and rec["unit"] == "MLUPS" and rec["higher_is_better"] is True
-    assert rec["dtype"] == "fp64" and rec["scaling"] == "strong"
+    assert rec["dtype"] == "fp64" and rec["scaling"] == scaling
     assert {"model", "global_batch", "seq_len", "parallelism"} <= set(rec["config"])
-    assert rec["config"]["global_batch"] == 256 * 256
+    assert rec["config"]["global_batch"] == points
 
 
 def test_bench_single_process_native_engine_cpu():
@@ -39,7 +40,7 @@ def test_bench_single_process_native_engine_cpu():
 
 
 def test_bench_two_ranks_torchrun_cpu():
-    port = str(random.randint(20000, 40000))
+    port = str(free_port())
     rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
                 "--device", "cpu", "--size", "256", "--steps", "3", "--warmup", "1",
@@ -51,7 +52,7 @@ def test_bench_two_ranks_torchrun_cpu():
 
 
 def test_bench_two_ranks_torch_engine_cpu():
-    port = str(random.randint(20000, 40000))
+    port = str(free_port())
     rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
                 "--device", "cpu", "--size", "256", "--steps", "3", "--warmup", "1",
@@ -59,3 +60,14 @@ def test_bench_two_ranks_torch_engine_cpu():
     _check(rec, 2, 3, 1)
     assert rec["config"]["engine"] == "torch"  # torch.distributed (gloo) P2P from Python
     assert rec["halo_exchange_us"] is not None and rec["halo_exchange_us"] > 0
+
+
+def test_bench_two_ranks_weak_scaling_cpu():
+    """--scaling weak: size x size per rank, the global domain grows with N."""
+    port = str(free_port())
+    rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
+                "--device", "cpu", "--size", "128", "--steps", "13", "--warmup", "1",
+                "--scaling", "weak", "--skip-extras"])
+    _check(rec, 2, 13, 1, scaling="weak", points=2 * 128 * 128)
+    assert rec["config"]["model"] == "mpi_stencil2d jacobi5 256x128 fp64"

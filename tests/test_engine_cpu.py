@@ -5,12 +5,12 @@ the libgmt.so SONAME, so one process may only ever bind one backend.
 """
 import json
 import os
-import random
 import subprocess
 import sys
 
 import pytest
 
+from conftest import free_port
 from native_util import ROOT, ensure_host_build
 
 CODE = r"""
@@ -87,7 +87,7 @@ def test_native_engine_multirank_rccl_semantics(np_, ny, nx, steps, periodic, ov
     send/recv, temporal-blocking halos with corners, residual all-reduce) at
     np_ ranks on the CPU backend: the result equals the serial sweep."""
     ensure_host_build()
-    port = str(random.randint(20000, 45000))
+    port = str(free_port())
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(np_),
            "--master-addr", "127.0.0.1", "--master-port", port,
            os.path.join(ROOT, "tests", "engine_mp_worker.py"), str(ny), str(nx), str(steps),

@@ -2,15 +2,15 @@
 distributed derivative test (reference test_deriv/test_sum) and distributed
 DAXPY + all-gather (reference mpi_daxpy_nvtx).  Values are the reference's
 closed forms."""
-import random
-
 import pytest
+
+from conftest import free_port
 
 from mp_util import run_dist
 
 
 def _port():
-    return random.randint(20000, 45000)
+    return free_port()
 
 
 def _deriv(env, dim, n_local, n_other):
