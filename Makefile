@@ -46,7 +46,8 @@ CCL_OBJ     := $(OBJ)/runtime/ccl_rccl.o
 HOST_OBJS   := $(OBJ)/host/kernels_host.o $(OBJ)/host/rt_host.o
 HOSTCCL_OBJ := $(OBJ)/host/ccl_host.o
 COMM_OBJS   := $(OBJ)/comm/transport_mpi.o $(OBJ)/comm/transport_core.o $(OBJ)/engine/jacobi.o
-ENG_OBJS    := $(OBJ)/comm/transport_core.o $(OBJ)/engine/jacobi.o $(OBJ)/engine/engine_capi.o
+ENG_OBJS    := $(OBJ)/comm/transport_core.o $(OBJ)/engine/jacobi.o $(OBJ)/engine/engine_capi.o \
+               $(OBJ)/engine/deriv_bench.o
 APP_HDRS    := $(wildcard csrc/include/gmt/*.hpp csrc/include/gmt/*.h csrc/apps/*.hpp)
 
 # reference binary names (Makefile:2, CMakeLists.txt:22-82) + MI355X additions

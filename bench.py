@@ -110,6 +110,25 @@ def halo_latency(env, solver, iters):
     return gdist.allreduce_max(dt, env)
 
 
+def ref_halo(env, n_local, n_other, iters):
+    """The reference's own headline measurement (mpi_stencil2d_gt test_deriv /
+    test_sum: 2-deep ghost faces of n_other doubles — 8 MiB at the defaults —
+    exchanged between 1-D slab neighbours, dim 0 packed, dim 1 in place, the
+    derivative kernel after each exchange; then the 1024-double all-reduce),
+    over RCCL on this job's GPUs.  Per-exchange median, max over ranks."""
+    from gpu_mpi_tests_amd.engine import deriv_bench
+
+    r = deriv_bench(n_local, n_other, n_iter=iters, n_warmup=5, env=env)
+    out = {"ref_halo_config": f"mpi_stencil2d_gt {n_local}x{n_other} per rank, 1-D slabs, "
+                              f"{iters} exchanges, rccl"}
+    for d in (0, 1):
+        out[f"ref_halo_dim{d}_us"] = round(gdist.allreduce_max(r[f"dim{d}"]["median_s"], env) * 1e6, 2)
+        out[f"ref_halo_dim{d}_err_norm"] = gdist.allreduce_max(r[f"dim{d}"]["err_norm"], env)
+    out["ref_halo_bytes_per_rank"] = int(gdist.allreduce_max(float(r["dim0"]["bytes"]), env))
+    out["ref_allreduce_1024_us"] = round(gdist.allreduce_max(r["allreduce_median_s"], env) * 1e6, 2)
+    return out
+
+
 def bench_daxpy(env, n, iters):
     """Per-GPU DAXPY rate (each rank on its own GPU), reported as whole-job GB/s."""
     dev = env.device
@@ -161,6 +180,11 @@ def main(argv=None):
     ap.add_argument("--dims", type=str, default=None, help="process grid PYxPX, e.g. 4x2")
     ap.add_argument("--daxpy-n", type=int, default=1 << 28)
     ap.add_argument("--skip-extras", action="store_true", help="headline stencil only")
+    ap.add_argument("--ref-n-local", type=int, default=1024,
+                    help="reference halo benchmark (N>1): n_local_deriv (mpi_stencil2d_gt default 1024)")
+    ap.add_argument("--ref-n-other", type=int, default=512 * 1024,
+                    help="reference halo benchmark: extent of the other axis (default 512Ki: 8 MiB faces)")
+    ap.add_argument("--ref-iters", type=int, default=100, help="reference halo benchmark: timed exchanges")
     ap.add_argument("--variant", type=int, default=0, help="jacobi kernel variant (0 auto,1 reg,2 lds,3 scalar)")
     ap.add_argument("--device", type=str, default=None, help="cuda|cpu (default: cuda if available)")
     args = ap.parse_args(argv)
@@ -200,6 +224,8 @@ def main(argv=None):
         del solver
         if env.is_gpu:
             torch.cuda.empty_cache()
+        if env.world_size > 1:
+            extras.update(ref_halo(env, args.ref_n_local, args.ref_n_other, args.ref_iters))
         gbps, ddt = bench_daxpy(env, args.daxpy_n, iters=20)
         extras["daxpy_GBps"] = round(gbps, 1)
         extras["daxpy_GBps_per_gpu"] = round(gbps / env.world_size, 1)

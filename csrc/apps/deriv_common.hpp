@@ -26,14 +26,13 @@
 
 #include "gmt/buffer.hpp"
 #include "gmt/comm.hpp"
+#include "gmt/deriv.hpp"
 #include "gmt/halo.hpp"
 #include "gmt/util.hpp"
 
 namespace gmt {
 namespace apps {
 
-constexpr double kDeriv5[5] = {1.0 / 12.0, -2.0 / 3.0, 0.0, 2.0 / 3.0, -1.0 / 12.0};
-constexpr double kPI = 3.141592653598793;  // the reference's constant, sic
 
 // One transport per kind for the whole run (RCCL communicators and IPC
 // streams are set up once, outside every timed loop).
@@ -55,19 +54,7 @@ class TransportPool {
   std::map<comm::Kind, std::unique_ptr<comm::Transport>> pool_;
 };
 
-struct DerivConfig {
-  int dim = 0;              // decomposed + derivative axis (0 = contiguous)
-  size_t n_local = 1024;    // extent along dim per rank
-  size_t n_other = 512 * 1024;
-  int n_iter = 1000, n_warmup = 5;
-  int space = GMT_SPACE_DEVICE;  // or GMT_SPACE_MANAGED
-  bool buf = true;               // reference `use_buffers` / `stage_host`
-  bool staged_is_host = true;    // dim 0 + buf means host staging (reference gt/sycl)
-  comm::Kind transport = comm::Kind::Auto;
-  bool host_init = false, host_verify = false;
-  bool realloc_per_call = false;  // emulate the gt version's per-call buffers
-  bool debug_dump = false;        // rank-serialised halo-row dumps (sycl_oo DEBUG build)
-};
+
 
 // Print rows [r0, r0+nr) of a column-major field (first <= 20 columns) for
 // every rank in rank order (mpi_stencil2d_sycl_oo.cc:636-659 serialises the
@@ -109,13 +96,7 @@ inline void dump_rows(MPI_Comm comm, int rank, int ws, const char* what, const d
   }
 }
 
-struct DerivResult {
-  double total_time = 0.0;  // seconds, this rank, timed iterations only
-  double err_norm = 0.0;
-  Stats iters;              // per-exchange seconds
-  std::string transport;
-  size_t bytes_per_exchange = 0;
-};
+
 
 inline comm::Kind pick_transport(const DerivConfig& c, const RankBinding& b) {
   if (c.transport != comm::Kind::Auto) return comm::resolve(c.transport, b);
@@ -125,189 +106,19 @@ inline comm::Kind pick_transport(const DerivConfig& c, const RankBinding& b) {
 
 inline DerivResult run_deriv(const DerivConfig& c, const RankBinding& b, MPI_Comm comm,
                              TransportPool& pool) {
-  const int ws = b.world_size, rank = b.rank;
-  const size_t n_bnd = 2;
-  const size_t n_global = c.n_local * ws;
-  const double ln = 8.0, delta = ln / n_global, scale = n_global / ln;
-  const double start = rank * (ln / ws);
-  const bool d0 = c.dim == 0;
-  const size_t nrows = d0 ? c.n_local + 2 * n_bnd : c.n_other;
-  const size_t ncols = d0 ? c.n_other : c.n_local + 2 * n_bnd;
-  const size_t nx_out = d0 ? c.n_local : c.n_other;
-  const size_t ny_out = d0 ? c.n_other : c.n_local;
-  gmt_stream_t s = nullptr;
-  GMT_CHECK("stream", gmt_rt_stream_create(&s, 0));
-
-  Buffer<double> z(nrows * ncols, c.space), dz(nx_out * ny_out, c.space);
-  Span2D<double> zf(z.data(), nrows, ncols);
-  // interior + physical-boundary ghosts (mpi_stencil2d_gt.cc:439-497)
-  const double x0 = d0 ? start : 0.0, y0 = d0 ? 0.0 : start;
-  if (c.host_init) {
-    std::vector<double> h(nrows * ncols, 0.0);
-    auto fn = [](double x, double y) { return x * x * x + y * y; };
-    const size_t gx = d0 ? n_bnd : 0, gy = d0 ? 0 : n_bnd;
-    for (size_t j = 0; j < ny_out; ++j)
-      for (size_t i = 0; i < nx_out; ++i)
-        h[(i + gx) + (j + gy) * nrows] = fn(x0 + i * delta, y0 + j * delta);
-    for (size_t k = 0; k < n_bnd; ++k) {
-      const double lo = (static_cast<double>(k) - n_bnd) * delta, hi = ln + k * delta;
-      for (size_t o = 0; o < (d0 ? ny_out : nx_out); ++o) {
-        if (d0) {
-          if (rank == 0) h[k + o * nrows] = fn(lo, o * delta);
-          if (rank == ws - 1) h[(n_bnd + c.n_local + k) + o * nrows] = fn(hi, o * delta);
-        } else {
-          if (rank == 0) h[o + k * nrows] = fn(o * delta, lo);
-          if (rank == ws - 1) h[o + (n_bnd + c.n_local + k) * nrows] = fn(o * delta, hi);
-        }
-      }
-    }
-    GMT_CHECK("z = h_z", gmt_rt_memcpy(z.data(), h.data(), z.bytes()));
-  } else {
-    GMT_CHECK("z = 0", gmt_rt_memset_async(z.data(), 0, z.bytes(), s));
-    if (d0) {
-      GMT_CHECK("fill", gmt_fill_poly(0, c.n_local, c.n_other, x0, delta, 0.0, delta,
-                                      &zf(n_bnd, 0), nrows, s));
-      if (rank == 0)
-        GMT_CHECK("fill lo", gmt_fill_poly(0, n_bnd, c.n_other, -(double)n_bnd * delta, delta,
-                                           0.0, delta, &zf(0, 0), nrows, s));
-      if (rank == ws - 1)
-        GMT_CHECK("fill hi", gmt_fill_poly(0, n_bnd, c.n_other, ln, delta, 0.0, delta,
-                                           &zf(n_bnd + c.n_local, 0), nrows, s));
-    } else {
-      GMT_CHECK("fill", gmt_fill_poly(0, c.n_other, c.n_local, 0.0, delta, y0, delta,
-                                      &zf(0, n_bnd), nrows, s));
-      if (rank == 0)
-        GMT_CHECK("fill lo", gmt_fill_poly(0, c.n_other, n_bnd, 0.0, delta,
-                                           -(double)n_bnd * delta, delta, &zf(0, 0), nrows, s));
-      if (rank == ws - 1)
-        GMT_CHECK("fill hi", gmt_fill_poly(0, c.n_other, n_bnd, 0.0, delta, ln, delta,
-                                           &zf(0, n_bnd + c.n_local), nrows, s));
-    }
-    GMT_CHECK("fill sync", gmt_rt_stream_synchronize(s));
-  }
-
-  const comm::Kind kind = pick_transport(c, b);
-  comm::Transport& tr = pool.get(kind);
-  Neighbors nb;
-  const int lo = rank > 0 ? rank - 1 : -1, hi = rank < ws - 1 ? rank + 1 : -1;
-  if (d0) {
-    nb.west = lo;
-    nb.east = hi;
-  } else {
-    nb.south = lo;
-    nb.north = hi;
-  }
-  const int gx = d0 ? static_cast<int>(n_bnd) : 0, gy = d0 ? 0 : static_cast<int>(n_bnd);
-  const bool pack_y = !d0 && c.buf;
-  const int buf_space = c.space;
-  auto halo = std::make_unique<Halo2D>(tr, zf, gx, gy, nb, pack_y, buf_space);
-
-  if (c.debug_dump && d0) {
-    dump_rows(comm, rank, ws, "send", z.data(), nrows, ncols, n_bnd, n_bnd);
-    dump_rows(comm, rank, ws, "send", z.data(), nrows, ncols, nrows - 2 * n_bnd, n_bnd);
-  }
-
-  DerivResult r;
-  r.transport = tr.name();
-  r.bytes_per_exchange = halo->bytes_sent();
-  for (int it = 0; it < c.n_warmup + c.n_iter; ++it) {
-    const double t0 = wtime();
-    if (c.realloc_per_call) halo = std::make_unique<Halo2D>(tr, zf, gx, gy, nb, pack_y, buf_space);
-    halo->exchange(s);
-    const double t1 = wtime();
-    if (it >= c.n_warmup) {
-      r.total_time += t1 - t0;
-      r.iters.add(t1 - t0);
-    }
-    if (c.debug_dump && d0 && it == 0) {
-      dump_rows(comm, rank, ws, "ghost", z.data(), nrows, ncols, 0, n_bnd);
-      dump_rows(comm, rank, ws, "ghost", z.data(), nrows, ncols, nrows - n_bnd, n_bnd);
-    }
-    // "do some calculation" between exchanges (mpi_stencil2d_gt.cc:528-534)
-    GMT_CHECK("stencil", gmt_stencil5_2d(c.dim, nx_out, ny_out, kDeriv5, scale, z.data(), nrows,
-                                         dz.data(), nx_out, s));
-    GMT_CHECK("stencil sync", gmt_rt_stream_synchronize(s));
-  }
-
-  // verification
-  const int mode = d0 ? 1 : 2;
-  if (c.host_verify) {
-    std::vector<double> h(nx_out * ny_out);
-    GMT_CHECK("h_dz = dz", gmt_rt_memcpy(h.data(), dz.data(), dz.bytes()));
-    double acc = 0.0;
-    for (size_t j = 0; j < ny_out; ++j)
-      for (size_t i = 0; i < nx_out; ++i) {
-        const double x = x0 + i * delta, y = y0 + j * delta;
-        const double a = d0 ? 3 * x * x : 2 * y;
-        const double d = h[i + j * nx_out] - a;
-        acc += d * d;
-      }
-    r.err_norm = std::sqrt(acc);
-  } else {
-    // the analytic derivative overwrites z (no longer needed), then one reduction
-    GMT_CHECK("fill exact", gmt_fill_poly(mode, nx_out, ny_out, x0, delta, y0, delta, z.data(),
-                                          nx_out, s));
-    const int64_t wn = gmt_diff_sq_workspace(nx_out, ny_out);
-    Buffer<double> ws_buf(wn + 1, GMT_SPACE_DEVICE);
-    GMT_CHECK("diff_sq", gmt_diff_sq(nx_out, ny_out, dz.data(), nx_out, z.data(), nx_out,
-                                     ws_buf.data(), ws_buf.data() + 1, s));
-    double acc = 0.0;
-    GMT_CHECK("err D2H", gmt_rt_memcpy_async(&acc, ws_buf.data(), sizeof(double), s));
-    GMT_CHECK("err sync", gmt_rt_stream_synchronize(s));
-    r.err_norm = std::sqrt(acc);
-  }
-  halo.reset();
-  gmt_rt_stream_destroy(s);
-  return r;
+  comm::Transport& tr = pool.get(pick_transport(c, b));
+  const int rank = b.rank, ws = b.world_size;
+  DumpFn dump = [&](const char* what, const double* f, size_t nr, size_t nc, size_t r0, size_t n) {
+    dump_rows(comm, rank, ws, what, f, nr, nc, r0, n);
+  };
+  return run_deriv_on(c, tr, rank, ws, dump);
 }
-
-// test_sum: axis reduction of a PI/world_size-filled array to 1024 values,
-// then a timed in-place all-reduce of them (mpi_stencil2d_gt.cc:574-649).
-struct SumResult {
-  double total_time = 0.0;
-  Stats iters;
-  double max_abs_err = 0.0;  // vs the analytic value (the reference does not check)
-  std::string transport;
-};
 
 inline SumResult run_sum(int dim, int space, size_t n_local, size_t n_other, int n_iter,
                          int n_warmup, comm::Kind want, const RankBinding& b, TransportPool& pool) {
-  const size_t nrows = dim == 0 ? n_local : n_other, ncols = dim == 0 ? n_other : n_local;
-  gmt_stream_t s = nullptr;
-  GMT_CHECK("stream", gmt_rt_stream_create(&s, 0));
-  Buffer<double> z(nrows * ncols, space);
-  // PI/world_size everywhere: reuse the analytic-fill kernel with a constant
-  // (mode 2 gives 2*y; y0 = PI/(2*ws), dy = 0)
-  GMT_CHECK("fill", gmt_fill_poly(2, nrows, ncols, 0.0, 0.0, kPI / (2.0 * b.world_size), 0.0,
-                                  z.data(), nrows, s));
-  const size_t n_sum = n_local;  // keep the decomposed axis: 1024 values in both dims
-  Buffer<double> sum(n_sum, space);
-  const int64_t wn = gmt_sum_axis_workspace(dim, nrows, ncols);
-  Buffer<double> wsb(wn > 0 ? wn : 1, GMT_SPACE_DEVICE);
   comm::Kind k = want != comm::Kind::Auto ? comm::resolve(want, b)
                                           : comm::resolve(comm::Kind::Auto, b, space == GMT_SPACE_MANAGED);
-  comm::Transport& tr = pool.get(k);
-  SumResult r;
-  r.transport = tr.name();
-  for (int it = 0; it < n_warmup + n_iter; ++it) {
-    GMT_CHECK("sum_axis", gmt_sum_axis(dim, nrows, ncols, z.data(), nrows, sum.data(),
-                                       wsb.data(), s));
-    GMT_CHECK("sum sync", gmt_rt_stream_synchronize(s));
-    const double t0 = wtime();
-    tr.allreduce_sum(sum.data(), n_sum, s);
-    GMT_CHECK("allreduce sync", gmt_rt_stream_synchronize(s));
-    const double t1 = wtime();
-    if (it >= n_warmup) {
-      r.total_time += t1 - t0;
-      r.iters.add(t1 - t0);
-    }
-  }
-  std::vector<double> h(n_sum);
-  GMT_CHECK("h_sum = sum", gmt_rt_memcpy(h.data(), sum.data(), sum.bytes()));
-  const double expect = kPI * static_cast<double>(n_other);
-  for (double v : h) r.max_abs_err = std::max(r.max_abs_err, std::fabs(v - expect) / expect);
-  gmt_rt_stream_destroy(s);
-  return r;
+  return run_sum_on(dim, space, n_local, n_other, n_iter, n_warmup, pool.get(k), b.world_size);
 }
 
 inline void device_tag(const RankBinding& b, char* out, size_t n) {

@@ -1,0 +1,49 @@
+// The reference's main benchmark (mpi_stencil2d_gt test_deriv / test_sum,
+// SURVEY.md §3.1) behind the MPI-free engine ABI (gmt/engine.h), so
+// bench.py can time the reference-shaped halo exchange over RCCL/xGMI on
+// every rank of a torch.distributed job: 8 MiB ghost faces per neighbour
+// (2 x 524288 doubles), dim 0 packed by the gfx950 copy kernel, dim 1
+// zero-copy, the derivative kernel after every exchange, err_norm against
+// the analytic derivative, then the 1024-double in-place all-reduce.
+#include <cstring>
+#include <memory>
+
+#include "gmt/deriv.hpp"
+#include "gmt/engine.h"
+
+extern "C" int gmt_engine_deriv_bench(int64_t n_local, int64_t n_other, int n_iter, int n_warmup,
+                                      int rank, int world, int transport, const void* ccl_id,
+                                      double* out) {
+  std::unique_ptr<gmt::comm::Transport> t;
+  if (transport == GMT_ENGINE_RCCL) {
+    gmt_ccl_id id;
+    std::memcpy(&id, ccl_id, sizeof(id));
+    t = gmt::comm::make_rccl_transport(rank, world, id);
+  } else {
+    if (world != 1) return 1;
+    t = gmt::comm::make_local_transport();
+  }
+  for (int dim = 0; dim < 2; ++dim) {
+    gmt::apps::DerivConfig c;
+    c.dim = dim;
+    c.n_local = static_cast<size_t>(n_local);
+    c.n_other = static_cast<size_t>(n_other);
+    c.n_iter = n_iter;
+    c.n_warmup = n_warmup;
+    c.buf = false;  // dim 0 packs into device buffers, dim 1 goes zero-copy
+    const gmt::apps::DerivResult r = gmt::apps::run_deriv_on(c, *t, rank, world);
+    double* o = out + 6 * dim;
+    o[0] = r.iters.median();
+    o[1] = r.iters.mean();
+    o[2] = r.iters.min();
+    o[3] = r.iters.max();
+    o[4] = static_cast<double>(r.bytes_per_exchange);
+    o[5] = r.err_norm;
+  }
+  const gmt::apps::SumResult s = gmt::apps::run_sum_on(0, GMT_SPACE_DEVICE, static_cast<size_t>(n_local),
+                                                       static_cast<size_t>(n_other), n_iter, n_warmup,
+                                                       *t, world);
+  out[12] = s.iters.median();
+  out[13] = s.max_abs_err;
+  return 0;
+}

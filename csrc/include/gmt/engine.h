@@ -34,6 +34,15 @@ int gmt_engine_jacobi_info(void* h, int64_t* out);
 int gmt_engine_jacobi_copy_interior(void* h, double* host);
 const char* gmt_engine_backend(void);
 
+/* The reference's halo-exchange benchmark (mpi_stencil2d_gt test_deriv for
+ * dim 0 and dim 1, then test_sum), n_local x n_other per rank, 2 ghosts,
+ * non-periodic 1-D slabs, on the RCCL transport (or local for world == 1).
+ * out[14]: per dim d (6 values at 6*d): exchange seconds median, mean, min,
+ * max, bytes sent per exchange, this rank's err_norm; out[12] = all-reduce
+ * (1024 doubles in place) median seconds, out[13] = its max relative error. */
+int gmt_engine_deriv_bench(int64_t n_local, int64_t n_other, int n_iter, int n_warmup, int rank,
+                           int world, int transport, const void* ccl_id, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -72,6 +72,8 @@ def load(device: str = "cuda") -> ctypes.CDLL:
     lib.gmt_engine_jacobi_copy_interior.argtypes = [vp, vp]
     lib.gmt_engine_jacobi_copy_interior.restype = c_int
     lib.gmt_engine_backend.restype = ctypes.c_char_p
+    lib.gmt_engine_deriv_bench.argtypes = [i64, i64, c_int, c_int, c_int, c_int, c_int, vp, vp]
+    lib.gmt_engine_deriv_bench.restype = c_int
     got = lib.gmt_engine_backend().decode()
     if got != kind:
         raise EngineError(f"{path} bound to the {got} runtime, expected {kind} "
@@ -168,6 +170,38 @@ class NativeJacobi:
             self.close()
         except Exception:
             pass
+
+
+def deriv_bench(n_local: int = 1024, n_other: int = 512 * 1024, n_iter: int = 100,
+                n_warmup: int = 5, env: "gdist.DistEnv | None" = None) -> dict:
+    """The reference's main benchmark on the native engine (one rank per GPU,
+    RCCL): ``mpi_stencil2d_gt``'s test_deriv for dim 0 and dim 1 (2-deep
+    ghost faces of ``n_other`` values per neighbour — 8 MiB at the reference
+    default — exchanged, then the derivative kernel, ``n_iter`` times) and
+    test_sum (in-place all-reduce of 1024 doubles).  Returns this rank's
+    per-exchange seconds (median/mean/min/max), bytes sent per exchange,
+    err_norm, and the all-reduce median seconds.  Collective: every rank calls it."""
+    e = env or gdist.get()
+    lib = load("cuda" if e.is_gpu else "cpu")
+    if e.world_size > 1:
+        transport = RCCL
+        cid = ctypes.create_string_buffer(_broadcast_unique_id(lib, e), 128)
+    else:
+        transport, cid = LOCAL, None
+    out = (ctypes.c_double * 14)()
+    err = lib.gmt_engine_deriv_bench(int(n_local), int(n_other), int(n_iter), int(n_warmup), e.rank,
+                                     e.world_size, transport, cid, out)
+    if err:
+        raise EngineError(f"gmt_engine_deriv_bench failed: {err}")
+    v = list(out)
+    res = {}
+    for d in (0, 1):
+        o = v[6 * d:6 * d + 6]
+        res[f"dim{d}"] = dict(median_s=o[0], mean_s=o[1], min_s=o[2], max_s=o[3], bytes=int(o[4]),
+                              err_norm=o[5])
+    res["allreduce_median_s"] = v[12]
+    res["allreduce_max_rel_err"] = v[13]
+    return res
 
 
 def serial_jacobi(ny: int, nx: int, steps: int, periodic: bool = False) -> np.ndarray:

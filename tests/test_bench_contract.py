@@ -44,11 +44,17 @@ def test_bench_two_ranks_torchrun_cpu():
     rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
                 "--device", "cpu", "--size", "256", "--steps", "3", "--warmup", "1",
-                "--daxpy-n", "20000"])
+                "--daxpy-n", "20000", "--ref-n-local", "32", "--ref-n-other", "300",
+                "--ref-iters", "4"])
     _check(rec, 2, 3, 1)
     # the GPU run's path: native engine, RCCL semantics (host emulation on CPU)
     assert rec["config"]["engine"] == "native" and rec["config"]["transport"] == "rccl-host"
     assert rec["halo_exchange_us"] is not None and rec["halo_exchange_us"] > 0
+    # the reference's own halo benchmark (test_deriv dim 0/1 + test_sum) on the same ranks
+    assert rec["ref_halo_dim0_us"] > 0 and rec["ref_halo_dim1_us"] > 0
+    assert rec["ref_halo_bytes_per_rank"] == 2 * 2 * 300 * 8 // 2  # edge ranks: one neighbour
+    assert rec["ref_halo_dim0_err_norm"] < 1e-6 and rec["ref_halo_dim1_err_norm"] < 1e-6
+    assert rec["ref_allreduce_1024_us"] > 0
 
 
 def test_bench_two_ranks_torch_engine_cpu():
@@ -56,7 +62,8 @@ def test_bench_two_ranks_torch_engine_cpu():
     rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
                 "--device", "cpu", "--size", "256", "--steps", "3", "--warmup", "1",
-                "--daxpy-n", "20000", "--engine", "torch"])
+                "--daxpy-n", "20000", "--engine", "torch", "--ref-n-local", "32",
+                "--ref-n-other", "300", "--ref-iters", "2"])
     _check(rec, 2, 3, 1)
     assert rec["config"]["engine"] == "torch"  # torch.distributed (gloo) P2P from Python
     assert rec["halo_exchange_us"] is not None and rec["halo_exchange_us"] > 0

@@ -112,3 +112,15 @@ def test_app_stencil2d_gt_err_norm(transport):
 def test_app_mpi_daxpy_nvtx_sums():
     out = _app(["mpi_daxpy_nvtx_unmanaged", "--iters=2"], np_=2)
     assert len(re.findall(r"\d/2 ALLSUM", out)) == 2
+
+
+def test_engine_deriv_bench_single_rank(env):
+    """bench.py's reference halo benchmark entry point (gmt_engine_deriv_bench)
+    on one GPU: no neighbours, so only the derivative kernel and err_norm."""
+    from gpu_mpi_tests_amd import engine
+
+    r = engine.deriv_bench(64, 300, n_iter=3, n_warmup=1, env=env)
+    for d in (0, 1):
+        assert r[f"dim{d}"]["bytes"] == 0
+        assert r[f"dim{d}"]["err_norm"] < 1e-6
+    assert r["allreduce_max_rel_err"] < 1e-12
