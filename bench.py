@@ -12,14 +12,14 @@ N=2^28 fp64 on one MI355X") and the measured halo-exchange latency.
 
 One step = one full Jacobi sweep of the global domain (every point updated
 once).  The native engine (C++, ``csrc/engine/jacobi.cpp``)
-runs the steps in fused passes of up to 12 sweeps by default (temporal
-blocking, ``--tblock on --tsteps 12``): one 12-wide halo exchange (RCCL over
+runs the steps in fused passes of up to 14 sweeps by default (temporal
+blocking, ``--tblock on --tsteps 14``): one 14-wide halo exchange (RCCL over
 xGMI on a high-priority stream, overlapped with the interior update) and one
 pass of the register-pipelined kernel (``csrc/kernels/jacobi5pipe.hip``) that
-reads u(t) once and writes u(t+12) once — bitwise the same result as twelve
-single sweeps, 1/12 of the HBM bytes.  The engine splits K steps into the
-cheapest sequence of passes (``JacobiSolver::plan_passes``): 100 steps = 7
-12-sweep passes + 2 8-sweep passes.  ``--tblock off`` runs one exchange + one
+reads u(t) once and writes u(t+14) once — bitwise the same result as fourteen
+single sweeps, 1/14 of the HBM bytes.  The engine splits K steps into the
+cheapest sequence of passes (``JacobiSolver::plan_passes``): 100 steps = 6
+14-sweep passes + 2 8-sweep passes.  ``--tblock off`` runs one exchange + one
 sweep per step; ``--engine torch`` runs the single-sweep algorithm through
 torch.distributed P2P from Python.  Nothing is skipped inside the timed
 region: K steps are K sweeps of every lattice point (an odd K ends with one single sweep).
@@ -41,7 +41,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-DEFAULT_TSTEPS = 12  # fused sweeps per memory pass / halo exchange (native engine; profiles/r01_k12.md)
+DEFAULT_TSTEPS = 14  # fused sweeps per memory pass / halo exchange (native engine; profiles/r01_k14.md)
 
 from gpu_mpi_tests_amd import ops  # noqa: E402
 from gpu_mpi_tests_amd.parallel import dist as gdist  # noqa: E402
@@ -176,7 +176,7 @@ def main(argv=None):
                     help="temporal blocking (native engine): --tsteps sweeps per memory pass and "
                          "per halo exchange; bitwise the same result as single sweeps")
     ap.add_argument("--tsteps", type=int, default=0,
-                    help="sweeps per fused pass with --tblock on (2-12; 0 = default %d)" % DEFAULT_TSTEPS)
+                    help="sweeps per fused pass with --tblock on (2-14; 0 = default %d)" % DEFAULT_TSTEPS)
     ap.add_argument("--dims", type=str, default=None, help="process grid PYxPX, e.g. 4x2")
     ap.add_argument("--daxpy-n", type=int, default=1 << 28)
     ap.add_argument("--skip-extras", action="store_true", help="headline stencil only")

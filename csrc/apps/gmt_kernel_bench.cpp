@@ -113,7 +113,7 @@ int main(int argc, char** argv) {
       }
     }
     // register-pipelined K-sweep kernel: rows per wave
-    for (int K = 2; K <= 12 && sec.find("pipe") != std::string::npos; K += 2) {
+    for (int K = 2; K <= 14 && sec.find("pipe") != std::string::npos; K += 2) {
       const int64_t g = K, xk = g > xo ? g : xo;  // the K-wide ring fits left of the interior
       const int64_t ld2 = ((xk + n + g + 63) / 64) * 64;
       Buffer<double> a(static_cast<size_t>(ld2) * (n + 2 * g), GMT_SPACE_DEVICE), b(a.size(), GMT_SPACE_DEVICE);

@@ -14,7 +14,7 @@
 //   --no-overlap --graph --periodic --warmup=W --variant=V (1 reg, 2 lds, 3 scalar, 9 pt)
 //   --tblock[=TY]           temporal blocking: 2 sweeps per pass and per exchange
 //                           (gmt_jacobi5x2; --tblock=TXxTY picks the tile, default 64x16)
-//   --tsteps=K              sweeps per fused pass with --tblock (2-12; default 2; 5 and 7
+//   --tsteps=K              sweeps per fused pass with --tblock (2-14; default 2; 5 and 7
 //                           round down to the register-pipelined kernel's even counts)
 //   --halo-iters=K          K blocking halo exchanges -> latency line
 //   --check                 rank 0 re-runs the whole problem serially on the host

@@ -71,8 +71,8 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   }
 
   ks_ = c.tsteps > 1 ? c.tsteps : (c.tblock ? 2 : 1);
-  if (ks_ > 12) ks_ = 12;
-  if (ks_ > 4 && ks_ % 2) --ks_;  // 5..12 sweeps: register-pipelined kernel, even counts only
+  if (ks_ > 14) ks_ = 14;
+  if (ks_ > 4 && ks_ % 2) --ks_;  // 5..14 sweeps: register-pipelined kernel, even counts only
   g_ = ks_;
   yo_ = g_;
   xo_ = round_up(g_, 8);  // ghost columns fit left of the interior; 64-B aligned interior
@@ -241,7 +241,7 @@ void JacobiSolver::step_block() {
 // flat in K up to 8 (HBM-bound: one read + one write of the field), so a
 // remainder is cheaper as two 8-passes than as a 12-pass plus a 4-pass.
 // 0 = no kernel for that K (odd K > 3).
-static constexpr double kPassCost[13] = {0, 3.05, 3.5, 4.5, 3.3, 0, 3.7, 0, 3.22, 0, 3.65, 0, 4.0};
+static constexpr double kPassCost[15] = {0, 3.05, 3.5, 4.5, 3.3, 0, 3.7, 0, 3.22, 0, 3.65, 0, 4.0, 0, 4.48};
 static constexpr double kPassOverhead = 0.05;  // launches + one halo exchange
 
 std::vector<int> JacobiSolver::plan_passes(int k) const {

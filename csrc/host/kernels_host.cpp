@@ -151,7 +151,7 @@ int gmt_jacobi5_rects(int n_rect, const int64_t* r, const double* u, double* un,
 
 int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom, int mask,
                   const double* u, double* un, int64_t ld, int tile, void*) {
-  if (n_rect < 0 || n_rect > 4 || nsweeps < 2 || nsweeps > 12) return 1;
+  if (n_rect < 0 || n_rect > 4 || nsweeps < 2 || nsweeps > 14) return 1;
   if (nsweeps > 4 && nsweeps % 2) return 1;  // same support matrix as the HIP build
   (void)tile;
   const int K = nsweeps;

@@ -58,7 +58,7 @@ struct PipeArgs {
 };
 
 constexpr int kPipeCols = 2 * kWave;  // columns per strip
-constexpr int kPipeMaxK = 12;         // sweeps per pass (even): K = 12 keeps 2 waves per SIMD
+constexpr int kPipeMaxK = 14;         // sweeps per pass (even): K = 14 still fits 2 waves per SIMD (254 VGPRs)
 
 // Waves per SIMD the fast path is held to (512 VGPRs / waves).  Without the
 // bound the scheduler interleaves all K independent levels of a step and the
@@ -440,7 +440,8 @@ extern "C" int gmt_jacobi5xk_pipe(int nsweeps, int n_rect, const int64_t* rects,
     case 6: run(std::integral_constant<int, 6>{}); break;
     case 8: run(std::integral_constant<int, 8>{}); break;
     case 10: run(std::integral_constant<int, 10>{}); break;
-    default: run(std::integral_constant<int, 12>{}); break;
+    case 12: run(std::integral_constant<int, 12>{}); break;
+    default: run(std::integral_constant<int, 14>{}); break;
   }
   GMT_RET_LAUNCH();
 }

@@ -278,7 +278,7 @@ def _check_xk_bounds(k: int, u: torch.Tensor, un: torch.Tensor, rects) -> None:
 
 def jacobi5xk(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, int, int, int]],
               dom: tuple[int, int, int, int], halo_mask: int = 0, tile: int = 0) -> None:
-    """``k`` (2-12) fused Laplace Jacobi sweeps (temporal blocking): ``un = J^k(u)`` on
+    """``k`` (2-14) fused Laplace Jacobi sweeps (temporal blocking): ``un = J^k(u)`` on
     each output rect (absolute coordinates, x0 even).  ``dom`` is the interior; bits
     of ``halo_mask`` (1 W, 2 E, 4 S, 8 N) mark ghost sides owned by a neighbour.
     ``tile``: 0 = default (register-pipelined kernel for even k, LDS tiles for k = 3),

@@ -326,7 +326,7 @@ def test_jacobi5xk_fused_k_sweeps(k, tile, ny, nx, mask):
     assert torch.equal(un[g:g + ny, xo:xo + nx].cpu(), exp[g:g + ny, xo:xo + nx])
 
 
-@pytest.mark.parametrize("k", [2, 4, 6, 8, 10, 12])
+@pytest.mark.parametrize("k", [2, 4, 6, 8, 10, 12, 14])
 @pytest.mark.parametrize("seg", [0, 1, 5, 64, (1 << 19) | 7, (1 << 19) | 64, (2 << 19) | 33, (2 << 19) | 3,
                                  (1 << 21) | 16, (1 << 22) | 24])
 @pytest.mark.parametrize("ny,nx", [(1, 2), (7, 9), (40, 126), (33, 130), (70, 515), (301, 700)])
@@ -348,7 +348,7 @@ def test_jacobi5xk_pipelined(k, seg, ny, nx, mask):
     assert torch.equal(un[g:g + ny, xo:xo + nx].cpu(), exp[g:g + ny, xo:xo + nx])
 
 
-@pytest.mark.parametrize("k", [4, 8, 12])
+@pytest.mark.parametrize("k", [4, 8, 12, 14])
 def test_jacobi5xk_pipelined_frame_rects(k):
     """core + 4 frame rects (the engine's overlapped block step) == full launch,
     and the output never touches cells outside the rects."""
@@ -389,7 +389,7 @@ def _engine_frame(k, xo, nx, g, ny, mask):
     return (cx0, cx1 - cx0, cy0, cy1 - cy0), frame
 
 
-@pytest.mark.parametrize("k", [2, 8, 12])
+@pytest.mark.parametrize("k", [2, 8, 12, 14])
 @pytest.mark.parametrize("mask", [15, 0, 1, 2, 5, 10, 12, 3])
 @pytest.mark.parametrize("ny,nx", [(90, 400), (130, 233), (64, 1031)])
 def test_jacobi5xk_pipelined_engine_frame_ext(k, mask, ny, nx):

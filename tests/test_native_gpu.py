@@ -33,7 +33,7 @@ def env():
 
 
 @pytest.mark.parametrize("ny,nx,steps", [(96, 130, 5), (255, 517, 27)])
-@pytest.mark.parametrize("tblock", [0, 2, 8, 12])
+@pytest.mark.parametrize("tblock", [0, 2, 8, 12, 14])
 @pytest.mark.parametrize("graph", [False, True])
 def test_engine_periodic_matches_serial(env, ny, nx, steps, tblock, graph):
     from gpu_mpi_tests_amd import engine
@@ -53,7 +53,7 @@ def test_engine_periodic_matches_serial(env, ny, nx, steps, tblock, graph):
     assert float(np.abs(got - ref).max()) < 1e-13
 
 
-@pytest.mark.parametrize("tblock", [0, 12])
+@pytest.mark.parametrize("tblock", [0, 12, 14])
 def test_engine_dirichlet_repeated_runs(env, tblock):
     """run() called several times (graph replays of both parities) == one serial run."""
     from gpu_mpi_tests_amd import engine
