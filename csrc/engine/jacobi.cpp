@@ -236,12 +236,14 @@ void JacobiSolver::step_block() {
   parity_ ^= 1;  // u(t+ks) lives in the other buffer
 }
 
-// Relative cost of one fused pass of K sweeps on a large domain (ms at
-// 32768², gmt_kernel_bench, profiles/r01_k12.md): per-pass time is nearly
-// flat in K up to 8 (HBM-bound: one read + one write of the field), so a
-// remainder is cheaper as two 8-passes than as a 12-pass plus a 4-pass.
+// Cost of one fused pass of K sweeps on a large domain (ms at 32768², fast +
+// ghost-rule kernels; rocprofv3 of bench.py, profiles/r01_k14.md; K <= 6
+// from gmt_kernel_bench, profiles/r01_k12.md): per-pass time is nearly flat
+// in K up to 8 (HBM-bound: one read + one write of the field), and K = 12 is
+// the cheapest per sweep; 14-sweep passes pay off as remainder fillers
+// (100 steps = 6 x 12 + 2 x 14).
 // 0 = no kernel for that K (odd K > 3).
-static constexpr double kPassCost[15] = {0, 3.05, 3.5, 4.5, 3.3, 0, 3.7, 0, 3.22, 0, 3.65, 0, 4.0, 0, 4.48};
+static constexpr double kPassCost[15] = {0, 3.05, 3.5, 4.5, 3.3, 0, 3.7, 0, 3.44, 0, 4.10, 0, 4.13, 0, 4.99};
 static constexpr double kPassOverhead = 0.05;  // launches + one halo exchange
 
 std::vector<int> JacobiSolver::plan_passes(int k) const {

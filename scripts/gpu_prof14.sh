@@ -1,0 +1,10 @@
+#!/bin/bash
+# rocprofv3 kernel stats + trace of bench.py at the defaults (K = 14, eager).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+R=$PWD
+OUT=$R/gpurun_out/prof14
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/b -o bench -- python3 $R/bench.py --steps 100 --warmup 10 > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
