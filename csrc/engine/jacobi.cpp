@@ -239,11 +239,11 @@ void JacobiSolver::step_block() {
 // Cost of one fused pass of K sweeps on a large domain (ms at 32768², fast +
 // ghost-rule kernels; rocprofv3 of bench.py, profiles/r01_k14.md; K <= 6
 // from gmt_kernel_bench, profiles/r01_k12.md): per-pass time is nearly flat
-// in K up to 8 (HBM-bound: one read + one write of the field), and K = 12 is
-// the cheapest per sweep; 14-sweep passes pay off as remainder fillers
-// (100 steps = 6 x 12 + 2 x 14).
+// in K up to 8 (HBM-bound: one read + one write of the field); with the
+// multiply-free scaled levels K = 14 is the cheapest per sweep
+// (profiles/r01_scaled.md).
 // 0 = no kernel for that K (odd K > 3).
-static constexpr double kPassCost[15] = {0, 3.05, 3.5, 4.5, 3.3, 0, 3.7, 0, 3.44, 0, 4.10, 0, 4.13, 0, 4.99};
+static constexpr double kPassCost[15] = {0, 3.05, 3.5, 4.5, 3.3, 0, 3.7, 0, 3.41, 0, 4.05, 0, 4.03, 0, 4.45};
 static constexpr double kPassOverhead = 0.05;  // launches + one halo exchange
 
 std::vector<int> JacobiSolver::plan_passes(int k) const {

@@ -28,6 +28,7 @@
 // (halo_mask bit0..3 = W/E/S/N); otherwise it keeps its (boundary) value.
 // Waves whose influence cone stays inside the interior skip the rule.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 #include "gmt/kernels.h"
@@ -84,7 +85,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 // three-row prefetch queue actually stays in flight.
 // SKEW: level p of step s is row s - 2p computed from the three previous
 // steps (K independent levels per step) instead of row s - p (a K-deep chain).
-template <int K, bool FAST, bool SKEW>
+template <int K, bool FAST, bool SKEW, bool SCALE = true>
 __device__ __forceinline__ void pipe_strip(const PipeArgs& a, const double* __restrict__ u,
                                            double* __restrict__ un, int64_t ld, int lane,
                                            int64_t xs, int64_t xe, int64_t ys, int64_t ye) {
@@ -123,6 +124,11 @@ __device__ __forceinline__ void pipe_strip(const PipeArgs& a, const double* __re
   const uint32_t st_off1 = st1 ? static_cast<uint32_t>(c0 + 1 - xs) * 8u : kDrop;
   const uint32_t st_bytes = static_cast<uint32_t>(xe - xs) * 8u;
   auto store = [&](int s, d2 v) {
+    if constexpr (FAST && SCALE) {  // level K was kept scaled by 4^K (see level)
+      constexpr double kUnscale = 1.0 / static_cast<double>(1ull << (2 * K));
+      v.x *= kUnscale;
+      v.y *= kUnscale;
+    }
     double* row = un + (yl + s - LAG) * ld;
     // 0x00020000: raw-buffer descriptor word 3 for gfx9 (32-bit data format)
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(row + xs, 0, st_bytes, 0x00020000);
@@ -158,9 +164,18 @@ __device__ __forceinline__ void pipe_strip(const PipeArgs& a, const double* __re
 #pragma clang fp contract(off)
     const double w = dpp_from_lower(c.y), e = dpp_from_upper(c.x);
     d2 v;
-    // a.quarter == 0.25 exactly: any fma contraction of the scaling is exact
-    v.x = a.quarter * ((w + c.y) + (up_.x + dn.x));
-    v.y = a.quarter * ((c.x + e) + (up_.y + dn.y));
+    if constexpr (FAST && SCALE) {
+      // scaled levels: V_p = 4^p u_p, so V_p = (W + C) + (N + S) with no
+      // multiply (scaling by a power of two commutes with every rounding
+      // step: bitwise 4^p times the unscaled update, barring overflow and
+      // subnormals); the output is scaled back once per stored value
+      v.x = (w + c.y) + (up_.x + dn.x);
+      v.y = (c.x + e) + (up_.y + dn.y);
+    } else {
+      // a.quarter == 0.25 exactly: any fma contraction of the scaling is exact
+      v.x = a.quarter * ((w + c.y) + (up_.x + dn.x));
+      v.y = a.quarter * ((c.x + e) + (up_.y + dn.y));
+    }
     if constexpr (!FAST) {
       const int64_t r = yl + s - D * p;  // row of this level's value
       const bool ry = (r >= dy0 && r < dy1) || (r < dy0 ? gs : gn);
@@ -226,7 +241,7 @@ __device__ __forceinline__ void pipe_strip(const PipeArgs& a, const double* __re
 // with the skewed pipeline).
 // MODE 0: both paths in one kernel (A/B measurement), 1: fast waves only,
 // 2: the other waves only.
-template <int K, bool SKEW, int MODE>
+template <int K, bool SKEW, int MODE, bool SCALE = true>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(pipe_waves(K, MODE))))
 void jacobi5pipe_kernel(PipeArgs a, const double* __restrict__ u, double* __restrict__ un, int64_t ld,
                         int64_t nblocks) {
@@ -260,7 +275,7 @@ void jacobi5pipe_kernel(PipeArgs a, const double* __restrict__ u, double* __rest
     return;
   }
   if (!a.classified && fast != (MODE == 1)) return;
-  pipe_strip<K, MODE == 1, SKEW>(a, u, un, ld, lane, xs, xe, ys, ye);
+  pipe_strip<K, MODE == 1, SKEW, SCALE>(a, u, un, ld, lane, xs, xe, ys, ye);
 }
 
 }  // namespace gmt
@@ -409,13 +424,19 @@ extern "C" int gmt_jacobi5xk_pipe(int nsweeps, int n_rect, const int64_t* rects,
   // skewed (level-parallel) pipeline by default: fewer VGPRs for the fast
   // path at K = 6, 8 (measured, profiles/r01_pipe.md)
   const bool skew = sk == 0 ? nsweeps >= 6 : sk == 1;
+  static const bool scaled = [] {
+    const char* e = std::getenv("GMT_PIPE_SCALED");
+    return !(e && e[0] == '0');
+  }();
   auto launch = [&](auto KC, auto MC, int64_t w0, int64_t w1) {
     constexpr int KK = decltype(KC)::value, MODE = decltype(MC)::value;
     if (w1 <= w0) return;
     a.wbase = w0;
     a.wend = w1;
     const int64_t nb = (w1 - w0 + wpb - 1) / wpb;
-    if (skew)
+    if (MODE == 1 && !scaled)  // A/B: GMT_PIPE_SCALED=0 keeps the 0.25 multiply per level
+      jacobi5pipe_kernel<KK, true, MODE, false><<<grid_1d(nb), kBlock, 0, s>>>(a, u, un, ld, nb);
+    else if (skew)
       jacobi5pipe_kernel<KK, true, MODE><<<grid_1d(nb), kBlock, 0, s>>>(a, u, un, ld, nb);
     else
       jacobi5pipe_kernel<KK, false, MODE><<<grid_1d(nb), kBlock, 0, s>>>(a, u, un, ld, nb);
