@@ -11,6 +11,7 @@
 //   --weak                  n x n PER RANK (global = py*n x px*n)
 //   --dims=PYxPX            process grid (default: minimise halo bytes)
 //   --transport=auto|rccl|ipc|mpi-host|mpi-direct
+//   --overlap=auto          time overlapped and serial passes once, keep the faster
 //   --no-overlap --graph --periodic --warmup=W --variant=V (1 reg, 2 lds, 3 scalar, 9 pt)
 //   --tblock[=TY]           temporal blocking: 2 sweeps per pass and per exchange
 //                           (gmt_jacobi5x2; --tblock=TXxTY picks the tile, default 64x16)
@@ -98,6 +99,7 @@ int main(int argc, char** argv) {
   }
   c.periodic = cli.flag("periodic");
   c.overlap = !cli.flag("no-overlap");
+  c.overlap_auto = cli.get("overlap", "") == "auto";  // --overlap=auto: time both, keep the faster
   c.graph = cli.flag("graph");
   c.variant = static_cast<int>(cli.geti("variant", 0));
   c.tblock = cli.has("tblock") && cli.get("tblock", "1") != "0";

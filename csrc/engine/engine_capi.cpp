@@ -44,6 +44,7 @@ void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank,
   c.px = px;
   c.periodic = flags & 1;
   c.overlap = (flags & 2) != 0;
+  c.overlap_auto = (flags & 16) != 0;  // bit4: time both modes, keep the faster
   c.graph = (flags & 4) != 0;
   c.tblock = (flags & 8) != 0;
   c.tsteps = (flags >> 8) & 0xf;  // bits 8-11: sweeps per fused pass (0 = from bit 3)
@@ -89,6 +90,8 @@ int gmt_engine_jacobi_info(void* p, int64_t* out) {
   out[8] = h->py;
   out[9] = h->px;
   out[10] = s.tsteps();
+  out[11] = static_cast<int64_t>(s.tuned_overlap_s() * 1e9);  // overlap_auto timings, ns per pass
+  out[12] = static_cast<int64_t>(s.tuned_serial_s() * 1e9);
   return 0;
 }
 int gmt_engine_jacobi_copy_interior(void* p, double* host) {

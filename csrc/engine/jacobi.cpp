@@ -1,5 +1,6 @@
 // Native distributed Jacobi engine (gmt/jacobi.hpp).
 #include "gmt/jacobi.hpp"
+#include "gmt/util.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -91,20 +92,56 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
 
   // deterministic, decomposition-independent initial field and Dirichlet
   // ring: u(x, y) = x^3 + y^2 at global ghost-inclusive coordinates * h
-  const double h = 1.0 / (static_cast<double>(c.ny_global > c.nx_global ? c.ny_global : c.nx_global) + 1);
-  for (int b = 0; b < 2; ++b) {
-    buf_[b] = Buffer<double>(elems, GMT_SPACE_DEVICE);
-    GMT_CHECK("memset", gmt_rt_memset_async(buf_[b].data(), 0, buf_[b].bytes(), s_));
-    GMT_CHECK("fill", gmt_fill_poly(0, nx_ + 2 * g_, ny_ + 2 * g_, (ox_ - g_) * h, h,
-                                    (oy_ - g_) * h, h, buf_[b].data() + (xo_ - g_), ld_, s_));
-  }
-  GMT_CHECK("init sync", gmt_rt_stream_synchronize(s_));
+  for (int b = 0; b < 2; ++b) buf_[b] = Buffer<double>(elems, GMT_SPACE_DEVICE);
+  init_field();
   resid_ws_ = Buffer<double>(gmt_jacobi_resid_workspace(nx_, ny_) + 1, GMT_SPACE_DEVICE);
   for (int b = 0; b < 2; ++b) {
     Span2D<double> f(buf_[b].data() + (xo_ - g_), nx_ + 2 * g_, ny_ + 2 * g_, ld_);
     halo_[b] = std::make_unique<Halo2D>(t_, f, g_, g_, nb_, false, GMT_SPACE_DEVICE, ks_ > 1);
   }
+  if (c.overlap_auto) autotune_overlap();
   if (c.graph) capture_graphs();
+}
+
+void JacobiSolver::init_field() {
+  const JacobiConfig& c = cfg_;
+  const double h = 1.0 / (static_cast<double>(c.ny_global > c.nx_global ? c.ny_global : c.nx_global) + 1);
+  for (int b = 0; b < 2; ++b) {
+    GMT_CHECK("memset", gmt_rt_memset_async(buf_[b].data(), 0, buf_[b].bytes(), s_));
+    GMT_CHECK("fill", gmt_fill_poly(0, nx_ + 2 * g_, ny_ + 2 * g_, (ox_ - g_) * h, h,
+                                    (oy_ - g_) * h, h, buf_[b].data() + (xo_ - g_), ld_, s_));
+  }
+  GMT_CHECK("init sync", gmt_rt_stream_synchronize(s_));
+  parity_ = 0;
+}
+
+void JacobiSolver::autotune_overlap() {
+  if (ks_ < 2 || !halo_[0]->active()) return;  // nothing to hide
+  Buffer<double> t(2, GMT_SPACE_DEVICE);
+  double host[2] = {0.0, 0.0};
+  constexpr int kPasses = 3;
+  for (int mode = 0; mode < 2; ++mode) {
+    cfg_.overlap = mode == 0;
+    enqueue_block(parity_, ks_);  // warm-up (first use of the mode's streams)
+    parity_ ^= 1;
+    synchronize();
+    const double t0 = wtime();
+    for (int i = 0; i < kPasses; ++i) {
+      enqueue_block(parity_, ks_);
+      parity_ ^= 1;
+    }
+    synchronize();
+    host[mode] = (wtime() - t0) / kPasses;
+  }
+  // one decision for every rank: the mode with the smaller summed time
+  GMT_CHECK("tune H2D", gmt_rt_memcpy(t.data(), host, sizeof(host)));
+  t_.allreduce_sum(t.data(), 2, s_);
+  GMT_CHECK("tune D2H", gmt_rt_memcpy_async(host, t.data(), sizeof(host), s_));
+  GMT_CHECK("tune sync", gmt_rt_stream_synchronize(s_));
+  tune_s_[0] = host[0] / t_.size();
+  tune_s_[1] = host[1] / t_.size();
+  cfg_.overlap = host[0] <= host[1];
+  init_field();  // the timed passes advanced the solution: start over
 }
 
 JacobiSolver::~JacobiSolver() {

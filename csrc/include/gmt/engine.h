@@ -21,7 +21,8 @@ enum gmt_engine_transport { GMT_ENGINE_LOCAL = 0, GMT_ENGINE_RCCL = 1 };
 /* fills 128 bytes (an RCCL unique id); returns 0 or an error code */
 int gmt_engine_unique_id(void* out128);
 /* flags: bit0 periodic, bit1 overlap, bit2 graph, bit3 temporal blocking (2 sweeps/pass),
- * bits 8-11 sweeps per fused pass (2-4; overrides bit3).  ccl_id: 128 bytes (RCCL) or NULL (local) */
+ * bit4 overlap auto-tune (time both modes once, keep the faster on every rank),
+ * bits 8-11 sweeps per fused pass (2-14; overrides bit3).  ccl_id: 128 bytes (RCCL) or NULL (local) */
 void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank, int world,
                                int transport, const void* ccl_id, int flags, int variant);
 void gmt_engine_jacobi_destroy(void* h);
@@ -29,7 +30,8 @@ int gmt_engine_jacobi_run(void* h, int steps); /* enqueue `steps` steps */
 int gmt_engine_jacobi_sync(void* h);
 double gmt_engine_jacobi_residual(void* h);
 int gmt_engine_jacobi_exchange(void* h); /* one blocking halo exchange */
-/* out[11]: nx, ny, off_x, off_y, bytes_per_exchange, messages, graph, overlap, py, px, tsteps */
+/* out[13]: nx, ny, off_x, off_y, bytes_per_exchange, messages, graph, overlap, py, px, tsteps,
+ * overlap_auto ns per pass with overlap, without (0 if not tuned) */
 int gmt_engine_jacobi_info(void* h, int64_t* out);
 int gmt_engine_jacobi_copy_interior(void* h, double* host);
 const char* gmt_engine_backend(void);

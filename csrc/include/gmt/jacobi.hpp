@@ -40,6 +40,12 @@ struct JacobiConfig {
   int py = 1, px = 1;                            // process grid (rank = cy*px + cx)
   bool periodic = false;                         // else Dirichlet (fixed ghost ring)
   bool overlap = true;
+  // overlap_auto: time a few fused passes with and without overlap at
+  // construction (then restore the initial field) and keep the faster — the
+  // same choice on every rank (summed over ranks).  Whether hiding the
+  // exchange pays for the frame pass depends on the link (self-exchange on
+  // one GPU: serial 4-8 % faster, profiles/r01_frame.md); measure it.
+  bool overlap_auto = false;
   bool graph = false;
   int variant = 0;                               // gmt_jacobi5_set_variant
   // temporal blocking: tsteps (2-12) sweeps per memory pass (gmt_jacobi5xk;
@@ -83,6 +89,9 @@ class JacobiSolver {
   int ghost() const { return g_; }
   bool overlap_active() const { return cfg_.overlap && halo_[0] && halo_[0]->active(); }
   const Neighbors& neighbors() const { return nb_; }
+  // overlap_auto: seconds per pass measured {overlap, serial} (max over ranks), 0 if not tuned
+  double tuned_overlap_s() const { return tune_s_[0]; }
+  double tuned_serial_s() const { return tune_s_[1]; }
   gmt_stream_t stream() const { return s_; }
 
  private:
@@ -91,6 +100,8 @@ class JacobiSolver {
   void step_block();
   void sweep_full(int parity, double* resid);
   void capture_graphs();
+  void init_field();
+  void autotune_overlap();
   int halo_mask() const;
 
   comm::Transport& t_;
@@ -109,6 +120,7 @@ class JacobiSolver {
   gmt_graph_t graph_[2] = {nullptr, nullptr};   // single sweep, per parity
   gmt_graph_t graph2_[2] = {nullptr, nullptr};  // fused ks_-sweep block, per parity
   int parity_ = 0;  // buf_[parity_] holds the current u
+  double tune_s_[2] = {0.0, 0.0};
 };
 
 // Balanced block split of n over p parts: offset and length of part i.

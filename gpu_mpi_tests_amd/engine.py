@@ -98,7 +98,7 @@ class NativeJacobi:
 
     def __init__(self, ny: int, nx: int, env: "gdist.DistEnv | None" = None,
                  dims: tuple[int, int] | None = None, periodic: bool = False,
-                 overlap: bool = True, graph: bool = True, variant: int = 0,
+                 overlap: "bool | str" = True, graph: bool = True, variant: int = 0,
                  tblock: bool | int = False):
         from .parallel.decomp import choose_dims
 
@@ -119,16 +119,20 @@ class NativeJacobi:
             transport = RCCL
             cid = ctypes.create_string_buffer(_broadcast_unique_id(self.lib, e), 128)
         ks = 0 if not tblock else (2 if tblock is True else int(tblock))
-        flags = ((1 if periodic else 0) | (2 if overlap else 0) | (4 if graph else 0)
-                 | ((ks & 0xF) << 8))
+        # overlap: True / False / "auto" (time both once, every rank keeps the faster)
+        auto = overlap == "auto"
+        flags = ((1 if periodic else 0) | (2 if (overlap or auto) else 0) | (4 if graph else 0)
+                 | (16 if auto else 0) | ((ks & 0xF) << 8))
         self.h = self.lib.gmt_engine_jacobi_create(ny, nx, py, px, e.rank, e.world_size, transport,
                                                    cid, flags, variant)
         if not self.h:
             raise EngineError("gmt_engine_jacobi_create failed")
-        info = (ctypes.c_int64 * 11)()
+        info = (ctypes.c_int64 * 13)()
         self.lib.gmt_engine_jacobi_info(self.h, info)
         (self.nx, self.ny, self.off_x, self.off_y, self.halo_bytes, self.halo_msgs,
-         graph_on, overlap_on, _, _, tb) = list(info)
+         graph_on, overlap_on, _, _, tb, t_ov, t_ser) = list(info)
+        # overlap="auto": measured seconds per fused pass {overlap, serial} (mean over ranks)
+        self.tuned = {"overlap_s": t_ov / 1e9, "serial_s": t_ser / 1e9} if auto and t_ov else None
         self.tsteps = int(tb)
         self.tblock = self.tsteps > 1
         self.graph = bool(graph_on)

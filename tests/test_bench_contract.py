@@ -78,3 +78,17 @@ def test_bench_two_ranks_weak_scaling_cpu():
                 "--scaling", "weak", "--skip-extras"])
     _check(rec, 2, 13, 1, scaling="weak", points=2 * 128 * 128)
     assert rec["config"]["model"] == "mpi_stencil2d jacobi5 256x128 fp64"
+
+
+def test_bench_overlap_autotune_keeps_the_solution():
+    """--overlap auto times both modes on the real field at start-up, then
+    restores the initial field: the residual after K steps is the 1-rank one."""
+    common = ["--device", "cpu", "--size", "192", "--steps", "17", "--warmup", "2",
+              "--daxpy-n", "2000", "--ref-n-local", "16", "--ref-n-other", "64", "--ref-iters", "2"]
+    one = _run([sys.executable, "bench.py", *common])
+    port = str(free_port())
+    two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2", *common])
+    tuned = two["config"]["overlap_tuning"]
+    assert tuned and tuned["overlap_s"] > 0 and tuned["serial_s"] > 0
+    assert abs(two["residual_l2"] - one["residual_l2"]) <= 1e-12 * max(1.0, one["residual_l2"])

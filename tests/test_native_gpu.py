@@ -124,3 +124,20 @@ def test_engine_deriv_bench_single_rank(env):
         assert r[f"dim{d}"]["bytes"] == 0
         assert r[f"dim{d}"]["err_norm"] < 1e-6
     assert r["allreduce_max_rel_err"] < 1e-12
+
+
+def test_engine_overlap_autotune_periodic(env):
+    """overlap="auto" (bench.py default): both modes timed on the real field,
+    then the initial field restored — the result still equals the serial run."""
+    from gpu_mpi_tests_amd import engine
+
+    e = engine.NativeJacobi(300, 517, env, periodic=True, overlap="auto", graph=False, tblock=14)
+    try:
+        assert e.tuned and e.tuned["overlap_s"] > 0 and e.tuned["serial_s"] > 0
+        e.run(31)
+        e.synchronize()
+        got = e.interior()
+    finally:
+        e.close()
+    ref = engine.serial_jacobi(300, 517, 31, True)
+    assert float(np.abs(got - ref).max()) < 1e-13
