@@ -48,6 +48,13 @@ from gpu_mpi_tests_amd.parallel import dist as gdist  # noqa: E402
 from gpu_mpi_tests_amd.parallel.decomp import choose_dims  # noqa: E402
 
 
+def default_tsteps(shape, world):
+    """14 sweeps per pass, 12 for per-GPU domains below 2^27 points (8192² on
+    one GPU): there the 14-deep pipeline's warm-up and ghost-rule bands cost
+    more than its fewer passes save (profiles/r01_8192.md)."""
+    return DEFAULT_TSTEPS if shape[0] * shape[1] // max(1, world) >= (1 << 27) else 12
+
+
 def _sync(env):
     if env.is_gpu:
         torch.cuda.synchronize(env.device)
@@ -210,7 +217,8 @@ def main(argv=None):
     if engine == "native":
         solver, dt, info = bench_native(env, shape, args.steps, args.warmup, overlap, dims,
                                         graph, args.variant,
-                                        (args.tsteps or DEFAULT_TSTEPS) if args.tblock == "on" else False)
+                                        (args.tsteps or default_tsteps(shape, env.world_size))
+                                        if args.tblock == "on" else False)
     else:
         if env.is_gpu and args.variant:
             ops.set_jacobi_variant(args.variant)
