@@ -434,9 +434,13 @@ extern "C" int gmt_jacobi5xk_pipe(int nsweeps, int n_rect, const int64_t* rects,
     a.wbase = w0;
     a.wend = w1;
     const int64_t nb = (w1 - w0 + wpb - 1) / wpb;
-    if (MODE == 1 && !scaled)  // A/B: GMT_PIPE_SCALED=0 keeps the 0.25 multiply per level
-      jacobi5pipe_kernel<KK, true, MODE, false><<<grid_1d(nb), kBlock, 0, s>>>(a, u, un, ld, nb);
-    else if (skew)
+    if constexpr (MODE == 1) {
+      if (!scaled) {  // A/B: GMT_PIPE_SCALED=0 keeps the 0.25 multiply per level
+        jacobi5pipe_kernel<KK, true, MODE, false><<<grid_1d(nb), kBlock, 0, s>>>(a, u, un, ld, nb);
+        return;
+      }
+    }
+    if (skew)
       jacobi5pipe_kernel<KK, true, MODE><<<grid_1d(nb), kBlock, 0, s>>>(a, u, un, ld, nb);
     else
       jacobi5pipe_kernel<KK, false, MODE><<<grid_1d(nb), kBlock, 0, s>>>(a, u, un, ld, nb);
