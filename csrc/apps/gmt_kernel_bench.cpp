@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <functional>
 #include <string>
+#include <vector>
 
 #include "gmt/buffer.hpp"
 #include "gmt/util.hpp"
@@ -71,6 +72,70 @@ int main(int argc, char** argv) {
     gmt_daxpy_set_variant(0);
     const double ms = time_ms(s, iters, [&] { GMT_CHECK("daxpy", gmt_blas_daxpy(n, 1e-3, x.data(), y.data(), s)); });
     report("rocblas", 0, shape, ms, 24.0 * n);
+  }
+  if (only.find("hot") != std::string::npos) {
+    // --only=hot: just the production (default) configuration of each hot
+    // kernel, `iters` launches each — the target of rocprofv3 --pmc passes
+    // (profiles/r02_pmc).  --hot-k=12,14 sweeps per pipelined pass,
+    // --jacobi-n=32768.
+    const int64_t n = cli.geti("jacobi-n", 32768);
+    const std::string ks = cli.get("hot-k", "12,14");
+    for (int K = 2; K <= 16; K += 2) {
+      if (("," + ks + ",").find("," + std::to_string(K) + ",") == std::string::npos) continue;
+      const int64_t g = K, xk = ((g + 7) / 8) * 8;
+      const int64_t ld2 = ((xk + n + g + 63) / 64) * 64;
+      Buffer<double> a(static_cast<size_t>(ld2) * (n + 2 * g), GMT_SPACE_DEVICE), b(a.size(), GMT_SPACE_DEVICE);
+      GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, a.data(), ld2, s));
+      GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, b.data(), ld2, s));
+      const int64_t rect[4] = {xk, n, g, n};
+      const double ms = time_ms(s, iters, [&] {
+        GMT_CHECK("pipe", gmt_jacobi5xk(K, 1, rect, rect, 0, a.data(), b.data(), ld2, 0, s));
+      });
+      char tag[64];
+      std::snprintf(tag, sizeof(tag), "%lldx%lld x%d default", (long long)n, (long long)n, K);
+      report("jacobi5pipe", K, tag, ms, K * 16.0 * n * n);
+      std::printf("%-10s    %-22s %9.1f MLUPS\n", "", tag, K * double(n) * n / (ms * 1e-3) / 1e6);
+    }
+  }
+  if (only.find("tb") != std::string::npos) {
+    // --only=tb: workgroup-cooperative temporal blocking (jacobi5tb.hip),
+    // --tb-k=12,14,16 --tb-nw=1,2,4,8 --tb-p=3,5 --tb-seg=0 --jacobi-n=32768
+    // --tb-mask=0 (Dirichlet everywhere: rule workgroups at the edges)
+    const int64_t n = cli.geti("jacobi-n", 32768);
+    auto list = [&](const char* key, const char* def) {
+      std::vector<int> v;
+      std::string str = cli.get(key, def);
+      size_t p = 0;
+      while (p < str.size()) {
+        size_t q = str.find(',', p);
+        if (q == std::string::npos) q = str.size();
+        v.push_back(std::atoi(str.substr(p, q - p).c_str()));
+        p = q + 1;
+      }
+      return v;
+    };
+    const int mask = static_cast<int>(cli.geti("tb-mask", 0));
+    for (int K : list("tb-k", "12,14,16")) {
+      const int64_t g = K, xk = ((g + 7) / 8) * 8;
+      const int64_t ld2 = ((xk + n + g + 63) / 64) * 64, rows = n + 2 * g;
+      Buffer<double> a(static_cast<size_t>(ld2) * rows, GMT_SPACE_DEVICE), b(a.size(), GMT_SPACE_DEVICE);
+      GMT_CHECK("fill", gmt_fill_poly(0, ld2, rows, 0.0, 1e-5, 0.0, 1e-5, a.data(), ld2, s));
+      GMT_CHECK("fill", gmt_fill_poly(0, ld2, rows, 0.0, 1e-5, 0.0, 1e-5, b.data(), ld2, s));
+      const int64_t rect[4] = {xk, n, g, n};
+      for (int nw : list("tb-nw", "4"))
+        for (int P : list("tb-p", "3,5"))
+          for (int seg : list("tb-seg", "0")) {
+            gmt_tb_opts o{K, nw, seg, 0, P};
+            const double ms = time_ms(s, iters, [&] {
+              GMT_CHECK("tb", gmt_jacobi5tb(&o, 1, rect, rect, mask, a.data(), b.data(), ld2, rows, s));
+            });
+            char tag[96];
+            std::snprintf(tag, sizeof(tag), "%lldx%lld x%d nw%d P%d seg%d m%d", (long long)n, (long long)n, K, nw,
+                          P, seg, mask);
+            report("jacobi5tb", K, tag, ms, K * 16.0 * n * n);
+            std::printf("%-10s    %-30s %9.1f MLUPS\n", "", tag, K * double(n) * n / (ms * 1e-3) / 1e6);
+          }
+    }
   }
   if (only.find("jacobi") != std::string::npos) {
     const int64_t n = cli.geti("jacobi-n", 32768);

@@ -125,6 +125,25 @@ int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int halo
  * pass), so rects narrower than a 128 - 2K column strip still take the
  * branch-free path. */
 #define GMT_XK_EXT 0x20000000
+
+/* ---- Temporal-blocking Jacobi (csrc/kernels/jacobi5tb.hip): `sweeps` fused
+ *      Laplace sweeps per memory pass on up to 8 output rects {x0, nx, y0, ny}
+ *      (absolute, x0 even, x0 >= sweeps, y0 >= sweeps, y0+ny+sweeps <= nrows).
+ *      Workgroups of `wg_waves` waves (128 columns each) share their edge
+ *      columns through LDS.  Cells of the interior `dom` outside the rects
+ *      are never written.  halo_mask as for gmt_jacobi5x2. */
+#define GMT_TB_MAX_SWEEPS 16
+typedef struct gmt_tb_opts {
+  int sweeps;   /* K: even, 2..GMT_TB_MAX_SWEEPS */
+  int wg_waves; /* waves per workgroup, 1..8 (0 = auto: 4, or 1 for rects <= one strip) */
+  int seg_rows; /* output rows per workgroup (0 = auto from the device occupancy) */
+  int exact;    /* 1: multiply by 1/4 per level (bitwise for any magnitude);
+                   0: power-of-two scaled levels (bitwise unless a value is
+                   subnormal or |u| * 4^K overflows) */
+  int prefetch; /* input rows in flight per wave: 3 or 6 (0 = 3) */
+} gmt_tb_opts;
+int gmt_jacobi5tb(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, const int64_t* dom,
+                  int halo_mask, const double* u, double* un, int64_t ld, int64_t nrows, void* stream);
 int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
                   const double* u, double* un, int64_t ld, int tile, void* stream);
 /* Register-pipelined K-sweep kernel: one wave per 128-column strip and

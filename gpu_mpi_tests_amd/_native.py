@@ -42,6 +42,17 @@ class Copy2dDesc(ctypes.Structure):
 
 MAX_COPY2D = 8
 
+
+class TbOpts(ctypes.Structure):
+    """gmt_tb_opts (csrc/include/gmt/kernels.h)."""
+    _fields_ = [
+        ("sweeps", c_int),
+        ("wg_waves", c_int),
+        ("seg_rows", c_int),
+        ("exact", c_int),
+        ("prefetch", c_int),
+    ]
+
 _SIGS = {
     "gmt_daxpy": (c_int, [c_i64, c_dbl, c_vp, c_vp, c_vp]),
     "gmt_stencil5_1d": (c_int, [c_i64, c_vp, c_dbl, c_vp, c_vp, c_vp]),
@@ -63,6 +74,7 @@ _SIGS = {
     ),
     "gmt_jacobi5x2": (c_int, [c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
     "gmt_jacobi5xk": (c_int, [c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
+    "gmt_jacobi5tb": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_vp]),
     "gmt_jacobi5_set_variant": (None, [c_int]),
     "gmt_daxpy_set_variant": (None, [c_int]),
     "gmt_stencil5_set_variant": (None, [c_int]),

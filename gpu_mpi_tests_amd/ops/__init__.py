@@ -15,6 +15,7 @@ from .kernels import (  # noqa: F401
     jacobi5_rects,
     jacobi5x2,
     jacobi5xk,
+    jacobi5tb,
     XK_EXT,
     XK_PIPE,
     set_jacobi_variant,

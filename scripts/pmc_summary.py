@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""Per-kernel table from a scripts/gpu_r02_pmc.sh output directory.
+
+Joins the kernel trace (duration, VGPR/SGPR/scratch per dispatch) with every
+--pmc pass (counter means per dispatch, grouped by kernel name) and derives:
+
+* HBM bytes: FETCH_SIZE x 2 (gfx950 tallies 16-B/lane streaming reads at half
+  their bytes, MI355X_MICROARCH.md "HBM") and WRITE_SIZE as is; both in KB.
+* VALU / fp64 instruction counts per wave and, with --updates NAME=N, per
+  lattice update (N = lattice updates per dispatch of kernel NAME).
+* SQ time split: WAIT_ANY (parked on s_waitcnt / barrier), WAIT_INST_ANY
+  (issue-stalled), ACTIVE_INST_ANY; VALU-active share of wave cycles.
+* Effective clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel time.
+
+Usage: scripts/pmc_summary.py DIR [--match SUBSTR] [--updates SUBSTR=N ...] [--md]
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import os
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    name = name.split("(")[0] if "(" in name and "<" not in name.split("(")[0][-1:] else name
+    return name.replace("gmt::", "")[:70]
+
+
+def load_trace(d):
+    out = defaultdict(lambda: {"n": 0, "ns": 0.0, "vgpr": 0, "agpr": 0, "sgpr": 0, "scratch": 0, "lds": 0})
+    for f in glob.glob(os.path.join(d, "trace", "*kernel_trace.csv")):
+        for r in csv.DictReader(open(f)):
+            k = out[r["Kernel_Name"]]
+            k["n"] += 1
+            k["ns"] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            k["vgpr"] = int(r["VGPR_Count"])
+            k["agpr"] = int(r.get("Accum_VGPR_Count", 0) or 0)
+            k["sgpr"] = int(r["SGPR_Count"])
+            k["scratch"] = int(r["Scratch_Size"])
+            k["lds"] = int(r["LDS_Block_Size"])
+    return out
+
+
+def load_pmc(d):
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(d, "pmc*", "*counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--match", default="")
+    ap.add_argument("--updates", action="append", default=[],
+                    help="SUBSTR=N: lattice updates (or elements) per dispatch of kernels matching SUBSTR")
+    ap.add_argument("--md", action="store_true", help="markdown table")
+    a = ap.parse_args()
+    tr = load_trace(a.dir)
+    pm = load_pmc(a.dir)
+    ups = [(s.split("=")[0], float(s.split("=")[1])) for s in a.updates]
+    rows = []
+    for name, t in sorted(tr.items(), key=lambda kv: -kv[1]["ns"]):
+        if a.match and a.match not in name:
+            continue
+        c = pm.get(name, {})
+        us = t["ns"] / t["n"] / 1e3
+        g = lambda k: c.get(k, float("nan"))  # noqa: E731
+        waves = g("SQ_WAVES")
+        wc = g("SQ_WAVE_CYCLES")
+        upd = next((n for s, n in ups if s in name), None)
+        row = {
+            "kernel": short(name), "calls": t["n"], "us": us,
+            "vgpr": t["vgpr"], "agpr": t["agpr"], "sgpr": t["sgpr"], "scratch": t["scratch"], "lds": t["lds"],
+            "rd_GB": 2 * g("FETCH_SIZE") * 1024 / 1e9, "wr_GB": g("WRITE_SIZE") * 1024 / 1e9,
+            "valu_per_wave": g("SQ_INSTS_VALU") / waves,
+            "f64_add": g("SQ_INSTS_VALU_ADD_F64"), "f64_mul": g("SQ_INSTS_VALU_MUL_F64"),
+            "f64_fma": g("SQ_INSTS_VALU_FMA_F64"), "valu": g("SQ_INSTS_VALU"),
+            "vmem_rd": g("SQ_INSTS_VMEM_RD"), "vmem_wr": g("SQ_INSTS_VMEM_WR"), "salu": g("SQ_INSTS_SALU"),
+            "wait_any": g("SQ_WAIT_ANY") / wc, "wait_inst": g("SQ_WAIT_INST_ANY") / wc,
+            "active": g("SQ_ACTIVE_INST_ANY") / wc, "valu_active": g("SQ_ACTIVE_INST_VALU") / wc,
+            "clk_GHz": g("GRBM_GUI_ACTIVE") / 8 / (us * 1e-6) / 1e9,
+            "l2_hit": g("TCC_HIT_sum") / (g("TCC_HIT_sum") + g("TCC_MISS_sum")),
+            "waves": waves,
+        }
+        row["rd_TBps"] = row["rd_GB"] / (us * 1e-6) / 1e3
+        row["wr_TBps"] = row["wr_GB"] / (us * 1e-6) / 1e3
+        if upd:
+            row["valu_per_upd"] = row["valu"] / upd
+            row["dadd_per_upd"] = row["f64_add"] / upd
+            row["B_per_upd"] = (row["rd_GB"] + row["wr_GB"]) * 1e9 / upd
+            row["Gupd_s"] = upd / (us * 1e-6) / 1e9
+        rows.append(row)
+    if a.md:
+        cols = ["kernel", "calls", "us", "vgpr", "scratch", "rd_TBps", "wr_TBps", "valu_per_wave", "wait_any",
+                "wait_inst", "valu_active", "clk_GHz", "l2_hit"]
+        if ups:
+            cols += ["valu_per_upd", "dadd_per_upd", "B_per_upd", "Gupd_s"]
+        print("| " + " | ".join(cols) + " |")
+        print("|" + "---|" * len(cols))
+        for r in rows:
+            print("| " + " | ".join(f"{r.get(k):.3g}" if isinstance(r.get(k), float) else f"`{r.get(k)}`"
+                                    if k == "kernel" else str(r.get(k)) for k in cols) + " |")
+    else:
+        for r in rows:
+            print(r["kernel"])
+            print("   " + "  ".join(f"{k}={v:.4g}" if isinstance(v, float) else f"{k}={v}"
+                                    for k, v in r.items() if k != "kernel"))
+
+
+if __name__ == "__main__":
+    main()
