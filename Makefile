@@ -33,7 +33,7 @@ HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-funct
 ROCM_HOST := -O2 -std=c++17 -fPIC -Wall -Icsrc/include -I$(ROCM)/include -D__HIP_PLATFORM_AMD__=1
 # SAN: host-side sanitizer flags (make asan-host); never applied to GPU code
 SAN       ?=
-HOSTFLAGS := -O3 -std=c++17 -fPIC -Wall -Icsrc/include $(SAN)
+HOSTFLAGS := -O3 -std=c++17 -fPIC -Wall -ffp-contract=off -Icsrc/include $(SAN)
 APPFLAGS  := -O2 -std=c++17 -Wall -Icsrc/include -Icsrc/apps -I$(MPI_HOME)/include $(SAN)
 ENGFLAGS  := -O2 -std=c++17 -Wall -fPIC -Icsrc/include $(SAN)
 MPI_LIBS  := $(MPI_HOME)/lib/libmpi.so -Wl,-rpath,$(MPI_HOME)/lib -static-libstdc++ -static-libgcc -Wl,--allow-shlib-undefined

@@ -6,27 +6,39 @@ halo-exchange latency".  The headline ``value`` is the whole-job stencil rate
 in MLUPS (million lattice-point updates per second, summed over all GPUs) on
 the BASELINE multi-GPU config "mpi_stencil2d 32768² ... (2×4 decomp), halo
 exchange/interior overlap".  The global domain is FIXED at 32768² for every N
-(strong scaling: N = 8 is exactly the named config).  The same JSON line also
-carries the single-GPU-per-rank DAXPY bandwidth (BASELINE config "daxpy
-N=2^28 fp64 on one MI355X") and the measured halo-exchange latency.
+(strong scaling: N = 8 is exactly the named config).  The same JSON line
+carries every other BASELINE quantity:
+
+* ``stencil_8192_MLUPS``: the same engine on the 8192² domain (BASELINE
+  "mpi_stencil2d 8192² fp64 single GPU" at N = 1);
+* ``daxpy_GBps``: DAXPY N = 2^28 fp64 per GPU (BASELINE "daxpy N=2^28");
+* ``halo_exchange_us``: one blocking K-wide halo exchange of the 32768² field
+  (N > 1: the job's own exchange over RCCL/xGMI; N = 1: a 1-rank periodic
+  RCCL self-exchange of the same faces, labelled in ``halo_exchange_kind``);
+* N > 1: the reference's own halo benchmark (``ref_halo_*``, test_deriv /
+  test_sum of mpi_stencil2d_gt) over RCCL.
 
 One step = one full Jacobi sweep of the global domain (every point updated
-once).  The native engine (C++, ``csrc/engine/jacobi.cpp``)
-runs the steps in fused passes of up to 14 sweeps by default (temporal
-blocking, ``--tblock on --tsteps 14``): one 14-wide halo exchange (RCCL over
-xGMI on a high-priority stream, overlapped with the interior update) and one
-pass of the register-pipelined kernel (``csrc/kernels/jacobi5pipe.hip``) that
-reads u(t) once and writes u(t+14) once — bitwise the same result as fourteen
-single sweeps, 1/14 of the HBM bytes.  The engine splits K steps into the
-cheapest sequence of passes (``JacobiSolver::plan_passes``): 100 steps = 6
-14-sweep passes + 2 8-sweep passes.  ``--tblock off`` runs one exchange + one
-sweep per step; ``--engine torch`` runs the single-sweep algorithm through
-torch.distributed P2P from Python.  Nothing is skipped inside the timed
-region: K steps are K sweeps of every lattice point (an odd K ends with one single sweep).
+once).  The native engine (C++, ``csrc/engine/jacobi.cpp``) runs the steps in
+fused passes of up to ``--tsteps`` sweeps (temporal blocking with
+``csrc/kernels/jacobi5tb.hip``): one K-wide halo exchange (RCCL over xGMI on a
+high-priority stream, overlapped with the core of the pass) and one pass that
+reads u(t) once and writes u(t+K) once — bitwise the same result as K single
+sweeps.  ``JacobiSolver::plan_passes`` splits the timed steps into the
+cheapest sequence of passes; the JSON reports that plan (``pass_plan``), and
+every pass type of it is launched once before the warm-up
+(``NativeJacobi.prepare``), so no first launch lands in the timed region.
+Nothing is skipped inside the timed region: K steps are K sweeps of every
+lattice point.
+
+Before timing, every run checks its decomposition: the engine with the same
+process grid and K runs a small domain and is compared with the serial NumPy
+reference (``check_max_diff``, must be 0 — the engine is bitwise); a
+mismatch exits non-zero.
 
 Launch (driver contract):
     python bench.py --gpus 1 --steps K --warmup W
-    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
 """
 from __future__ import annotations
@@ -37,22 +49,17 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-DEFAULT_TSTEPS = 14  # fused sweeps per memory pass / halo exchange (native engine; profiles/r01_k14.md)
+DEFAULT_TSTEPS = 14  # fused sweeps per memory pass / halo exchange (profiles/r02_tb.md)
 
 from gpu_mpi_tests_amd import ops  # noqa: E402
+from gpu_mpi_tests_amd.engine import MAX_TSTEPS  # noqa: E402
 from gpu_mpi_tests_amd.parallel import dist as gdist  # noqa: E402
 from gpu_mpi_tests_amd.parallel.decomp import choose_dims  # noqa: E402
-
-
-def default_tsteps(shape, world):
-    """14 sweeps per pass, 12 for per-GPU domains below 2^27 points (8192² on
-    one GPU): there the 14-deep pipeline's warm-up and ghost-rule bands cost
-    more than its fewer passes save (profiles/r01_8192.md)."""
-    return DEFAULT_TSTEPS if shape[0] * shape[1] // max(1, world) >= (1 << 27) else 12
 
 
 def _sync(env):
@@ -74,48 +81,111 @@ def _timed(env, fn_run, fn_sync, steps, warmup):
     return gdist.allreduce_max(dt, env)
 
 
-def bench_native(env, shape, steps, warmup, overlap, dims, graph, variant, tblock):
+def plan_str(plan):
+    """[14, 14, 12] -> '2x14+1x12' (sweeps per fused pass, launch order grouped)."""
+    out, i = [], 0
+    while i < len(plan):
+        j = i
+        while j < len(plan) and plan[j] == plan[i]:
+            j += 1
+        out.append(f"{j - i}x{plan[i]}")
+        i = j
+    return "+".join(out)
+
+
+def bench_native(env, shape, steps, warmup, overlap, dims, graph, tblock, wg_waves, seg_rows):
     from gpu_mpi_tests_amd.engine import NativeJacobi
 
-    eng = NativeJacobi(shape[0], shape[1], env, dims=dims, overlap=overlap, graph=graph, variant=variant,
-                       tblock=tblock)
+    eng = NativeJacobi(shape[0], shape[1], env, dims=dims, overlap=overlap, graph=graph, tblock=tblock,
+                       wg_waves=wg_waves, seg_rows=seg_rows)
+    eng.prepare(steps)  # one launch of every pass type of the timed plan, initial field restored
     dt = _timed(env, eng.run, eng.synchronize, steps, warmup)
     info = {"engine": "native", "graph": eng.graph, "overlap": eng.overlap, "tblock": eng.tblock,
-            "overlap_tuning": eng.tuned,
-            "tsteps": eng.tsteps,
+            "overlap_tuning": eng.tuned, "tsteps": eng.tsteps, "pass_plan": plan_str(eng.plan(steps)),
+            "exact": eng.exact,
             "transport": eng.transport if env.world_size > 1 else "none",
             "halo_bytes_per_rank": eng.halo_bytes, "dims": (eng.py, eng.px)}
     return eng, dt, info
 
 
-def bench_torch(env, shape, steps, warmup, overlap, dims):
-    from gpu_mpi_tests_amd.models.jacobi import Jacobi2D
+def check_engine(env, dims, tsteps, graph):
+    """Distributed-correctness gate (reference: mpi_stencil2d_gt.cc:555-570
+    err_norm): the engine with this job's process grid and sweeps per pass on
+    a small Dirichlet domain, overlap on and off, vs the serial NumPy
+    reference.  Returns the max |difference| over both runs (0 = bitwise)."""
+    from gpu_mpi_tests_amd.engine import NativeJacobi, serial_jacobi
 
-    solver = Jacobi2D(shape[0], shape[1], env=env, dims=dims, overlap=overlap)
-    dt = _timed(env, solver.run, lambda: _sync(env), steps, warmup)
-    ex = solver.ex[id(solver.u)]
-    info = {"engine": "torch", "graph": False, "overlap": overlap, "tblock": False,
-            "transport": env.backend if env.world_size > 1 else "none",
-            "halo_bytes_per_rank": ex.bytes_per_exchange() if ex.active else 0,
-            "dims": (solver.decomp.py, solver.decomp.px)}
-    return solver, dt, info
+    py, px = dims
+    k = max(1, tsteps)
+    # every rank at least 4K+8 cells each way: the overlapped core/frame split runs
+    ny, nx = py * (4 * k + 11) + 3, px * (8 * k + 37) + 5
+    steps = 2 * k + 3  # full passes, a remainder pass and (odd) single sweeps
+    ref = serial_jacobi(ny, nx, steps) if env.rank == 0 else None
+    worst = 0.0
+    for ov in (True, False):
+        e = NativeJacobi(ny, nx, env, dims=dims, overlap=ov, graph=graph, tblock=k if k > 1 else False)
+        e.run(steps)
+        e.synchronize()
+        part = (e.off_y, e.off_x, e.interior())
+        e.close()
+        if env.world_size > 1:
+            parts = [None] * env.world_size
+            torch.distributed.all_gather_object(parts, part, group=env.host_group)
+        else:
+            parts = [part]
+        if env.rank == 0:
+            full = np.full((ny, nx), np.nan)
+            for oy, ox, a in parts:
+                full[oy:oy + a.shape[0], ox:ox + a.shape[1]] = a
+            worst = max(worst, float(np.nanmax(np.abs(full - ref))) if not np.isnan(full).any() else float("inf"))
+    return gdist.allreduce_max(worst, env)
 
 
-def halo_latency(env, solver, iters):
-    """Blocking halo exchange of the current field: mean seconds (max over ranks)."""
-    if env.world_size == 1:
-        return None
-    exch = solver.exchange if hasattr(solver, "exchange") else solver.ex[id(solver.u)].exchange
+def peer_status(env, dims):
+    """Which process-grid neighbours' GPUs this rank's GPU can reach directly
+    (xGMI peer access), gathered on rank 0: {"peer_access": bool, "rccl": version}."""
+    if not env.is_gpu or env.world_size == 1:
+        return {}
+    py, px = dims
+    cy, cx = divmod(env.rank, px)
+    nbrs = [(cy + dy) * px + (cx + dx) for dy, dx in ((-1, 0), (1, 0), (0, -1), (0, 1))
+            if 0 <= cy + dy < py and 0 <= cx + dx < px]
+    ok = True
+    for r in nbrs:
+        dev = r % max(1, env.n_devices)  # one rank per GPU: rank r runs on device r (single node)
+        if dev != env.device.index:
+            ok = ok and bool(torch.cuda.can_device_access_peer(env.device.index, dev))
+    flags = [None] * env.world_size
+    torch.distributed.all_gather_object(flags, ok, group=env.host_group)
+    ver = torch.cuda.nccl.version() if hasattr(torch.cuda, "nccl") else None
+    return {"peer_access": all(flags), "rccl_version": ".".join(map(str, ver)) if isinstance(ver, tuple) else ver}
+
+
+def halo_latency(env, eng, iters):
+    """Blocking halo exchange of the engine's current field: mean seconds (max over ranks)."""
     for _ in range(5):
-        exch()
+        eng.exchange()
     _sync(env)
     gdist.barrier(env)
     t0 = time.perf_counter()
     for _ in range(iters):
-        exch()
+        eng.exchange()
     _sync(env)
     dt = (time.perf_counter() - t0) / iters
     return gdist.allreduce_max(dt, env)
+
+
+def self_halo_latency(env, shape, tsteps, iters):
+    """N = 1: the same K-wide faces of the same field exchanged by a 1-rank
+    periodic engine with itself over RCCL (send/recv to self)."""
+    from gpu_mpi_tests_amd.engine import NativeJacobi
+
+    eng = NativeJacobi(shape[0], shape[1], env, periodic=True, overlap=False, graph=False,
+                       tblock=tsteps if tsteps > 1 else False, transport="rccl")
+    try:
+        return halo_latency(env, eng, iters), eng.halo_bytes, eng.transport
+    finally:
+        eng.close()
 
 
 def ref_halo(env, n_local, n_other, iters):
@@ -173,30 +243,32 @@ def main(argv=None):
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
                     help="strong (default): the global domain is size x size for every N (the BASELINE "
                          "config); weak: size x size PER GPU, global (py*size) x (px*size)"),
-    ap.add_argument("--engine", choices=("native", "torch"), default="native")
     ap.add_argument("--overlap", choices=("auto", "on", "off"), default="auto",
-                    help="halo exchange overlapped with the interior pass (native engine): auto = "
-                         "time both once at start-up on the real links, every rank keeps the faster")
+                    help="halo exchange overlapped with the interior pass: auto = time both once at "
+                         "start-up on the real links, every rank keeps the faster")
     ap.add_argument("--no-overlap", action="store_true", help="same as --overlap off")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
-                    help="hipGraph replay of the fused passes (auto = off: a 12-sweep pass is "
-                         ">0.5 ms of GPU work, its 2-3 launches hide, and replaying the captured "
-                         "graph measured 2-6%% slower than eager launches at every domain size, "
-                         "profiles/r01_frame.md)")
+                    help="hipGraph replay of the fused passes (auto = off: a fused pass is >0.5 ms of "
+                         "GPU work, its launches hide behind it, profiles/r01_frame.md)")
     ap.add_argument("--tblock", choices=("on", "off"), default="on",
-                    help="temporal blocking (native engine): --tsteps sweeps per memory pass and "
-                         "per halo exchange; bitwise the same result as single sweeps")
-    ap.add_argument("--tsteps", type=int, default=0,
-                    help="sweeps per fused pass with --tblock on (2-14; 0 = default %d)" % DEFAULT_TSTEPS)
+                    help="temporal blocking: --tsteps sweeps per memory pass and per halo exchange; "
+                         "bitwise the same result as single sweeps")
+    ap.add_argument("--tsteps", type=int, default=0, choices=range(0, MAX_TSTEPS + 1), metavar=f"0-{MAX_TSTEPS}",
+                    help=f"sweeps per fused pass with --tblock on (2-{MAX_TSTEPS}; 0 = default {DEFAULT_TSTEPS})")
+    ap.add_argument("--wg-waves", type=int, default=0, choices=range(0, 9), metavar="0-8",
+                    help="temporal-blocking kernel: 128-column waves per workgroup (0 = auto)")
+    ap.add_argument("--seg-rows", type=int, default=0, help="temporal-blocking kernel: rows per workgroup (0 = auto)")
     ap.add_argument("--dims", type=str, default=None, help="process grid PYxPX, e.g. 4x2")
     ap.add_argument("--daxpy-n", type=int, default=1 << 28)
+    ap.add_argument("--small-size", type=int, default=8192,
+                    help="second stencil domain (BASELINE single-GPU config 8192^2; 0 = skip)")
     ap.add_argument("--skip-extras", action="store_true", help="headline stencil only")
+    ap.add_argument("--skip-check", action="store_true", help="skip the small-domain correctness gate")
     ap.add_argument("--ref-n-local", type=int, default=1024,
                     help="reference halo benchmark (N>1): n_local_deriv (mpi_stencil2d_gt default 1024)")
     ap.add_argument("--ref-n-other", type=int, default=512 * 1024,
                     help="reference halo benchmark: extent of the other axis (default 512Ki: 8 MiB faces)")
     ap.add_argument("--ref-iters", type=int, default=100, help="reference halo benchmark: timed exchanges")
-    ap.add_argument("--variant", type=int, default=0, help="jacobi kernel variant (0 auto,1 reg,2 lds,3 scalar)")
     ap.add_argument("--device", type=str, default=None, help="cuda|cpu (default: cuda if available)")
     args = ap.parse_args(argv)
 
@@ -212,31 +284,50 @@ def main(argv=None):
         shape = (args.size * gdims[0], args.size * gdims[1])
     else:
         shape = (args.size, args.size)
-    engine = args.engine
     graph = args.graph == "on"
-    if engine == "native":
-        solver, dt, info = bench_native(env, shape, args.steps, args.warmup, overlap, dims,
-                                        graph, args.variant,
-                                        (args.tsteps or default_tsteps(shape, env.world_size))
-                                        if args.tblock == "on" else False)
-    else:
-        if env.is_gpu and args.variant:
-            ops.set_jacobi_variant(args.variant)
-        solver, dt, info = bench_torch(env, shape, args.steps, args.warmup, overlap_mode != "off", dims)
+    tsteps = (args.tsteps or DEFAULT_TSTEPS) if args.tblock == "on" else 1
+    extras = {}
+    if not args.skip_check:
+        diff = check_engine(env, dims or gdims, tsteps, graph)
+        extras["check_max_diff"] = diff
+        extras.update(peer_status(env, dims or gdims))
+        if diff != 0.0:
+            if env.rank == 0:
+                print(f"bench.py: distributed result differs from the serial reference by {diff}",
+                      file=sys.stderr)
+            gdist.shutdown()
+            sys.exit(3)
+    solver, dt, info = bench_native(env, shape, args.steps, args.warmup, overlap, dims, graph,
+                                    tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows)
     points = shape[0] * shape[1]
     mlups = points * args.steps / dt / 1e6
     ms_per_step = dt / args.steps * 1e3
-    extras = {}
     if not args.skip_extras:
-        hl = halo_latency(env, solver, iters=max(20, min(args.steps, 200)))
-        extras["halo_exchange_us"] = None if hl is None else round(hl * 1e6, 2)
-        resid = solver.residual() if hasattr(solver, "residual") else solver.global_residual()
-        extras["residual_l2"] = resid
-        if hasattr(solver, "close"):
-            solver.close()
+        iters = max(20, min(args.steps, 200))
+        if env.world_size > 1:
+            extras["halo_exchange_us"] = round(halo_latency(env, solver, iters) * 1e6, 2)
+            extras["halo_exchange_kind"] = (f"{info['transport']}, {info['tsteps']}-wide faces + corners "
+                                            f"of the {shape[0]}x{shape[1]} field, process grid "
+                                            f"{info['dims'][0]}x{info['dims'][1]}")
+        extras["residual_l2"] = solver.residual()
+        solver.close()
         del solver
         if env.is_gpu:
             torch.cuda.empty_cache()
+        if env.world_size == 1:
+            t, nbytes, kind = self_halo_latency(env, shape, tsteps, iters)
+            extras["halo_exchange_us"] = round(t * 1e6, 2)
+            extras["halo_exchange_kind"] = (f"1-rank periodic {kind} self-exchange, {tsteps}-wide faces + "
+                                            f"corners of the {shape[0]}x{shape[1]} field ({nbytes} bytes)")
+        if args.small_size:
+            s2 = (args.small_size, args.small_size)
+            steps2 = max(100, 4 * args.steps)
+            eng2, dt2, info2 = bench_native(env, s2, steps2, max(args.warmup, 10), overlap, dims, graph,
+                                            tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows)
+            eng2.close()
+            extras[f"stencil_{args.small_size}_MLUPS"] = round(s2[0] * s2[1] * steps2 / dt2 / 1e6, 1)
+            extras[f"stencil_{args.small_size}_ms_per_step"] = round(dt2 / steps2 * 1e3, 5)
+            extras[f"stencil_{args.small_size}_pass_plan"] = f"{steps2} steps: {info2['pass_plan']}"
         if env.world_size > 1:
             extras.update(ref_halo(env, args.ref_n_local, args.ref_n_other, args.ref_iters))
         gbps, ddt = bench_daxpy(env, args.daxpy_n, iters=20)
@@ -244,6 +335,8 @@ def main(argv=None):
         extras["daxpy_GBps_per_gpu"] = round(gbps / env.world_size, 1)
         extras["daxpy_n"] = args.daxpy_n
         extras["daxpy_ms"] = round(ddt * 1e3, 4)
+    else:
+        solver.close()
     py, px = info["dims"] if info.get("dims") else gdims
     if env.rank == 0:
         rec = {
@@ -270,6 +363,8 @@ def main(argv=None):
                 "overlap_tuning": info.get("overlap_tuning"),
                 "temporal_blocking": info["tblock"],
                 "sweeps_per_pass": info.get("tsteps", 1),
+                "pass_plan": info.get("pass_plan"),
+                "exact_levels": info.get("exact"),
                 "transport": info["transport"],
                 "halo_bytes_per_rank": info["halo_bytes_per_rank"],
                 "device": str(env.device),

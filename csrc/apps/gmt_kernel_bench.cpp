@@ -98,8 +98,8 @@ int main(int argc, char** argv) {
     }
   }
   if (only.find("tb") != std::string::npos) {
-    // --only=tb: workgroup-cooperative temporal blocking (jacobi5tb.hip),
-    // --tb-k=12,14,16 --tb-nw=1,2,4,8 --tb-p=3,5 --tb-seg=0 --jacobi-n=32768
+    // --only=tb: temporal-blocking kernel (jacobi5tb.hip),
+    // --tb-k=12,14,16 --tb-nw=1,2,4,8 --tb-seg=0 --jacobi-n=32768
     // --tb-mask=0 (Dirichlet everywhere: rule workgroups at the edges)
     const int64_t n = cli.geti("jacobi-n", 32768);
     auto list = [&](const char* key, const char* def) {
@@ -123,9 +123,9 @@ int main(int argc, char** argv) {
       GMT_CHECK("fill", gmt_fill_poly(0, ld2, rows, 0.0, 1e-5, 0.0, 1e-5, b.data(), ld2, s));
       const int64_t rect[4] = {xk, n, g, n};
       for (int nw : list("tb-nw", "4"))
-        for (int P : list("tb-p", "3,5"))
+        for (int P : list("tb-p", "3"))
           for (int seg : list("tb-seg", "0")) {
-            gmt_tb_opts o{K, nw, seg, 0, P};
+            gmt_tb_opts o{K, nw, seg, 0};
             const double ms = time_ms(s, iters, [&] {
               GMT_CHECK("tb", gmt_jacobi5tb(&o, 1, rect, rect, mask, a.data(), b.data(), ld2, rows, s));
             });

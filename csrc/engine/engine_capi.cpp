@@ -1,9 +1,11 @@
 // C ABI of the native Jacobi engine (gmt/engine.h) for the Python package.
 #include <cstring>
 #include <memory>
+#include <vector>
 
 #include "gmt/engine.h"
 #include "gmt/jacobi.hpp"
+#include "gmt/kernels.h"
 
 namespace {
 struct Handle {
@@ -24,7 +26,12 @@ int gmt_engine_unique_id(void* out128) {
 }
 
 void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank, int world,
-                               int transport, const void* ccl_id, int flags, int variant) {
+                               int transport, const void* ccl_id, const gmt_engine_opts* opts) {
+  gmt_engine_opts o{};
+  if (opts) o = *opts;
+  if (o.tsteps < 0 || o.tsteps > GMT_TB_MAX_SWEEPS || o.overlap < 0 || o.overlap > 2 || o.wg_waves < 0 ||
+      o.wg_waves > 8 || o.seg_rows < 0 || o.exact < -1 || o.exact > 1)
+    return nullptr;
   auto* h = new Handle();
   if (transport == GMT_ENGINE_RCCL) {
     gmt_ccl_id id;
@@ -42,13 +49,16 @@ void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank,
   c.nx_global = nx;
   c.py = py;
   c.px = px;
-  c.periodic = flags & 1;
-  c.overlap = (flags & 2) != 0;
-  c.overlap_auto = (flags & 16) != 0;  // bit4: time both modes, keep the faster
-  c.graph = (flags & 4) != 0;
-  c.tblock = (flags & 8) != 0;
-  c.tsteps = (flags >> 8) & 0xf;  // bits 8-11: sweeps per fused pass (0 = from bit 3)
-  c.variant = variant;
+  c.periodic = o.periodic != 0;
+  c.overlap = o.overlap != 0;
+  c.overlap_auto = o.overlap == 2;  // time both modes, keep the faster
+  c.graph = o.graph != 0;
+  c.tblock = o.tsteps > 1;
+  c.tsteps = o.tsteps;
+  c.variant = o.variant;
+  c.wg_waves = o.wg_waves;
+  c.seg_rows = o.seg_rows;
+  c.exact = o.exact;
   h->py = py;
   h->px = px;
   h->s = std::make_unique<gmt::JacobiSolver>(*h->t, c);
@@ -92,6 +102,16 @@ int gmt_engine_jacobi_info(void* p, int64_t* out) {
   out[10] = s.tsteps();
   out[11] = static_cast<int64_t>(s.tuned_overlap_s() * 1e9);  // overlap_auto timings, ns per pass
   out[12] = static_cast<int64_t>(s.tuned_serial_s() * 1e9);
+  out[13] = s.exact();
+  return 0;
+}
+int gmt_engine_jacobi_plan(void* p, int steps, int* out, int max) {
+  const std::vector<int> plan = static_cast<Handle*>(p)->s->plan_passes(steps);
+  for (int i = 0; i < static_cast<int>(plan.size()) && i < max; ++i) out[i] = plan[i];
+  return static_cast<int>(plan.size());
+}
+int gmt_engine_jacobi_prepare(void* p, int steps) {
+  static_cast<Handle*>(p)->s->prepare(steps);
   return 0;
 }
 int gmt_engine_jacobi_copy_interior(void* p, double* host) {

@@ -1,5 +1,6 @@
 // Native distributed Jacobi engine (gmt/jacobi.hpp).
 #include "gmt/jacobi.hpp"
+#include "gmt/kernels.h"
 #include "gmt/util.hpp"
 
 #include <algorithm>
@@ -72,8 +73,15 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   }
 
   ks_ = c.tsteps > 1 ? c.tsteps : (c.tblock ? 2 : 1);
-  if (ks_ > 14) ks_ = 14;
-  if (ks_ > 4 && ks_ % 2) --ks_;  // 5..14 sweeps: register-pipelined kernel, even counts only
+  if (ks_ > GMT_TB_MAX_SWEEPS) ks_ = GMT_TB_MAX_SWEEPS;
+  if (ks_ > 4 && ks_ % 2) --ks_;  // 5..16 sweeps: gmt_jacobi5tb, even counts only
+  // Scaled levels (4^p u_p) are bitwise equal to the exact form while
+  // max|u| * 4^K stays finite (and no level value is subnormal).  The initial
+  // field x^3 + y^2 on [-gh, 1 + gh]^2 is bounded by 2 + 3gh, and every
+  // Jacobi sweep averages, so that bound holds for every later field.
+  const double hb = 1.0 / (static_cast<double>(c.ny_global > c.nx_global ? c.ny_global : c.nx_global) + 1);
+  const double umax = 2.0 + 3.0 * ks_ * hb;
+  exact_ = c.exact == 1 || !(umax * std::ldexp(1.0, 2 * ks_) < 1e300);
   g_ = ks_;
   yo_ = g_;
   xo_ = round_up(g_, 8);  // ghost columns fit left of the interior; 64-B aligned interior
@@ -108,8 +116,8 @@ void JacobiSolver::init_field() {
   const double h = 1.0 / (static_cast<double>(c.ny_global > c.nx_global ? c.ny_global : c.nx_global) + 1);
   for (int b = 0; b < 2; ++b) {
     GMT_CHECK("memset", gmt_rt_memset_async(buf_[b].data(), 0, buf_[b].bytes(), s_));
-    GMT_CHECK("fill", gmt_fill_poly(0, nx_ + 2 * g_, ny_ + 2 * g_, (ox_ - g_) * h, h,
-                                    (oy_ - g_) * h, h, buf_[b].data() + (xo_ - g_), ld_, s_));
+    GMT_CHECK("fill", gmt_fill_poly(4, nx_ + 2 * g_, ny_ + 2 * g_, static_cast<double>(ox_ - g_), h,
+                                    static_cast<double>(oy_ - g_), h, buf_[b].data() + (xo_ - g_), ld_, s_));
   }
   GMT_CHECK("init sync", gmt_rt_stream_synchronize(s_));
   parity_ = 0;
@@ -201,32 +209,42 @@ int JacobiSolver::halo_mask() const {
          (nb_.north >= 0 ? 8 : 0);
 }
 
+void JacobiSolver::xk_launch(int K, int n, const int64_t* rects, int parity, bool frame) {
+  const double* u = buf_[parity].data();
+  double* un = buf_[parity ^ 1].data();
+  const int64_t dom[4] = {xo_, nx_, yo_, ny_};
+  const int mask = halo_mask();
+  if (K % 2 == 0) {
+    // the frame bands are at most K wide or K tall: one-wave workgroups
+    gmt_tb_opts o{K, frame ? 1 : cfg_.wg_waves, cfg_.seg_rows, exact_ ? 1 : 0};
+    GMT_CHECK("jacobi tb", gmt_jacobi5tb(&o, n, rects, dom, mask, u, un, ld_, ny_ + 2 * g_, s_));
+  } else {
+    GMT_CHECK("jacobi xk", gmt_jacobi5xk(K, n, rects, dom, mask, u, un, ld_, cfg_.tile, s_));
+  }
+}
+
 // ks_ sweeps u(t) -> u(t+ks) in one pass: the ks-wide halo (corners included)
 // travels on the comm stream while the fused kernel updates the core whose
 // ks-step dependency cone stays inside the interior; the ks-wide frame
 // follows once the halo has landed.
 void JacobiSolver::enqueue_block(int parity, int K) {
   Halo2D& h = *halo_[parity];
-  const double* u = buf_[parity].data();
-  double* un = buf_[parity ^ 1].data();
   const int64_t dom[4] = {xo_, nx_, yo_, ny_};
   const int mask = halo_mask();
-  // the remainder pass of run() (K < ks_) uses the kernel default tile
-  const int tr = K == ks_ ? cfg_.tile : 0;
-  const int64_t KA = (K + 1) & ~1;  // x offsets stay even (16-B staging)
+  const int64_t KA = (K + 1) & ~1;  // x offsets stay even (16-B loads)
   if (!h.active()) {
-    GMT_CHECK("jacobi xk", gmt_jacobi5xk(K, 1, dom, dom, mask, u, un, ld_, tr, s_));
+    xk_launch(K, 1, dom, parity, false);
     return;
   }
   if (!cfg_.overlap || nx_ < 4 * KA + 2 || ny_ < 4 * K) {
     h.start(s_);
     h.finish(s_);
-    GMT_CHECK("jacobi xk", gmt_jacobi5xk(K, 1, dom, dom, mask, u, un, ld_, tr, s_));
+    xk_launch(K, 1, dom, parity, false);
     return;
   }
   // The core is inset only on the sides whose ghost ring is a neighbour's
   // halo (a Dirichlet side does not wait for the exchange; the kernel's rule
-  // band handles it).  The frame — the K-wide bands along the halo sides —
+  // path handles it).  The frame — the K-wide bands along the halo sides —
   // follows once the halo has landed.  The right band starts at an even
   // column: KA or KA+1 columns wide.
   const bool hw = mask & 1, he = mask & 2, hs = mask & 4, hn = mask & 8;
@@ -243,7 +261,7 @@ void JacobiSolver::enqueue_block(int parity, int K) {
   // GMT_CORE_AFTER_PACK=0 launches the core at once (A/B).
   h.start(cs_, core_after_pack_ ? ev_packed_ : nullptr);
   if (core_after_pack_) GMT_CHECK("wait", gmt_rt_stream_wait_event(s_, ev_packed_));
-  GMT_CHECK("core xk", gmt_jacobi5xk(K, 1, core, dom, mask, u, un, ld_, tr, s_));
+  xk_launch(K, 1, core, parity, false);
   h.finish(cs_);
   GMT_CHECK("event", gmt_rt_event_record(ev_halo_, cs_));
   GMT_CHECK("wait", gmt_rt_stream_wait_event(s_, ev_halo_));
@@ -258,11 +276,7 @@ void JacobiSolver::enqueue_block(int parity, int K) {
   if (hn) add(xo_, nx_, yo_ + ny_ - K, K);
   if (hw) add(xo_, KA, cy0, cy1 - cy0);
   if (he) add(xr, xo_ + nx_ - xr, cy0, cy1 - cy0);
-  // the pipelined kernel may cover the narrow bands with whole strips that
-  // reach into the finished core (same values rewritten): branch-free path
-  const bool pipe = (tr == 0 && K % 2 == 0) || (tr & GMT_XK_PIPE);
-  const int tf = pipe ? (tr | GMT_XK_PIPE | GMT_XK_EXT) : tr;
-  GMT_CHECK("frame xk", gmt_jacobi5xk(K, nf, frame, dom, mask, u, un, ld_, tf, s_));
+  xk_launch(K, nf, frame, parity, true);
 }
 
 void JacobiSolver::step_block() {
@@ -273,14 +287,13 @@ void JacobiSolver::step_block() {
   parity_ ^= 1;  // u(t+ks) lives in the other buffer
 }
 
-// Cost of one fused pass of K sweeps on a large domain (ms at 32768², fast +
-// ghost-rule kernels; rocprofv3 of bench.py, profiles/r01_k14.md; K <= 6
-// from gmt_kernel_bench, profiles/r01_k12.md): per-pass time is nearly flat
-// in K up to 8 (HBM-bound: one read + one write of the field); with the
-// multiply-free scaled levels K = 14 is the cheapest per sweep
-// (profiles/r01_scaled.md).
+// Cost of one fused pass of K sweeps on a large domain (ms at 32768²,
+// gmt_kernel_bench --only=tb, profiles/r02_tb.md): per-pass time is nearly
+// flat in K while the pass is HBM-bound (one read + one write of the
+// field) and grows once the K levels' VALU work dominates.
 // 0 = no kernel for that K (odd K > 3).
-static constexpr double kPassCost[15] = {0, 3.05, 3.5, 4.5, 3.3, 0, 3.7, 0, 3.41, 0, 4.05, 0, 4.03, 0, 4.45};
+static constexpr double kPassCost[GMT_TB_MAX_SWEEPS + 1] = {0,   3.05, 3.3, 4.5, 3.3, 0,   3.4, 0,  3.5,
+                                                           0,   3.7,  0,   3.9, 0,   4.2, 0,   4.6};
 static constexpr double kPassOverhead = 0.05;  // launches + one halo exchange
 
 std::vector<int> JacobiSolver::plan_passes(int k) const {
@@ -319,6 +332,22 @@ void JacobiSolver::run(int k) {
     }
   }
   watchdog_kick("jacobi steps enqueued");
+}
+
+void JacobiSolver::prepare(int k) {
+  std::vector<int> kinds;
+  for (int K : plan_passes(k))
+    if (std::find(kinds.begin(), kinds.end(), K) == kinds.end()) kinds.push_back(K);
+  for (int K : kinds) {
+    if (K == 1) {
+      enqueue_step(parity_);
+    } else {
+      enqueue_block(parity_, K);
+    }
+    parity_ ^= 1;
+  }
+  synchronize();
+  init_field();
 }
 
 void JacobiSolver::capture_graphs() {
@@ -387,6 +416,10 @@ double JacobiSolver::residual() {
 
 void JacobiSolver::exchange_only() {
   Halo2D& h = *halo_[parity_];
+  // the exchange packs the current field and writes its ghost ring: order it
+  // after every pass already enqueued on the compute stream
+  GMT_CHECK("event", gmt_rt_event_record(ev_start_, s_));
+  GMT_CHECK("wait", gmt_rt_stream_wait_event(cs_, ev_start_));
   h.start(cs_);
   h.finish(cs_);
   GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));

@@ -106,6 +106,11 @@ int gmt_fill_poly(int mode, int64_t nx, int64_t ny, double x0, double dx, double
                   double* z, int64_t ld, void*) {
   for (int64_t j = 0; j < ny; ++j)
     for (int64_t i = 0; i < nx; ++i) {
+      if (mode == 4) {  // integer lattice, see reduce.hip (built with -ffp-contract=off)
+        const double xl = (x0 + static_cast<double>(i)) * dx, yl = (y0 + static_cast<double>(j)) * dy;
+        z[j * ld + i] = xl * xl * xl + yl * yl;
+        continue;
+      }
       const double x = x0 + i * dx, y = y0 + j * dy;
       z[j * ld + i] = mode == 0 ? x * x * x + y * y : (mode == 1 ? 3 * x * x : (mode == 2 ? 2 * y : x));
     }

@@ -20,19 +20,35 @@ enum gmt_engine_transport { GMT_ENGINE_LOCAL = 0, GMT_ENGINE_RCCL = 1 };
 
 /* fills 128 bytes (an RCCL unique id); returns 0 or an error code */
 int gmt_engine_unique_id(void* out128);
-/* flags: bit0 periodic, bit1 overlap, bit2 graph, bit3 temporal blocking (2 sweeps/pass),
- * bit4 overlap auto-tune (time both modes once, keep the faster on every rank),
- * bits 8-11 sweeps per fused pass (2-14; overrides bit3).  ccl_id: 128 bytes (RCCL) or NULL (local) */
+/* Engine options (explicit fields; 0 = default everywhere). */
+typedef struct gmt_engine_opts {
+  int periodic; /* 1: periodic process grid, else Dirichlet (fixed ghost ring) */
+  int overlap;  /* 0 off, 1 halo exchange overlapped with the core pass, 2 auto (time both once) */
+  int graph;    /* 1: capture the per-parity passes into hipGraphs */
+  int tsteps;   /* sweeps per fused pass and per halo exchange: 1 (or 0) = single sweeps, 2..16 */
+  int variant;  /* single-sweep kernel variant (gmt_jacobi5_set_variant; 0 = default) */
+  int wg_waves; /* temporal-blocking kernel: waves per workgroup (0 = auto) */
+  int seg_rows; /* temporal-blocking kernel: output rows per workgroup (0 = auto) */
+  int exact;    /* -1 / 0: power-of-two scaled levels when the field bound allows (auto),
+                   1: always the exact 1/4-per-level form */
+} gmt_engine_opts;
+/* ccl_id: 128 bytes (RCCL) or NULL (local); NULL on invalid options */
 void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank, int world,
-                               int transport, const void* ccl_id, int flags, int variant);
+                               int transport, const void* ccl_id, const gmt_engine_opts* opts);
 void gmt_engine_jacobi_destroy(void* h);
 int gmt_engine_jacobi_run(void* h, int steps); /* enqueue `steps` steps */
 int gmt_engine_jacobi_sync(void* h);
 double gmt_engine_jacobi_residual(void* h);
 int gmt_engine_jacobi_exchange(void* h); /* one blocking halo exchange */
-/* out[13]: nx, ny, off_x, off_y, bytes_per_exchange, messages, graph, overlap, py, px, tsteps,
- * overlap_auto ns per pass with overlap, without (0 if not tuned) */
+/* out[14]: nx, ny, off_x, off_y, bytes_per_exchange, messages, graph, overlap, py, px, tsteps,
+ * overlap_auto ns per pass with overlap, without (0 if not tuned), exact arithmetic in use */
 int gmt_engine_jacobi_info(void* h, int64_t* out);
+/* The fused passes (sweeps per pass, in launch order) that run(steps) enqueues:
+ * writes min(n, max) entries, returns n. */
+int gmt_engine_jacobi_plan(void* h, int steps, int* out, int max);
+/* Launch one pass of every pass type run(steps) will use, then restore the
+ * initial field (first-launch costs stay out of a timed run). */
+int gmt_engine_jacobi_prepare(void* h, int steps);
 int gmt_engine_jacobi_copy_interior(void* h, double* host);
 const char* gmt_engine_backend(void);
 

@@ -17,10 +17,12 @@
 //     are captured into hipGraphs and replayed — one host call per step, so
 //     small per-GPU domains (strong scaling at 8 GPUs) are not launch-bound.
 //
-//   * tblock: two sweeps per kernel and per exchange (temporal blocking):
-//     u(t) is read once and u(t+2) written once (gmt_jacobi5x2), the halo is
-//     2 wide and exchanged every other sweep, with corners (two-phase
-//     exchange) — bitwise the same result as single sweeps.
+//   * tblock: K = tsteps sweeps per kernel and per exchange (temporal
+//     blocking): u(t) is read once and u(t+K) written once (gmt_jacobi5tb,
+//     csrc/kernels/jacobi5tb.hip, for even K; the LDS-tiled gmt_jacobi5xk
+//     for K = 3), the halo is K wide and exchanged once per pass with its
+//     corners (one-phase exchange) — bitwise the same result as K single
+//     sweeps.
 // Storage is column-major (x contiguous) with the interior origin at x = 8
 // so every interior row starts 64-B aligned and the sweep kernels take their
 // 16-B vector path; the row pitch is padded to 64 doubles.
@@ -42,20 +44,25 @@ struct JacobiConfig {
   bool overlap = true;
   // overlap_auto: time a few fused passes with and without overlap at
   // construction (then restore the initial field) and keep the faster — the
-  // same choice on every rank (summed over ranks).  Whether hiding the
+  // same choice on every rank (the per-pass times are averaged over ranks).  Whether hiding the
   // exchange pays for the frame pass depends on the link (self-exchange on
   // one GPU: serial 4-8 % faster, profiles/r01_frame.md); measure it.
   bool overlap_auto = false;
   bool graph = false;
   int variant = 0;                               // gmt_jacobi5_set_variant
-  // temporal blocking: tsteps (2-12) sweeps per memory pass (gmt_jacobi5xk;
-  // even counts run the register-pipelined kernel, 3 the LDS-tiled one)
-  // and per halo exchange (ghost width tsteps, corners via a two-phase
-  // exchange) — 1/tsteps of the HBM bytes and messages per lattice update.
-  // 1 = off.  tblock = true is tsteps = 2.
+  // temporal blocking: tsteps (2-16) sweeps per memory pass (even counts:
+  // gmt_jacobi5tb; 3: the LDS-tiled gmt_jacobi5xk; other odd counts round
+  // down) and per halo exchange (ghost width tsteps, corners in the same
+  // exchange phase) — 1/tsteps of the HBM bytes and messages per lattice
+  // update.  1 = off.  tblock = true with tsteps = 0 is tsteps = 2.
   bool tblock = false;
   int tsteps = 0;
-  int tile = 0;                                  // gmt_jacobi5x2 tile ((TX<<16)|TY, 0 = default)
+  int tile = 0;                                  // gmt_jacobi5x2 tile ((TX<<16)|TY, 0 = default; K = 3 only)
+  int wg_waves = 0;                              // gmt_tb_opts.wg_waves (0 = auto)
+  int seg_rows = 0;                              // gmt_tb_opts.seg_rows (0 = auto)
+  // -1 / 0: power-of-two scaled levels when max|u| * 4^K stays finite (the
+  // initial field bounds every later one: Jacobi averages), 1: always exact
+  int exact = -1;
 };
 
 class JacobiSolver {
@@ -72,8 +79,14 @@ class JacobiSolver {
   void synchronize();
   // sqrt(global sum (u_{k+1} - u_k)^2) of one extra sweep (advances the solution)
   double residual();
-  // one blocking halo exchange of the current field (latency measurements)
+  // one blocking halo exchange of the current field (latency measurements);
+  // ordered after every pass already enqueued
   void exchange_only();
+  // launch one pass of every pass type run(k) uses, then restore the initial
+  // field: first-launch costs (code object, occupancy query) stay out of a
+  // timed run(k)
+  void prepare(int k);
+  bool exact() const { return exact_; }
   // local interior, row-major [ny][nx] (host memory)
   void copy_interior(double* host) const;
 
@@ -89,7 +102,7 @@ class JacobiSolver {
   int ghost() const { return g_; }
   bool overlap_active() const { return cfg_.overlap && halo_[0] && halo_[0]->active(); }
   const Neighbors& neighbors() const { return nb_; }
-  // overlap_auto: seconds per pass measured {overlap, serial} (max over ranks), 0 if not tuned
+  // overlap_auto: seconds per pass measured {overlap, serial} (mean over ranks), 0 if not tuned
   double tuned_overlap_s() const { return tune_s_[0]; }
   double tuned_serial_s() const { return tune_s_[1]; }
   gmt_stream_t stream() const { return s_; }
@@ -97,6 +110,8 @@ class JacobiSolver {
  private:
   void enqueue_step(int parity);
   void enqueue_block(int parity, int k);  // k <= ks_ fused sweeps
+  // one fused k-sweep launch on `n` output rects (gmt_jacobi5tb / gmt_jacobi5xk)
+  void xk_launch(int k, int n, const int64_t* rects, int parity, bool frame);
   void step_block();
   void sweep_full(int parity, double* resid);
   void capture_graphs();
@@ -110,6 +125,7 @@ class JacobiSolver {
   int64_t xo_ = 8, yo_ = 1, ld_ = 0;           // interior origin (absolute), row pitch
   int g_ = 1;                                  // ghost width
   int ks_ = 1;                                 // sweeps per fused pass
+  bool exact_ = false;                         // gmt_tb_opts.exact for the fused passes
   Neighbors nb_;
   Buffer<double> buf_[2];
   std::unique_ptr<Halo2D> halo_[2];

@@ -82,7 +82,9 @@ int gmt_diff_sq(int64_t nx, int64_t ny, const double* a, int64_t lda, const doub
 /* ---- analytic fill z[y][x] = (x0+i*dx)^3 + (y0+j*dy)^2 over nx x ny (device
  *      side replacement of the reference's host init loops,
  *      mpi_stencil2d_gt.cc:439-497).  mode 0: x^3+y^2 (z), 1: 3x^2 (dz/dx),
- *      2: 2y (dz/dy), 3: x (linear ramp; DAXPY inputs). */
+ *      2: 2y (dz/dy), 3: x (linear ramp; DAXPY inputs), 4: x^3+y^2 on the
+ *      integer lattice x = (x0 + i)*dx, y = (y0 + j)*dy with x0, y0 integer
+ *      indices, no fma contraction (bitwise reproducible on the host). */
 int gmt_fill_poly(int mode, int64_t nx, int64_t ny, double x0, double dx, double y0,
                   double dy, double* z, int64_t ld, void* stream);
 
@@ -129,18 +131,16 @@ int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int halo
 /* ---- Temporal-blocking Jacobi (csrc/kernels/jacobi5tb.hip): `sweeps` fused
  *      Laplace sweeps per memory pass on up to 8 output rects {x0, nx, y0, ny}
  *      (absolute, x0 even, x0 >= sweeps, y0 >= sweeps, y0+ny+sweeps <= nrows).
- *      Workgroups of `wg_waves` waves (128 columns each) share their edge
- *      columns through LDS.  Cells of the interior `dom` outside the rects
- *      are never written.  halo_mask as for gmt_jacobi5x2. */
+ *      Cells of the interior `dom` outside the rects are never written.
+ *      halo_mask as for gmt_jacobi5x2. */
 #define GMT_TB_MAX_SWEEPS 16
 typedef struct gmt_tb_opts {
   int sweeps;   /* K: even, 2..GMT_TB_MAX_SWEEPS */
-  int wg_waves; /* waves per workgroup, 1..8 (0 = auto: 4, or 1 for rects <= one strip) */
-  int seg_rows; /* output rows per workgroup (0 = auto from the device occupancy) */
+  int wg_waves; /* independent 128-column waves per workgroup, 1..8 (0 = 4) */
+  int seg_rows; /* output rows per wave (0 = default: 192-384 by K, fewer for small domains) */
   int exact;    /* 1: multiply by 1/4 per level (bitwise for any magnitude);
                    0: power-of-two scaled levels (bitwise unless a value is
                    subnormal or |u| * 4^K overflows) */
-  int prefetch; /* input rows in flight per wave: 3 or 6 (0 = 3) */
 } gmt_tb_opts;
 int gmt_jacobi5tb(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, const int64_t* dom,
                   int halo_mask, const double* u, double* un, int64_t ld, int64_t nrows, void* stream);

@@ -160,8 +160,17 @@ __global__ __launch_bounds__(kBlock) void fill_poly_kernel(int mode, int64_t nx,
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
   if (i >= nx * ny) return;
   const int64_t ix = i % nx, iy = i / nx;
-  const double x = x0 + ix * dx, y = y0 + iy * dy;
   double v;
+  if (mode == 4) {
+    // integer lattice: x = (x0 + ix) * dx with x0 an integer index (exact
+    // sum, one rounding) and no fma contraction, so a NumPy reference
+    // (x*x*x + y*y on the same lattice) is bitwise equal
+#pragma clang fp contract(off)
+    const double x = (x0 + static_cast<double>(ix)) * dx, y = (y0 + static_cast<double>(iy)) * dy;
+    z[iy * ld + ix] = x * x * x + y * y;
+    return;
+  }
+  const double x = x0 + ix * dx, y = y0 + iy * dy;
   if (mode == 0)
     v = x * x * x + y * y;
   else if (mode == 1)

@@ -50,7 +50,6 @@ class TbOpts(ctypes.Structure):
         ("wg_waves", c_int),
         ("seg_rows", c_int),
         ("exact", c_int),
-        ("prefetch", c_int),
     ]
 
 _SIGS = {

@@ -30,7 +30,14 @@ HIP_ENGINE = os.path.join(_HERE, "_lib", "libgmt_engine.so")
 HOST_ENGINE = os.path.join(_ROOT, "build", "lib-host", "libgmt_engine.so")
 
 LOCAL, RCCL = 0, 1
+MAX_TSTEPS = 16  # GMT_TB_MAX_SWEEPS (csrc/include/gmt/kernels.h)
 _libs: dict[str, ctypes.CDLL] = {}
+
+
+class EngineOpts(ctypes.Structure):
+    """gmt_engine_opts (csrc/include/gmt/engine.h)."""
+    _fields_ = [(n, ctypes.c_int) for n in
+                ("periodic", "overlap", "graph", "tsteps", "variant", "wg_waves", "seg_rows", "exact")]
 
 
 class EngineError(RuntimeError):
@@ -55,8 +62,7 @@ def load(device: str = "cuda") -> ctypes.CDLL:
     vp, i64, c_int = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
     lib.gmt_engine_unique_id.argtypes = [vp]
     lib.gmt_engine_unique_id.restype = c_int
-    lib.gmt_engine_jacobi_create.argtypes = [i64, i64, c_int, c_int, c_int, c_int, c_int, vp, c_int,
-                                             c_int]
+    lib.gmt_engine_jacobi_create.argtypes = [i64, i64, c_int, c_int, c_int, c_int, c_int, vp, vp]
     lib.gmt_engine_jacobi_create.restype = vp
     lib.gmt_engine_jacobi_destroy.argtypes = [vp]
     lib.gmt_engine_jacobi_destroy.restype = None
@@ -69,6 +75,10 @@ def load(device: str = "cuda") -> ctypes.CDLL:
     lib.gmt_engine_jacobi_residual.restype = ctypes.c_double
     lib.gmt_engine_jacobi_info.argtypes = [vp, ctypes.POINTER(i64)]
     lib.gmt_engine_jacobi_info.restype = c_int
+    lib.gmt_engine_jacobi_plan.argtypes = [vp, c_int, ctypes.POINTER(c_int), c_int]
+    lib.gmt_engine_jacobi_plan.restype = c_int
+    lib.gmt_engine_jacobi_prepare.argtypes = [vp, c_int]
+    lib.gmt_engine_jacobi_prepare.restype = c_int
     lib.gmt_engine_jacobi_copy_interior.argtypes = [vp, vp]
     lib.gmt_engine_jacobi_copy_interior.restype = c_int
     lib.gmt_engine_backend.restype = ctypes.c_char_p
@@ -99,7 +109,8 @@ class NativeJacobi:
     def __init__(self, ny: int, nx: int, env: "gdist.DistEnv | None" = None,
                  dims: tuple[int, int] | None = None, periodic: bool = False,
                  overlap: "bool | str" = True, graph: bool = True, variant: int = 0,
-                 tblock: bool | int = False):
+                 tblock: bool | int = False, wg_waves: int = 0, seg_rows: int = 0, exact: int = -1,
+                 transport: str = "auto"):
         from .parallel.decomp import choose_dims
 
         self.env = env or gdist.get()
@@ -110,27 +121,43 @@ class NativeJacobi:
         if py * px != e.world_size:
             raise ValueError(f"process grid {py}x{px} != world size {e.world_size}")
         self.ny_g, self.nx_g, self.py, self.px = ny, nx, py, px
-        if e.world_size == 1:
+        if transport not in ("auto", "local", "rccl"):
+            raise ValueError(f"transport must be auto, local or rccl, got {transport!r}")
+        if e.world_size == 1 and transport != "rccl":
             transport, cid = LOCAL, None
+        elif e.world_size == 1:
+            # a 1-rank RCCL communicator: a periodic domain exchanges its halo
+            # with itself through ncclSend/ncclRecv (latency measurements)
+            transport = RCCL
+            buf = ctypes.create_string_buffer(128)
+            if self.lib.gmt_engine_unique_id(buf):
+                raise EngineError("RCCL unique id failed")
+            cid = ctypes.create_string_buffer(bytes(buf.raw), 128)
         else:
+            if transport == "local":
+                raise ValueError("transport 'local' needs world size 1")
             # GPU: RCCL over xGMI.  CPU: the host backend's emulation of the same
             # RCCL semantics over Unix sockets (csrc/host/ccl_host.cpp), so the
             # multi-rank engine path runs and is checked without GPUs.
             transport = RCCL
             cid = ctypes.create_string_buffer(_broadcast_unique_id(self.lib, e), 128)
-        ks = 0 if not tblock else (2 if tblock is True else int(tblock))
+        ks = 1 if not tblock else (2 if tblock is True else int(tblock))
+        if not 1 <= ks <= MAX_TSTEPS:
+            raise ValueError(f"tblock: sweeps per fused pass must be 1..{MAX_TSTEPS}, got {ks}")
         # overlap: True / False / "auto" (time both once, every rank keeps the faster)
         auto = overlap == "auto"
-        flags = ((1 if periodic else 0) | (2 if (overlap or auto) else 0) | (4 if graph else 0)
-                 | (16 if auto else 0) | ((ks & 0xF) << 8))
+        opts = EngineOpts(periodic=int(bool(periodic)), overlap=2 if auto else int(bool(overlap)),
+                          graph=int(bool(graph)), tsteps=ks, variant=int(variant), wg_waves=int(wg_waves),
+                          seg_rows=int(seg_rows), exact=int(exact))
         self.h = self.lib.gmt_engine_jacobi_create(ny, nx, py, px, e.rank, e.world_size, transport,
-                                                   cid, flags, variant)
+                                                   cid, ctypes.byref(opts))
         if not self.h:
             raise EngineError("gmt_engine_jacobi_create failed")
-        info = (ctypes.c_int64 * 13)()
+        info = (ctypes.c_int64 * 14)()
         self.lib.gmt_engine_jacobi_info(self.h, info)
         (self.nx, self.ny, self.off_x, self.off_y, self.halo_bytes, self.halo_msgs,
-         graph_on, overlap_on, _, _, tb, t_ov, t_ser) = list(info)
+         graph_on, overlap_on, _, _, tb, t_ov, t_ser, exact_on) = list(info)
+        self.exact = bool(exact_on)
         # overlap="auto": measured seconds per fused pass {overlap, serial} (mean over ranks)
         self.tuned = {"overlap_s": t_ov / 1e9, "serial_s": t_ser / 1e9} if auto and t_ov else None
         self.tsteps = int(tb)
@@ -145,6 +172,16 @@ class NativeJacobi:
 
     def step(self) -> None:
         self.run(1)
+
+    def plan(self, steps: int) -> list[int]:
+        """Sweeps per fused pass, in launch order, that ``run(steps)`` enqueues."""
+        buf = (ctypes.c_int * max(1, steps))()
+        n = self.lib.gmt_engine_jacobi_plan(self.h, int(steps), buf, max(1, steps))
+        return list(buf[:n])
+
+    def prepare(self, steps: int) -> None:
+        """One pass of every pass type ``run(steps)`` uses, then the initial field again."""
+        self.lib.gmt_engine_jacobi_prepare(self.h, int(steps))
 
     def synchronize(self) -> None:
         self.lib.gmt_engine_jacobi_sync(self.h)
@@ -209,11 +246,13 @@ def deriv_bench(n_local: int = 1024, n_other: int = 512 * 1024, n_iter: int = 10
 
 
 def serial_jacobi(ny: int, nx: int, steps: int, periodic: bool = False) -> np.ndarray:
-    """NumPy reference of exactly the engine's problem (init, boundary, update)."""
+    """NumPy reference of exactly the engine's problem (init, boundary, update):
+    bitwise — the engine fills x^3 + y^2 on the same integer lattice with the
+    same operation order (gmt_fill_poly mode 4) and sweeps in the same order."""
     h = 1.0 / (max(ny, nx) + 1)
-    x = (np.arange(nx + 2) - 1) * h
-    y = (np.arange(ny + 2) - 1) * h
-    u = (x[None, :] ** 3) + (y[:, None] ** 2)
+    x = (np.arange(nx + 2, dtype=np.float64) - 1.0) * h
+    y = (np.arange(ny + 2, dtype=np.float64) - 1.0) * h
+    u = (x[None, :] * x[None, :] * x[None, :]) + (y[:, None] * y[:, None])
     un = u.copy()
     for _ in range(steps):
         if periodic:

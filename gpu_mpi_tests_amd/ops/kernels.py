@@ -303,13 +303,13 @@ def jacobi5xk(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[i
 
 def jacobi5tb(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, int, int, int]],
               dom: tuple[int, int, int, int], halo_mask: int = 0, *, wg_waves: int = 0, seg_rows: int = 0,
-              exact: bool = False, prefetch: int = 0) -> None:
+              exact: bool = False) -> None:
     """``k`` (even, 2-16) fused Laplace sweeps with the workgroup-cooperative
     temporal-blocking kernel (csrc/kernels/jacobi5tb.hip): ``un = J^k(u)`` on up to
     8 output rects (absolute coordinates, x0 even, x0 >= k, y0 >= k); the rest of
-    ``un`` is never written.  ``wg_waves``: 128-column waves per workgroup (0 = auto),
-    ``seg_rows``: output rows per workgroup (0 = auto), ``exact``: 1/4 multiply per
-    level instead of power-of-two scaled levels, ``prefetch``: 3 or 5 rows in flight."""
+    ``un`` is never written.  ``wg_waves``: independent 128-column waves per
+    workgroup (0 = 4), ``seg_rows``: output rows per wave (0 = default), ``exact``:
+    1/4 multiply per level instead of power-of-two scaled levels."""
     rects = [tuple(int(v) for v in r) for r in rects if r[1] > 0 and r[3] > 0]
     if not rects:
         return
@@ -321,7 +321,7 @@ def jacobi5tb(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[i
     L = _native.lib()
     arr = (ctypes.c_int64 * (4 * len(rects)))(*[v for r in rects for v in r])
     d = (ctypes.c_int64 * 4)(*[int(v) for v in dom])
-    o = _native.TbOpts(int(k), int(wg_waves), int(seg_rows), int(bool(exact)), int(prefetch))
+    o = _native.TbOpts(int(k), int(wg_waves), int(seg_rows), int(bool(exact)))
     _native.check(L.gmt_jacobi5tb(ctypes.byref(o), len(rects), ctypes.cast(arr, ctypes.c_void_p),
                                   ctypes.cast(d, ctypes.c_void_p), int(halo_mask), u.data_ptr(),
                                   un.data_ptr(), u.stride(0), u.shape[0], _stream(u)),

@@ -31,12 +31,25 @@ def _check(rec, n, steps, warmup, scaling="strong", points=256 * 256):
     assert rec["config"]["global_batch"] == points
 
 
+def _baseline_keys(rec, small):
+    """Every BASELINE quantity is in the line, plus the correctness gate."""
+    assert rec["check_max_diff"] == 0.0  # the engine is bitwise equal to the serial reference
+    assert rec["daxpy_GBps"] > 0 and rec["daxpy_n"] > 0
+    assert rec[f"stencil_{small}_MLUPS"] > 0 and "steps:" in rec[f"stencil_{small}_pass_plan"]
+    assert rec["halo_exchange_us"] is not None and rec["halo_exchange_us"] > 0
+    assert rec["halo_exchange_kind"]
+    plan = rec["config"]["pass_plan"]
+    assert plan and sum(int(a) * int(b) for a, b in (p.split("x") for p in plan.split("+"))) == rec["steps"]
+
+
 def test_bench_single_process_native_engine_cpu():
-    rec = _run([sys.executable, "bench.py", "--device", "cpu", "--size", "256", "--steps", "4",
-                "--warmup", "1", "--daxpy-n", "20000"])
-    _check(rec, 1, 4, 1)
+    rec = _run([sys.executable, "bench.py", "--device", "cpu", "--size", "256", "--steps", "20",
+                "--warmup", "5", "--daxpy-n", "20000", "--small-size", "96"])
+    _check(rec, 1, 20, 5)
     assert rec["config"]["engine"] == "native"
-    assert rec["daxpy_GBps"] > 0
+    _baseline_keys(rec, 96)
+    # N = 1: the halo latency is a labelled 1-rank periodic RCCL self-exchange
+    assert "self-exchange" in rec["halo_exchange_kind"]
 
 
 def test_bench_two_ranks_torchrun_cpu():
@@ -45,9 +58,9 @@ def test_bench_two_ranks_torchrun_cpu():
                 "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
                 "--device", "cpu", "--size", "256", "--steps", "3", "--warmup", "1",
                 "--daxpy-n", "20000", "--ref-n-local", "32", "--ref-n-other", "300",
-                "--ref-iters", "4"])
+                "--ref-iters", "4", "--small-size", "96"])
     _check(rec, 2, 3, 1)
-    # the GPU run's path: native engine, RCCL semantics (host emulation on CPU)
+    _baseline_keys(rec, 96)
     assert rec["config"]["engine"] == "native" and rec["config"]["transport"] == "rccl-host"
     assert rec["halo_exchange_us"] is not None and rec["halo_exchange_us"] > 0
     # the reference's own halo benchmark (test_deriv dim 0/1 + test_sum) on the same ranks
@@ -55,18 +68,6 @@ def test_bench_two_ranks_torchrun_cpu():
     assert rec["ref_halo_bytes_per_rank"] == 2 * 2 * 300 * 8 // 2  # edge ranks: one neighbour
     assert rec["ref_halo_dim0_err_norm"] < 1e-6 and rec["ref_halo_dim1_err_norm"] < 1e-6
     assert rec["ref_allreduce_1024_us"] > 0
-
-
-def test_bench_two_ranks_torch_engine_cpu():
-    port = str(free_port())
-    rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
-                "--device", "cpu", "--size", "256", "--steps", "3", "--warmup", "1",
-                "--daxpy-n", "20000", "--engine", "torch", "--ref-n-local", "32",
-                "--ref-n-other", "300", "--ref-iters", "2"])
-    _check(rec, 2, 3, 1)
-    assert rec["config"]["engine"] == "torch"  # torch.distributed (gloo) P2P from Python
-    assert rec["halo_exchange_us"] is not None and rec["halo_exchange_us"] > 0
 
 
 def test_bench_two_ranks_weak_scaling_cpu():
