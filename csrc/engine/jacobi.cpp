@@ -287,26 +287,44 @@ void JacobiSolver::step_block() {
   parity_ ^= 1;  // u(t+ks) lives in the other buffer
 }
 
-// Cost of one fused pass of K sweeps on a large domain (ms at 32768²,
-// gmt_kernel_bench --only=tb, profiles/r02_tb.md): per-pass time is nearly
-// flat in K while the pass is HBM-bound (one read + one write of the
-// field) and grows once the K levels' VALU work dominates.
-// 0 = no kernel for that K (odd K > 3).
-static constexpr double kPassCost[GMT_TB_MAX_SWEEPS + 1] = {0,   3.05, 3.3, 4.5, 3.3, 0,   3.4, 0,  3.5,
-                                                           0,   3.7,  0,   3.9, 0,   4.2, 0,   4.6};
-static constexpr double kPassOverhead = 0.05;  // launches + one halo exchange
+// Measured cost of one fused pass of K sweeps (ms; gmt_kernel_bench
+// --only=tb with the default launch, MI355X, profiles/r02_tb.md) on two
+// domain sizes: the pass is HBM-bound up to K ~ 10 (the strip access
+// pattern's ~5.2 TB/s: about the same time for every K) and VALU-bound
+// beyond, and where that turns depends on the domain (strip count, rule
+// waves, launch tail).  K = 1 is the single-sweep kernel, K = 3 the
+// LDS-tiled one; 0 = no kernel for that K (odd K > 3).
+namespace {
+struct PassCosts {
+  double points;  // lattice points of the measured domain
+  double ms[GMT_TB_MAX_SWEEPS + 1];
+};
+constexpr PassCosts kCostLarge = {32768.0 * 32768.0, {0, 3.05, 3.62, 4.5, 3.43, 0, 3.51, 0, 3.46, 0, 3.74, 0,
+                                                      3.58, 0, 4.08, 0, 4.64}};
+constexpr PassCosts kCostSmall = {8192.0 * 8192.0, {0, 0.20, 0.225, 0.30, 0.219, 0, 0.236, 0, 0.235, 0, 0.261,
+                                                    0, 0.295, 0, 0.346, 0, 0.445}};
+constexpr double kLaunchMs = 0.015;    // host launch + dispatch per pass
+constexpr double kExchangeMs = 0.035;  // a halo exchange not hidden by the overlap
+}  // namespace
 
 std::vector<int> JacobiSolver::plan_passes(int k) const {
   std::vector<int> plan;
   if (k <= 0) return plan;
   if (ks_ <= 1) return std::vector<int>(k, 1);
+  // the table measured on the closer domain size, scaled to this rank's
+  const double pts = static_cast<double>(nx_) * static_cast<double>(ny_);
+  const PassCosts& tab = std::fabs(std::log(pts / kCostLarge.points)) < std::fabs(std::log(pts / kCostSmall.points))
+                             ? kCostLarge
+                             : kCostSmall;
+  const double scale = pts / tab.points;
+  const double over = kLaunchMs + (halo_[0] && halo_[0]->active() && !cfg_.overlap ? kExchangeMs : 0.0);
   std::vector<double> best(k + 1, 1e300);
   std::vector<int> pick(k + 1, 0);
   best[0] = 0.0;
   for (int s = 1; s <= k; ++s)
     for (int K = 1; K <= ks_ && K <= s; ++K) {
-      if (kPassCost[K] <= 0) continue;
-      const double c = best[s - K] + kPassCost[K] + kPassOverhead;
+      if (tab.ms[K] <= 0) continue;
+      const double c = best[s - K] + tab.ms[K] * scale + over;
       if (c < best[s]) {
         best[s] = c;
         pick[s] = K;

@@ -92,6 +92,29 @@ def load(device: str = "cuda") -> ctypes.CDLL:
     return lib
 
 
+class _StdoutToStderr:
+    """RCCL prints its init banner ("RCCL version : ...") on the process's
+    C stdout; bench.py's driver contract is ONE JSON line on stdout, so
+    communicator creation runs with fd 1 pointed at stderr."""
+
+    def __enter__(self):
+        import sys
+        sys.stdout.flush()
+        self._libc = ctypes.CDLL(None)
+        self._libc.fflush(None)
+        self._saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        import sys
+        self._libc.fflush(None)
+        sys.stdout.flush()
+        os.dup2(self._saved, 1)
+        os.close(self._saved)
+        return False
+
+
 def _broadcast_unique_id(lib, env) -> bytes:
     buf = ctypes.create_string_buffer(128)
     if env.rank == 0:
@@ -149,8 +172,9 @@ class NativeJacobi:
         opts = EngineOpts(periodic=int(bool(periodic)), overlap=2 if auto else int(bool(overlap)),
                           graph=int(bool(graph)), tsteps=ks, variant=int(variant), wg_waves=int(wg_waves),
                           seg_rows=int(seg_rows), exact=int(exact))
-        self.h = self.lib.gmt_engine_jacobi_create(ny, nx, py, px, e.rank, e.world_size, transport,
-                                                   cid, ctypes.byref(opts))
+        with _StdoutToStderr():
+            self.h = self.lib.gmt_engine_jacobi_create(ny, nx, py, px, e.rank, e.world_size, transport,
+                                                       cid, ctypes.byref(opts))
         if not self.h:
             raise EngineError("gmt_engine_jacobi_create failed")
         info = (ctypes.c_int64 * 14)()
@@ -230,8 +254,9 @@ def deriv_bench(n_local: int = 1024, n_other: int = 512 * 1024, n_iter: int = 10
     else:
         transport, cid = LOCAL, None
     out = (ctypes.c_double * 14)()
-    err = lib.gmt_engine_deriv_bench(int(n_local), int(n_other), int(n_iter), int(n_warmup), e.rank,
-                                     e.world_size, transport, cid, out)
+    with _StdoutToStderr():
+        err = lib.gmt_engine_deriv_bench(int(n_local), int(n_other), int(n_iter), int(n_warmup), e.rank,
+                                         e.world_size, transport, cid, out)
     if err:
         raise EngineError(f"gmt_engine_deriv_bench failed: {err}")
     v = list(out)

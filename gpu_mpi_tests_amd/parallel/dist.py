@@ -118,7 +118,10 @@ def init(backend: str | None = None, device: str | None = None, timeout_s: float
         if backend == "nccl":
             kw["device_id"] = env.device  # eager RCCL communicator init
         if not dist.is_initialized():
-            dist.init_process_group(**kw)
+            from ..engine import _StdoutToStderr  # RCCL's init banner stays off stdout
+
+            with _StdoutToStderr():
+                dist.init_process_group(**kw)
             env.initialized_here = True
         env.backend = backend
         env.host_group = dist.new_group(backend="gloo") if backend != "gloo" else dist.group.WORLD
