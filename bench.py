@@ -54,7 +54,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-DEFAULT_TSTEPS = 16  # max fused sweeps per memory pass / halo exchange; the engine plans the mix (profiles/r02_tb.md)
+DEFAULT_TSTEPS = 20  # max fused sweeps per memory pass / halo exchange; the engine plans the mix (profiles/r02_tb.md)
 
 from gpu_mpi_tests_amd import ops  # noqa: E402
 from gpu_mpi_tests_amd.engine import MAX_TSTEPS  # noqa: E402

@@ -20,11 +20,27 @@
 
 using namespace gmt;
 
+// --sustained=1: the mean of `iters` back-to-back launches (one event pair,
+// the GPU never idles: what a solver loop sees, clocks included); default:
+// the median of `iters` launches each synchronised on its own
+static bool g_sustained = false;
+
 static double time_ms(gmt_stream_t s, int iters, const std::function<void()>& f) {
   gmt_event_t e0, e1;
   GMT_CHECK("event", gmt_rt_event_create(&e0, 1));
   GMT_CHECK("event", gmt_rt_event_create(&e1, 1));
   for (int w = 0; w < 3; ++w) f();
+  if (g_sustained) {
+    GMT_CHECK("rec", gmt_rt_event_record(e0, s));
+    for (int k = 0; k < iters; ++k) f();
+    GMT_CHECK("rec", gmt_rt_event_record(e1, s));
+    GMT_CHECK("sync", gmt_rt_event_synchronize(e1));
+    float ms = 0;
+    GMT_CHECK("elapsed", gmt_rt_event_elapsed_ms(&ms, e0, e1));
+    gmt_rt_event_destroy(e0);
+    gmt_rt_event_destroy(e1);
+    return ms / iters;
+  }
   Stats st;
   for (int k = 0; k < iters; ++k) {
     GMT_CHECK("rec", gmt_rt_event_record(e0, s));
@@ -45,6 +61,7 @@ int main(int argc, char** argv) {
   const int iters = static_cast<int>(cli.geti("iters", 20));
   const std::string only = cli.get("only", "daxpy,jacobi,stencil,pack");
   const std::string json = cli.get("json", "");
+  g_sustained = cli.geti("sustained", 0) != 0;
   gmt_stream_t s = nullptr;
   GMT_CHECK("stream", gmt_rt_stream_create(&s, 0));
   auto report = [&](const char* kernel, int variant, const char* shape, double ms, double bytes) {
@@ -55,7 +72,8 @@ int main(int argc, char** argv) {
         .add("ms", ms).add("GBps", gbps).add("backend", gmt_rt_backend_name());
     j.append_to(json);
   };
-  std::printf("# gmt_kernel_bench backend=%s iters=%d (median)\n", gmt_rt_backend_name(), iters);
+  std::printf("# gmt_kernel_bench backend=%s iters=%d (%s)\n", gmt_rt_backend_name(), iters,
+              g_sustained ? "sustained mean" : "median");
 
   if (only.find("daxpy") != std::string::npos) {
     const size_t n = static_cast<size_t>(cli.geti("daxpy-n", 1LL << 28));
@@ -74,26 +92,27 @@ int main(int argc, char** argv) {
     report("rocblas", 0, shape, ms, 24.0 * n);
   }
   if (only.find("hot") != std::string::npos) {
-    // --only=hot: just the production (default) configuration of each hot
-    // kernel, `iters` launches each — the target of rocprofv3 --pmc passes
-    // (profiles/r02_pmc).  --hot-k=12,14 sweeps per pipelined pass,
-    // --jacobi-n=32768.
+    // --only=hot: just the production (default) configuration of the
+    // temporal-blocking kernel, `iters` launches each — the target of
+    // rocprofv3 --pmc passes (profiles/r02_pmc).  --hot-k=12,20 sweeps per
+    // pass, --jacobi-n=32768.
     const int64_t n = cli.geti("jacobi-n", 32768);
-    const std::string ks = cli.get("hot-k", "12,14");
-    for (int K = 2; K <= 16; K += 2) {
+    const std::string ks = cli.get("hot-k", "12,20");
+    for (int K = 1; K <= GMT_TB_MAX_SWEEPS; ++K) {
       if (("," + ks + ",").find("," + std::to_string(K) + ",") == std::string::npos) continue;
       const int64_t g = K, xk = ((g + 7) / 8) * 8;
-      const int64_t ld2 = ((xk + n + g + 63) / 64) * 64;
-      Buffer<double> a(static_cast<size_t>(ld2) * (n + 2 * g), GMT_SPACE_DEVICE), b(a.size(), GMT_SPACE_DEVICE);
-      GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, a.data(), ld2, s));
-      GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, b.data(), ld2, s));
+      const int64_t ld2 = ((xk + n + g + 63) / 64) * 64, rows = n + 2 * g;
+      Buffer<double> a(static_cast<size_t>(ld2) * rows, GMT_SPACE_DEVICE), b(a.size(), GMT_SPACE_DEVICE);
+      GMT_CHECK("fill", gmt_fill_poly(0, ld2, rows, 0.0, 1e-5, 0.0, 1e-5, a.data(), ld2, s));
+      GMT_CHECK("fill", gmt_fill_poly(0, ld2, rows, 0.0, 1e-5, 0.0, 1e-5, b.data(), ld2, s));
       const int64_t rect[4] = {xk, n, g, n};
+      gmt_tb_opts o{K, 0, 0, 0};
       const double ms = time_ms(s, iters, [&] {
-        GMT_CHECK("pipe", gmt_jacobi5xk(K, 1, rect, rect, 0, a.data(), b.data(), ld2, 0, s));
+        GMT_CHECK("tb", gmt_jacobi5tb(&o, 1, rect, rect, 0, a.data(), b.data(), ld2, rows, s));
       });
       char tag[64];
       std::snprintf(tag, sizeof(tag), "%lldx%lld x%d default", (long long)n, (long long)n, K);
-      report("jacobi5pipe", K, tag, ms, K * 16.0 * n * n);
+      report("jacobi5tb", K, tag, ms, K * 16.0 * n * n);
       std::printf("%-10s    %-22s %9.1f MLUPS\n", "", tag, K * double(n) * n / (ms * 1e-3) / 1e6);
     }
   }
@@ -122,7 +141,7 @@ int main(int argc, char** argv) {
       GMT_CHECK("fill", gmt_fill_poly(0, ld2, rows, 0.0, 1e-5, 0.0, 1e-5, a.data(), ld2, s));
       GMT_CHECK("fill", gmt_fill_poly(0, ld2, rows, 0.0, 1e-5, 0.0, 1e-5, b.data(), ld2, s));
       const int64_t rect[4] = {xk, n, g, n};
-      for (int nw : list("tb-nw", "4"))
+      for (int nw : list("tb-nw", "0"))
         for (int P : list("tb-p", "3"))
           for (int seg : list("tb-seg", "0")) {
             gmt_tb_opts o{K, nw, seg, 0};
@@ -145,9 +164,8 @@ int main(int argc, char** argv) {
     GMT_CHECK("fill", gmt_fill_poly(0, ld, n + 2, 0.0, 1e-5, 0.0, 1e-5, un.data(), ld, s));
     char shape[64];
     std::snprintf(shape, sizeof(shape), "%lldx%lld", (long long)n, (long long)n);
-    // --sections=v,xk,pipe (default all): single-sweep variants, LDS-tiled
-    // K-sweep kernel, register-pipelined K-sweep kernel
-    const std::string sec = cli.get("sections", "v,xk,pipe");
+    // single-sweep kernel variants (the K-sweep kernel: --only=tb)
+    const std::string sec = cli.get("sections", "v");
     for (int v = 1; v <= 9 && sec.find('v') != std::string::npos; ++v) {
       if (v == 3 && n > 16384) continue;  // scalar reference kernel: too slow to matter
       gmt_jacobi5_set_variant(v);
@@ -157,62 +175,6 @@ int main(int argc, char** argv) {
       report("jacobi5", v, shape, ms, 16.0 * n * n);
     }
     gmt_jacobi5_set_variant(0);
-    // temporal blocking: K sweeps per call; "GB/s" is the single-sweep
-    // equivalent (K x 16 B per point), i.e. directly comparable with v1-v9
-    for (int K = 2; K <= 4 && sec.find("xk") != std::string::npos; ++K) {
-      const int64_t g = K;
-      const int64_t ld2 = ((xo + n + g + 63) / 64) * 64;
-      Buffer<double> a(static_cast<size_t>(ld2) * (n + 2 * g), GMT_SPACE_DEVICE), b(a.size(), GMT_SPACE_DEVICE);
-      GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, a.data(), ld2, s));
-      GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, b.data(), ld2, s));
-      const int64_t rect[4] = {xo, n, g, n};
-      const int tiles[][2] = {{32, 16}, {32, 32}, {64, 8}, {64, 16}, {64, 24}, {64, 32}, {128, 8}};
-      for (auto& t : tiles) {
-        const int tile = (t[0] << 16) | t[1];
-        const double ms = time_ms(s, iters, [&] {
-          GMT_CHECK("xk", gmt_jacobi5xk(K, 1, rect, rect, 0, a.data(), b.data(), ld2, tile, s));
-        });
-        char tag[64];
-        std::snprintf(tag, sizeof(tag), "%s x%d %dx%d", shape, K, t[0], t[1]);
-        report("jacobi5xk", K, tag, ms, K * 16.0 * n * n);
-      }
-    }
-    // register-pipelined K-sweep kernel: rows per wave
-    for (int K = 2; K <= 14 && sec.find("pipe") != std::string::npos; K += 2) {
-      const int64_t g = K, xk = g > xo ? g : xo;  // the K-wide ring fits left of the interior
-      const int64_t ld2 = ((xk + n + g + 63) / 64) * 64;
-      Buffer<double> a(static_cast<size_t>(ld2) * (n + 2 * g), GMT_SPACE_DEVICE), b(a.size(), GMT_SPACE_DEVICE);
-      GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, a.data(), ld2, s));
-      GMT_CHECK("fill", gmt_fill_poly(0, ld2, n + 2 * g, 0.0, 1e-5, 0.0, 1e-5, b.data(), ld2, s));
-      const int64_t rect[4] = {xk, n, g, n};
-      // launch: 0 = rule bands split off (default), 1 = per-wave split over
-      // two launches, 2 = one kernel for both paths
-      static const char* lname[] = {"", " nosplit", " single"};
-      for (int launch : {0, 1, 2})
-      for (int order : {1, 2})
-        for (int seg : {64, 128, 256}) {
-          const int tile = GMT_XK_PIPE | (launch == 2 ? 1 << 21 : 0) | (launch == 1 ? 1 << 22 : 0) |
-                           (order << 19) | seg;
-          const double ms = time_ms(s, iters, [&] {
-            GMT_CHECK("pipe", gmt_jacobi5xk(K, 1, rect, rect, 0, a.data(), b.data(), ld2, tile, s));
-          });
-          char tag[64];
-          std::snprintf(tag, sizeof(tag), "%s x%d seg%d %s%s", shape, K, seg, order == 1 ? "skew" : "chain",
-                        lname[launch]);
-          report("jacobi5pipe", K, tag, ms, K * 16.0 * n * n);
-        }
-      // rows per rule-band wave (split launch, default level order)
-      for (int rr : {4, 8, 32})
-        for (int seg : {64, 128, 256}) {
-          const int tile = GMT_XK_PIPE | (rr << 23) | seg;
-          const double ms = time_ms(s, iters, [&] {
-            GMT_CHECK("pipe", gmt_jacobi5xk(K, 1, rect, rect, 0, a.data(), b.data(), ld2, tile, s));
-          });
-          char tag[64];
-          std::snprintf(tag, sizeof(tag), "%s x%d seg%d rule%d", shape, K, seg, rr);
-          report("jacobi5pipe", K, tag, ms, K * 16.0 * n * n);
-        }
-    }
   }
   if (only.find("stencil") != std::string::npos) {
     // the reference's default deriv shapes: 1028 x 524288 (dim 0), 524288 x 1028 (dim 1)

@@ -13,10 +13,11 @@
 //   --transport=auto|rccl|ipc|mpi-host|mpi-direct
 //   --overlap=auto          time overlapped and serial passes once, keep the faster
 //   --no-overlap --graph --periodic --warmup=W --variant=V (1 reg, 2 lds, 3 scalar, 9 pt)
-//   --tblock[=TY]           temporal blocking: 2 sweeps per pass and per exchange
-//                           (gmt_jacobi5x2; --tblock=TXxTY picks the tile, default 64x16)
-//   --tsteps=K              sweeps per fused pass with --tblock (2-14; default 2; 5 and 7
-//                           round down to the register-pipelined kernel's even counts)
+//   --tblock                temporal blocking (gmt_jacobi5tb): K sweeps per memory pass
+//                           and per (K-wide) halo exchange
+//   --tsteps=K              sweeps per fused pass with --tblock (2-24; default 2; odd
+//                           counts above 10 round down)
+//   --wg-strips=N --seg-rows=L   gmt_tb_opts launch shape (0 = default)
 //   --halo-iters=K          K blocking halo exchanges -> latency line
 //   --check                 rank 0 re-runs the whole problem serially on the host
 //   --json=FILE
@@ -104,15 +105,8 @@ int main(int argc, char** argv) {
   c.variant = static_cast<int>(cli.geti("variant", 0));
   c.tblock = cli.has("tblock") && cli.get("tblock", "1") != "0";
   if (c.tblock) c.tsteps = static_cast<int>(cli.geti("tsteps", 2));
-  if (c.tblock && cli.get("tblock", "1") != "1") {
-    int tx = 64, ty = 16;  // --tblock=TY (128-column tiles) or --tblock=TXxTY
-    const std::string v = cli.get("tblock", "16");
-    if (std::sscanf(v.c_str(), "%dx%d", &tx, &ty) != 2) {
-      tx = 128;
-      ty = std::atoi(v.c_str());
-    }
-    c.tile = (tx << 16) | ty;
-  }
+  c.wg_waves = static_cast<int>(cli.geti("wg-strips", 0));
+  c.seg_rows = static_cast<int>(cli.geti("seg-rows", 0));
   // with one rank and no periodic wrap there is nothing to exchange; with a
   // periodic wrap a single rank exchanges with itself
   comm::Kind kind = comm::parse_kind(cli.get("transport", "auto"));

@@ -74,7 +74,7 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
 
   ks_ = c.tsteps > 1 ? c.tsteps : (c.tblock ? 2 : 1);
   if (ks_ > GMT_TB_MAX_SWEEPS) ks_ = GMT_TB_MAX_SWEEPS;
-  if (ks_ > 4 && ks_ % 2) --ks_;  // 5..16 sweeps: gmt_jacobi5tb, even counts only
+  while (ks_ > 1 && !gmt_jacobi5tb_supported(ks_)) --ks_;  // odd counts above 10: the next even one
   // Scaled levels (4^p u_p) are bitwise equal to the exact form while
   // max|u| * 4^K stays finite (and no level value is subnormal).  The initial
   // field x^3 + y^2 on [-gh, 1 + gh]^2 is bounded by 2 + 3gh, and every
@@ -214,13 +214,9 @@ void JacobiSolver::xk_launch(int K, int n, const int64_t* rects, int parity, boo
   double* un = buf_[parity ^ 1].data();
   const int64_t dom[4] = {xo_, nx_, yo_, ny_};
   const int mask = halo_mask();
-  if (K % 2 == 0) {
-    // the frame bands are at most K wide or K tall: one-wave workgroups
-    gmt_tb_opts o{K, frame ? 1 : cfg_.wg_waves, cfg_.seg_rows, exact_ ? 1 : 0};
-    GMT_CHECK("jacobi tb", gmt_jacobi5tb(&o, n, rects, dom, mask, u, un, ld_, ny_ + 2 * g_, s_));
-  } else {
-    GMT_CHECK("jacobi xk", gmt_jacobi5xk(K, n, rects, dom, mask, u, un, ld_, cfg_.tile, s_));
-  }
+  // the frame bands are at most K wide or K tall: one-strip workgroups
+  gmt_tb_opts o{K, frame ? 1 : cfg_.wg_waves, cfg_.seg_rows, exact_ ? 1 : 0};
+  GMT_CHECK("jacobi tb", gmt_jacobi5tb(&o, n, rects, dom, mask, u, un, ld_, ny_ + 2 * g_, s_));
 }
 
 // ks_ sweeps u(t) -> u(t+ks) in one pass: the ks-wide halo (corners included)
@@ -231,12 +227,11 @@ void JacobiSolver::enqueue_block(int parity, int K) {
   Halo2D& h = *halo_[parity];
   const int64_t dom[4] = {xo_, nx_, yo_, ny_};
   const int mask = halo_mask();
-  const int64_t KA = (K + 1) & ~1;  // x offsets stay even (16-B loads)
   if (!h.active()) {
     xk_launch(K, 1, dom, parity, false);
     return;
   }
-  if (!cfg_.overlap || nx_ < 4 * KA + 2 || ny_ < 4 * K) {
+  if (!cfg_.overlap || nx_ < 4 * K + 2 || ny_ < 4 * K) {
     h.start(s_);
     h.finish(s_);
     xk_launch(K, 1, dom, parity, false);
@@ -245,11 +240,10 @@ void JacobiSolver::enqueue_block(int parity, int K) {
   // The core is inset only on the sides whose ghost ring is a neighbour's
   // halo (a Dirichlet side does not wait for the exchange; the kernel's rule
   // path handles it).  The frame — the K-wide bands along the halo sides —
-  // follows once the halo has landed.  The right band starts at an even
-  // column: KA or KA+1 columns wide.
+  // follows once the halo has landed.
   const bool hw = mask & 1, he = mask & 2, hs = mask & 4, hn = mask & 8;
-  const int64_t xr = (xo_ + nx_ - K) & ~int64_t(1);
-  const int64_t cx0 = hw ? xo_ + KA : xo_, cx1 = he ? xr : xo_ + nx_;
+  const int64_t xr = xo_ + nx_ - K;
+  const int64_t cx0 = hw ? xo_ + K : xo_, cx1 = he ? xr : xo_ + nx_;
   const int64_t cy0 = hs ? yo_ + K : yo_, cy1 = hn ? yo_ + ny_ - K : yo_ + ny_;
   const int64_t core[4] = {cx0, cx1 - cx0, cy0, cy1 - cy0};
   GMT_CHECK("event", gmt_rt_event_record(ev_start_, s_));
@@ -274,8 +268,8 @@ void JacobiSolver::enqueue_block(int parity, int K) {
   };
   if (hs) add(xo_, nx_, yo_, K);
   if (hn) add(xo_, nx_, yo_ + ny_ - K, K);
-  if (hw) add(xo_, KA, cy0, cy1 - cy0);
-  if (he) add(xr, xo_ + nx_ - xr, cy0, cy1 - cy0);
+  if (hw) add(xo_, K, cy0, cy1 - cy0);
+  if (he) add(xr, K, cy0, cy1 - cy0);
   xk_launch(K, nf, frame, parity, true);
 }
 
@@ -288,21 +282,23 @@ void JacobiSolver::step_block() {
 }
 
 // Measured cost of one fused pass of K sweeps (ms; gmt_kernel_bench
-// --only=tb with the default launch, MI355X, profiles/r02_tb.md) on two
-// domain sizes: the pass is HBM-bound up to K ~ 10 (the strip access
-// pattern's ~5.2 TB/s: about the same time for every K) and VALU-bound
-// beyond, and where that turns depends on the domain (strip count, rule
-// waves, launch tail).  K = 1 is the single-sweep kernel, K = 3 the
-// LDS-tiled one; 0 = no kernel for that K (odd K > 3).
+// --only=tb --sustained=1: back-to-back launches with the default launch
+// shape, MI355X, profiles/r02_tb4.md) on two domain sizes.  One-wave strips
+// (K <= 10) run near the HBM floor (~3.8-4.1 ms at 32768^2); two-stage strips
+// (K >= 12) are VALU bound from K ~ 14.  K = 1 is the single-sweep kernel;
+// 0 = no kernel for that K (odd K > 10).
 namespace {
 struct PassCosts {
   double points;  // lattice points of the measured domain
   double ms[GMT_TB_MAX_SWEEPS + 1];
 };
-constexpr PassCosts kCostLarge = {32768.0 * 32768.0, {0, 3.05, 3.62, 4.5, 3.43, 0, 3.51, 0, 3.46, 0, 3.74, 0,
-                                                      3.58, 0, 4.08, 0, 4.64}};
-constexpr PassCosts kCostSmall = {8192.0 * 8192.0, {0, 0.20, 0.225, 0.30, 0.219, 0, 0.236, 0, 0.235, 0, 0.261,
-                                                    0, 0.295, 0, 0.346, 0, 0.445}};
+constexpr PassCosts kCostLarge = {32768.0 * 32768.0,
+                                  {0,    3.05, 3.94, 4.23, 4.03, 4.07, 4.13, 4.40, 3.88, 4.10, 3.81, 0,    3.55,
+                                   0,    3.98, 0,    4.39, 0,    4.93, 0,    5.59, 0,    6.37, 0,    6.97}};
+constexpr PassCosts kCostSmall = {8192.0 * 8192.0,
+                                  {0,     0.20,  0.268, 0.283, 0.267, 0.275, 0.275, 0.286, 0.274,
+                                   0.284, 0.279, 0,     0.270, 0,     0.300, 0,     0.368, 0,
+                                   0.408, 0,     0.502, 0,     0.579, 0,     0.644}};
 constexpr double kLaunchMs = 0.015;    // host launch + dispatch per pass
 constexpr double kExchangeMs = 0.035;  // a halo exchange not hidden by the overlap
 }  // namespace

@@ -190,37 +190,20 @@ static int host_xk(int K, int n_rect, const int64_t* rects, const int64_t* dom, 
   return 0;
 }
 
-int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom, int mask,
-                  const double* u, double* un, int64_t ld, int tile, void*) {
-  if (n_rect < 0 || n_rect > 4 || nsweeps < 2 || nsweeps > 14) return 1;
-  if (nsweeps > 4 && nsweeps % 2) return 1;  // same support matrix as the HIP build
-  (void)tile;
-  return host_xk(nsweeps, n_rect, rects, dom, mask, u, un, ld);
-}
+int gmt_jacobi5tb_supported(int K) { return (K >= 1 && K <= 10) || (K > 10 && K <= GMT_TB_MAX_SWEEPS && K % 2 == 0); }
 
 // CPU backend of csrc/kernels/jacobi5tb.hip: same argument checks, reference loops
 int gmt_jacobi5tb(const gmt_tb_opts* o, int n_rect, const int64_t* rects, const int64_t* dom, int mask,
                   const double* u, double* un, int64_t ld, int64_t nrows, void*) {
   const int K = o ? o->sweeps : 0;
-  if (K < 2 || K > GMT_TB_MAX_SWEEPS || K % 2 || n_rect < 0 || n_rect > 8 || ld <= 0 || ld % 2) return 1;
+  if (!gmt_jacobi5tb_supported(K) || n_rect < 0 || n_rect > 8 || ld <= 0) return 1;
   if (o->wg_waves < 0 || o->wg_waves > 8 || o->seg_rows < 0) return 1;
   for (int k = 0; k < n_rect; ++k) {
     const int64_t* r = rects + 4 * k;
     if (r[1] <= 0 || r[3] <= 0) continue;
-    if (r[0] % 2 || r[0] < K || r[2] < K || r[0] + r[1] > ld || r[2] + r[3] + K > nrows) return 1;
+    if (r[0] < K || r[2] < K || r[0] + r[1] + K > ld || r[2] + r[3] + K > nrows) return 1;
   }
   return host_xk(K, n_rect, rects, dom, mask, u, un, ld);
-}
-
-int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int mask, const double* u,
-                  double* un, int64_t ld, int tile, void* stream) {
-  return gmt_jacobi5xk(2, n_rect, rects, dom, mask, u, un, ld, tile, stream);
-}
-
-int gmt_jacobi5xk_pipe(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom, int mask,
-                       const double* u, double* un, int64_t ld, int, void* stream) {
-  if (nsweeps % 2) return 1;
-  return gmt_jacobi5xk(nsweeps, n_rect, rects, dom, mask, u, un, ld, 0, stream);
 }
 
 void gmt_jacobi5_set_variant(int v) { g_variant = v; }

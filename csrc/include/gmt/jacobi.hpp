@@ -19,8 +19,7 @@
 //
 //   * tblock: K = tsteps sweeps per kernel and per exchange (temporal
 //     blocking): u(t) is read once and u(t+K) written once (gmt_jacobi5tb,
-//     csrc/kernels/jacobi5tb.hip, for even K; the LDS-tiled gmt_jacobi5xk
-//     for K = 3), the halo is K wide and exchanged once per pass with its
+//     csrc/kernels/jacobi5tb.hip), the halo is K wide and exchanged once per pass with its
 //     corners (one-phase exchange) — bitwise the same result as K single
 //     sweeps.
 // Storage is column-major (x contiguous) with the interior origin at x = 8
@@ -50,15 +49,14 @@ struct JacobiConfig {
   bool overlap_auto = false;
   bool graph = false;
   int variant = 0;                               // gmt_jacobi5_set_variant
-  // temporal blocking: tsteps (2-16) sweeps per memory pass (even counts:
-  // gmt_jacobi5tb; 3: the LDS-tiled gmt_jacobi5xk; other odd counts round
-  // down) and per halo exchange (ghost width tsteps, corners in the same
+  // temporal blocking: tsteps (2-24) sweeps per memory pass (gmt_jacobi5tb;
+  // odd counts above 10 round down) and per halo exchange (ghost width
+  // tsteps, corners in the same
   // exchange phase) — 1/tsteps of the HBM bytes and messages per lattice
   // update.  1 = off.  tblock = true with tsteps = 0 is tsteps = 2.
   bool tblock = false;
   int tsteps = 0;
-  int tile = 0;                                  // gmt_jacobi5x2 tile ((TX<<16)|TY, 0 = default; K = 3 only)
-  int wg_waves = 0;                              // gmt_tb_opts.wg_waves (0 = auto)
+  int wg_waves = 0;                              // gmt_tb_opts.wg_waves: strips per workgroup (0 = auto)
   int seg_rows = 0;                              // gmt_tb_opts.seg_rows (0 = auto)
   // -1 / 0: power-of-two scaled levels when max|u| * 4^K stays finite (the
   // initial field bounds every later one: Jacobi averages), 1: always exact
@@ -110,7 +108,7 @@ class JacobiSolver {
  private:
   void enqueue_step(int parity);
   void enqueue_block(int parity, int k);  // k <= ks_ fused sweeps
-  // one fused k-sweep launch on `n` output rects (gmt_jacobi5tb / gmt_jacobi5xk)
+  // one fused k-sweep launch on `n` output rects (gmt_jacobi5tb)
   void xk_launch(int k, int n, const int64_t* rects, int parity, bool frame);
   void step_block();
   void sweep_full(int parity, double* resid);

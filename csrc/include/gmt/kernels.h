@@ -103,56 +103,31 @@ int gmt_jacobi5(int64_t x0, int64_t nx, int64_t y0, int64_t ny, const double* u,
 int gmt_jacobi5_rects(int n_rect, const int64_t* rects, const double* u, double* un,
                       int64_t ld, const double* f, int64_t ldf, double c0, double c1,
                       void* stream);
-/* Two fused Jacobi sweeps (temporal blocking, Laplace form c0 = 1/4):
- * un = J(J(u)) on up to 4 output rects {x0, nx, y0, ny} (absolute array
- * coordinates, x0 even) in one launch.  dom = the rank's interior
- * {x0, nx, y0, ny}.  halo_mask bit0/1/2/3 = west/east/south/north ghost cells
- * belong to a neighbour (they get the intermediate update); a clear bit means
- * a fixed Dirichlet ghost.  u must be valid on each rect + 2 cells.
- * tile: (TX << 16) | TY output tile per workgroup (32x16/32, 64x4..32,
- * 128x4..32, 256x4..8); a plain row count means 128 columns; 0 = default
- * (64 x 16, the measured best). */
-int gmt_jacobi5x2(int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
-                  const double* u, double* un, int64_t ld, int tile, void* stream);
-/* The same for nsweeps = 2..8 fused sweeps (u valid on rect + nsweeps;
- * ghost width >= nsweeps).  gmt_jacobi5x2 == gmt_jacobi5xk(2, ...).
- * Two kernels: the register-pipelined one (jacobi5pipe.hip, even nsweeps;
- * tile = GMT_XK_PIPE | (pipe << 19) | rows-per-wave, pipe 0 = default, 1 =
- * skewed, 2 = chained level order; or tile = 0 with an even nsweeps) and
- * the LDS-tiled one (jacobi5x2.hip, nsweeps 2..4; tile = (TX << 16) | TY,
- * or tile = 0 with nsweeps = 3). */
-#define GMT_XK_PIPE 0x40000000
-/* With GMT_XK_PIPE: the caller allows interior cells outside the rects to be
- * rewritten with their own K-sweep values (e.g. a frame pass after the core
- * pass), so rects narrower than a 128 - 2K column strip still take the
- * branch-free path. */
-#define GMT_XK_EXT 0x20000000
-
 /* ---- Temporal-blocking Jacobi (csrc/kernels/jacobi5tb.hip): `sweeps` fused
- *      Laplace sweeps per memory pass on up to 8 output rects {x0, nx, y0, ny}
- *      (absolute, x0 even, x0 >= sweeps, y0 >= sweeps, y0+ny+sweeps <= nrows).
- *      Cells of the interior `dom` outside the rects are never written.
- *      halo_mask as for gmt_jacobi5x2. */
-#define GMT_TB_MAX_SWEEPS 16
+ *      Laplace sweeps per memory pass, un = J^sweeps(u), on up to 8 output
+ *      rects {x0, nx, y0, ny} (absolute array coordinates, x0 >= sweeps,
+ *      y0 >= sweeps, x0+nx+sweeps <= ld, y0+ny+sweeps <= nrows; u must hold
+ *      each rect plus its sweeps-wide ring).  `dom` = the rank's interior
+ *      {x0, nx, y0, ny}.  halo_mask bit0/1/2/3 = west/east/south/north ghost
+ *      cells belong to a neighbour (they get the intermediate updates); a
+ *      clear bit means a fixed Dirichlet ghost.  Cells of `un` outside the
+ *      rects are never written.  Sweep counts: 1..10 (one wave per strip)
+ *      and even 12..GMT_TB_MAX_SWEEPS (two waves per strip, levels split);
+ *      gmt_jacobi5tb_supported() says which. */
+#define GMT_TB_MAX_SWEEPS 24
 typedef struct gmt_tb_opts {
-  int sweeps;   /* K: even, 2..GMT_TB_MAX_SWEEPS */
-  int wg_waves; /* independent 128-column waves per workgroup, 1..8 (0 = 4) */
-  int seg_rows; /* output rows per wave (0 = default: 192-384 by K, fewer for small domains) */
+  int sweeps;   /* K, see gmt_jacobi5tb_supported */
+  int wg_waves; /* 192-column strips per workgroup, 1..8 (0 = default; at
+                   most 4 when K > 10) */
+  int seg_rows; /* output rows per strip (0 = default: 192-384 by K, fewer
+                   for small domains) */
   int exact;    /* 1: multiply by 1/4 per level (bitwise for any magnitude);
                    0: power-of-two scaled levels (bitwise unless a value is
                    subnormal or |u| * 4^K overflows) */
 } gmt_tb_opts;
+int gmt_jacobi5tb_supported(int sweeps);
 int gmt_jacobi5tb(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, const int64_t* dom,
                   int halo_mask, const double* u, double* un, int64_t ld, int64_t nrows, void* stream);
-int gmt_jacobi5xk(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
-                  const double* u, double* un, int64_t ld, int tile, void* stream);
-/* Register-pipelined K-sweep kernel: one wave per 128-column strip and
- * `seg & 0xffff` output rows (0 = auto: 256, fewer for small rects),
- * `(seg >> 19) & 3` = level order (0 default, 1 skewed, 2 chained);
- * nsweeps even, 2..8. */
-int gmt_jacobi5xk_pipe(int nsweeps, int n_rect, const int64_t* rects, const int64_t* dom,
-                       int halo_mask, const double* u, double* un, int64_t ld, int seg,
-                       void* stream);
 
 /* Kernel variant selection for A/B measurement: 0 = auto, 1 = register
  * sliding window (vector x2, W/E from L1), 2 = LDS-tiled, 3 = scalar

@@ -1,45 +1,50 @@
 // K fused 5-point Jacobi sweeps per memory pass (temporal blocking), gfx950.
 //
-// One wave owns a 128-column strip (2 columns per lane) and walks down a
-// segment of L output rows.  Time level p of row r needs level p-1 of rows
-// r-1, r, r+1, which the wave computed in its three previous steps (skewed
-// pipeline: at step s level p is computed for row s - 2p, so the K levels of
-// a step are independent of each other):
-//   step s:  level p = K..1 of row s-2p (level K is stored: 16-B buffer
-//            store); issue the buffer->LDS DMA of input row s+P into the
-//            ring slot that level 1 just released.
+// One strip = 192 columns, 3 per lane, walked down a segment of L output
+// rows.  Time level p of row r needs level p-1 of rows r-1, r, r+1, which
+// were computed in the three previous steps (skewed pipeline: at step s
+// level p is computed for row s - 2p, so the levels of a step are
+// independent of each other):
+//   step s:  level p = K..1 of row s-2p (level K is stored); issue the
+//            buffer->LDS DMA of input row s+P into the ring slot that
+//            level 1 just released.
 // West/east neighbours come from the adjacent lane through DPP (wave_shr /
 // wave_shl); the strip edges lose one column per level, so a strip yields
-// 128 - 2K output columns.  A workgroup is nw independent waves on adjacent
-// strips (no barrier): their 2K overlap columns are re-read from the CU's L1.
+// 192 - 2 KL output columns (KL = K rounded up to a multiple of 3, so both
+// output edges fall on a lane boundary).
 //
-// Memory pipeline: level-0 rows are DMA'd into a per-wave LDS ring of P+3
-// slots (rows s-3..s-1 in use, P in flight) and read back by ds_read_b128
-// when level 1 needs them: no loaded VGPR crosses the loop back edge, so
-// the loop keeps P rows in flight (the round-1 register-prefetch kernel,
-// jacobi5pipe.hip, copied its prefetched registers at the back edge and
-// waited vmcnt(1) every 3 steps: 44% SQ_WAIT_ANY, profiles/r02_pmc/).
-// One loop-invariant buffer descriptor per direction; the row is in the VGPR
-// offset and the buffer range check drops every row outside the segment.
-// Every step issues exactly one DMA and two stores — no branch around a
-// memory instruction — so the explicit s_waitcnt vmcnt(3P+2) before the
-// ring reads is exact.
+// Why 3 columns per lane (round 2, profiles/r02_tb.md): the kernel is VALU
+// issue bound from K ~ 10 and a DPP move costs as much as a DADD.  Per level
+// a lane issues 4 DPP moves (one double from each neighbour) and 3 DADD per
+// column: 10 instructions per 2 columns with 128-column strips, 13 per 3
+// columns here, and the recomputed strip overlap 2K/128 drops to 2K/192.
+//
+// Level split across waves (K > kMaxK1): the 3-slot register pipeline needs
+// 18 VGPRs per level, so one wave holds at most kMaxK1 levels at 2 waves per
+// SIMD.  Larger K runs as 2 stages per strip: stage 0 computes levels
+// 1..KA from the DMA ring and writes level KA to an LDS hand-off ring,
+// stage 1 reads it there as its level 0 and computes KA+1..K; one
+// s_barrier per step publishes the hand-off row.  This lets a single memory
+// pass fuse up to GMT_TB_MAX_SWEEPS sweeps, which is what a 20-step run
+// needs to stay under the two-pass memory floor (2 x 3.3 ms at 32768^2).
+//
+// Memory pipeline: level-0 rows are DMA'd into a per-strip LDS ring of P+3
+// slots (two dwordx4 DMAs per row) and read back when level 1 needs
+// them: no loaded VGPR crosses the loop back edge.  The compiler does not
+// track LDS-DMA -> ds_read dependencies, so the wait is an explicit
+// s_waitcnt vmcnt; every step issues the same memory instructions — no
+// branch around any of them — so the count is exact.  One loop-invariant
+// buffer descriptor per direction; the row is in the VGPR offset and the
+// buffer range check drops (stores) or zero-fills (loads) every row
+// outside the segment.
 //
 // Arithmetic: scaled levels V_p = 4^p u_p, V_p = (W + E) + (N + S), output
 // V_K * 4^-K: bitwise equal to K single sweeps u' = 0.25((W+E)+(N+S))
 // unless a level value is subnormal or 4^K |u| overflows; EXACT keeps the
 // 0.25 multiply per level (used by the engine when max|u| is too large).
 // Dirichlet sides (halo_mask bit clear): ring cells keep their value at every
-// level (RULE path, per-lane column masks + a per-row scalar test, chosen
-// per wave); on halo sides the K-wide ghost ring is updated as data.
-//
-// Measured limits (csrc/bench/valu_rate.hip, profiles/r02_tb.md): a level
-// (4 v_mov_b32_dpp + 6 v_add_f64 per 128 cells) issues at ~19.5 ns per SIMD
-// at 2 waves/SIMD — DPP moves cost as much as a DADD — so the kernel is
-// VALU-issue bound once K >= 12.  Sharing the strip edges between the waves
-// of a workgroup through LDS (no recomputed overlap) was built and measured:
-// the K exec-masked ds_write per step made it LDS-issue bound (2.0-2.4M vs
-// 3.4-3.8M MLUPS), with or without the per-step barrier; removed.
+// level (RULE path, per-lane column masks + a per-row test, chosen per
+// wave); on halo sides the K-wide ghost ring is updated as data.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -52,26 +57,46 @@ namespace gmt {
 namespace tb {
 
 constexpr int kMaxRect = 8;
-constexpr int kMaxWaves = 8;
-constexpr int kCols = 2 * kWave;  // columns per wave
-constexpr uint32_t kDrop = 0x80000000u;  // buffer offset past num_records: no-op access
+constexpr int kMaxThreads = 512;              // 8 waves: 2 per SIMD
+constexpr int kNC = 3;                        // columns per lane
+constexpr int kCols = kNC * kWave;            // 192 columns per strip
+constexpr uint32_t kRowBytes = kCols * 8;     // one row of a strip (hand-off slot)
+// DMA ring slot: a row is two 16-B-per-lane DMAs (1024 + 512 B; the second
+// one's upper 32 lanes are out of range and land zeros past the row).  A
+// 12-B DMA would fit one row in two full-wave DMAs, but gfx950 writes it to
+// LDS at a 16-B lane stride (measured), not 12.
+constexpr uint32_t kSlotBytes = 2048;
+constexpr uint32_t kDrop = 0x80000000u;       // buffer offset past num_records: no-op access
+constexpr int kP = 3;                         // input rows in flight
+constexpr int kRS = kP + 3;                   // DMA ring: rows s-3..s-1 in use, s..s+P-1 in flight
+constexpr int kHS = 6;                        // hand-off ring (2 stages)
+constexpr int kU = 6;                         // unroll = lcm(3, kRS, kHS): ring slots are static offsets
+constexpr int kMaxK1 = 10;                    // largest single-wave K (18 VGPRs per level)
+static_assert(kU % 3 == 0 && kU % kRS == 0 && kU % kHS == 0, "unroll");
+
+constexpr int ring_left(int K) { return (K + 2) / 3 * 3; }
+constexpr int strip_out(int K) { return kCols - 2 * ring_left(K); }
+constexpr int n_stages(int K) { return K <= kMaxK1 ? 1 : 2; }
+constexpr int stage0_levels(int K) { return (K + 1) / 2; }
 
 struct Args {
-  int64_t r[kMaxRect][4];        // output rects: x0, nx, y0, ny (absolute; x0 even)
-  int64_t nstrip[kMaxRect];      // workgroup strips per rect
+  int64_t r[kMaxRect][4];        // output rects: x0, nx, y0, ny (absolute)
+  int64_t nstrip[kMaxRect];      // strips per rect
   int64_t tstart[kMaxRect + 1];  // prefix sum of workgroups
   int64_t dom[4];                // interior x0, nx, y0, ny
-  int64_t ld;                    // row pitch (elements, even)
+  int64_t ld;                    // row pitch (elements)
   int64_t last_row;              // last allocated row (load clamp)
   int n;                         // rects
   int mask;                      // halo sides: bit0..3 = W/E/S/N
-  int nw;                        // waves per workgroup
-  int seg;                       // output rows per workgroup segment
+  int nw;                        // strips per workgroup
+  int seg;                       // output rows per segment
   int nsteps;                    // steps per segment, padded to the unroll
   double quarter;                // 0.25 (EXACT): an SGPR operand
 };
 
-constexpr int lcm3(int n) { return n % 3 == 0 ? n : 3 * n; }
+struct d3 {
+  double x, y, z;
+};
 
 template <int I, int N, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -89,10 +114,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double* p, uint
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(p), 0, bytes, 0x00020000);
 }
 
-// Per-wave LDS (dynamic, sized by the launch): the level-0 row ring,
-// ring[w][slot][lane], filled by buffer->LDS DMA.
-__host__ __device__ constexpr int64_t lds_bytes(int nw, int P) {
-  return static_cast<int64_t>(nw) * (P + 3) * kWave * 16;
+// LDS per strip: the DMA ring, plus the hand-off ring with 2 stages
+__host__ __device__ constexpr int64_t strip_lds(int stages) {
+  return static_cast<int64_t>(kRS) * kSlotBytes + (stages > 1 ? kHS * kRowBytes : 0);
 }
 
 // s_waitcnt vmcnt(n) only (expcnt / lgkmcnt left at their maxima), as a
@@ -104,15 +128,32 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// One wave: a 128-column strip (output columns [xs, xe)) and the output rows
-// [ys, ye).  Skewed pipeline: at step s level p is computed for row
-// yl + s - 2p (yl = ys - K), from level p-1 of the three previous steps.
-template <int K, int P, bool EXACT, bool ODD, bool RULE>
-__device__ __forceinline__ void run_strip(const Args& a, const double* __restrict__ u, double* __restrict__ un,
-                                          d2 (*ring)[kWave], int lane, int64_t xs, int64_t xe, int64_t ys,
+// hand-off rows written by this wave are visible to the workgroup after it.
+// Outstanding DMAs and stores are not waited for (gfx950 has the back-off
+// barrier, so s_barrier needs no vmcnt(0)).
+__device__ __forceinline__ void step_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ d3 lds_row(const char* slot, int lane) {
+  const double* p = reinterpret_cast<const double*>(slot) + kNC * lane;
+  return d3{p[0], p[1], p[2]};
+}
+
+// One wave = one stage of one strip: levels PB..PE of the K-level pipeline.
+// PB == 1: level 0 comes from the DMA ring; otherwise from the hand-off ring
+// (rows written by stage 0 in the three previous steps).  PE == K: level K
+// is stored to `un`; otherwise level PE goes to the hand-off ring.  Strip
+// output columns [xs, xe), rows [ys, ye).
+template <int K, int PB, int PE, bool EXACT, bool EDGE, bool RULE, bool SYNC>
+__device__ __forceinline__ void run_stage(const Args& a, const double* __restrict__ u, double* __restrict__ un,
+                                          char* ring, char* hand, int lane, int64_t xs, int64_t xe, int64_t ys,
                                           int64_t ye) {
-  constexpr int RS = P + 3;    // level-0 ring: rows s-3..s-1 in use, s..s+P-1 in flight
-  constexpr int U = lcm3(RS);  // unroll: ring slots are static offsets
+  constexpr bool kIn = PB == 1;
+  constexpr bool kOut = PE == K;
+  constexpr int SPS = kOut ? (EDGE ? 3 : 2) : 0;  // global stores per step
+  constexpr int DPS = kIn ? 2 : 0;                // DMAs per step
+  // input rows are read at level min(PB + 2, PE) of the top-down order: the
+  // later, the longer the DMA has had to land
+  constexpr int RL = PB + 2 < PE ? PB + 2 : PE;
   // every kernel argument the loop needs, as values: the asm memory clobbers
   // below would otherwise force a reload of the kernarg segment per use
   const int64_t ld = a.ld;
@@ -120,42 +161,50 @@ __device__ __forceinline__ void run_strip(const Args& a, const double* __restric
   const double quarter = a.quarter;
   const int64_t dx0 = a.dom[0], dx1 = a.dom[0] + a.dom[1];
   const int64_t dy0 = a.dom[2], dy1 = a.dom[2] + a.dom[3];
-  const int64_t c0 = xs - K + 2 * lane;  // this lane: columns c0, c0+1
+  const int64_t cf = xs - ring_left(K);  // first column of the strip window
+  const int64_t c0 = cf + kNC * lane;    // this lane: columns c0 .. c0+2
   const int64_t yl = ys - K;             // row of step 0
   const int L = static_cast<int>(ye - ys);
   const uint32_t ld8 = static_cast<uint32_t>(ld) * 8u;
 
-  // One loop-invariant descriptor per direction; the row lives in the VGPR
-  // offset, so the buffer range check drops (stores) or zero-fills (loads)
-  // every row outside the segment — no per-step scalar address math.
-  //  loads: rows [yl, min(yl + L + 2K, last_row + 1)); lane column c0 (a
-  //  column past the row end reads the next row: garbage outside every cone)
+  //  loads: rows [yl, min(yl + L + 2K, last_row + 1)), 1536 contiguous bytes
+  //  from column cf (a column outside the row wraps into the neighbouring
+  //  row or is zero-filled: garbage outside every output cone)
   const int64_t nrow_in = std::min<int64_t>(L + 2 * K, a.last_row + 1 - yl);
   const __amdgpu_buffer_rsrc_t lrs = row_rsrc(u + yl * ld, static_cast<uint32_t>(nrow_in) * ld8);
-  const uint32_t loff = static_cast<uint32_t>(c0) * 8u;
-  //  stores: rows [ys, ye) from column xs; a 16-B store for lanes with both
-  //  columns in [xs, xe), with ODD (a rect of the launch ends at an odd
-  //  column) also an 8-B store for the single lane at that edge; every other
-  //  lane is offset by 2^31 (out of range for any row).  The 8-B store is not
-  //  issued without ODD: dropped by every lane it still costs a TA slot, and
-  //  the memory-bound passes (K <= 8) are VMEM-issue bound (93% of wave
-  //  cycles in SQ_WAIT_INST_ANY, profiles/r02_pmc/).
-  const __amdgpu_buffer_rsrc_t srs = row_rsrc(un + ys * ld + xs, static_cast<uint32_t>(L) * ld8);
-  const bool in0 = c0 >= xs && c0 < xe, in1 = c0 + 1 >= xs && c0 + 1 < xe;
-  const uint32_t st16 = (in0 && in1) ? static_cast<uint32_t>(c0 - xs) * 8u : kDrop;
-  const uint32_t st8 = (in0 && !in1) ? static_cast<uint32_t>(c0 - xs) * 8u : kDrop;
-  auto store_step = [&](int s, d2 v) {  // level K of step s = output row ys + s - 3K
-    const uint32_t ro = static_cast<uint32_t>(s - 3 * K) * ld8;  // wraps for warm-up rows: out of range
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), srs, st16 + ro, 0, 2 /* nt */);
-    if constexpr (ODD) {
-      const u2 lo = {static_cast<unsigned>(__double2loint(v.x)), static_cast<unsigned>(__double2hiint(v.x))};
-      __builtin_amdgcn_raw_buffer_store_b64(lo, srs, st8 + ro, 0, 2);
+  const uint32_t loff = static_cast<uint32_t>(cf) * 8u + static_cast<uint32_t>(lane) * 16u;
+  const uint32_t loff2 = lane < kWave / 2 ? loff + 1024u : kDrop;
+  auto dma = [&](int s, int slot) {
+    if constexpr (kIn) {
+      char* dst = ring + slot * kSlotBytes;
+      const uint32_t o = static_cast<uint32_t>(s) * ld8;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst, 16, loff + o, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + 1024, 16, loff2 + o, 0, 0, 0);
     }
   };
-  constexpr int SPS = ODD ? 2 : 1;  // stores per step
-  auto dma = [&](int s, int slot) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, &ring[slot][0], 16, loff + static_cast<uint32_t>(s) * ld8, 0, 0,
-                                             0);
+  //  stores: rows [ys, ye) from column xs.  The left output edge is a lane
+  //  boundary (KL = 0 mod 3): a 16-B store of columns 0-1 where both are
+  //  inside, an 8-B store of column 2, and (EDGE: a rect of the launch has a
+  //  right edge inside a lane) an 8-B store of column 0 alone.  Lanes with
+  //  nothing to store get an offset past any row (dropped).
+  const __amdgpu_buffer_rsrc_t srs = row_rsrc(un + ys * ld + xs, static_cast<uint32_t>(L) * ld8);
+  const bool in0 = c0 >= xs && c0 < xe, in1 = c0 + 1 >= xs && c0 + 1 < xe, in2 = c0 + 2 >= xs && c0 + 2 < xe;
+  const uint32_t sta = (in0 && in1) ? static_cast<uint32_t>(c0 - xs) * 8u : kDrop;
+  const uint32_t stb = in2 ? static_cast<uint32_t>(c0 + 2 - xs) * 8u : kDrop;
+  const uint32_t stc = (in0 && !in1) ? static_cast<uint32_t>(c0 - xs) * 8u : kDrop;
+  auto store_step = [&](int s, const d3& v) {  // level K of step s = output row ys + s - 3K
+    if constexpr (kOut) {
+      const uint32_t ro = static_cast<uint32_t>(s - 3 * K) * ld8;  // wraps for warm-up rows: out of range
+      const u4 xy = {static_cast<unsigned>(__double2loint(v.x)), static_cast<unsigned>(__double2hiint(v.x)),
+                     static_cast<unsigned>(__double2loint(v.y)), static_cast<unsigned>(__double2hiint(v.y))};
+      const u2 z = {static_cast<unsigned>(__double2loint(v.z)), static_cast<unsigned>(__double2hiint(v.z))};
+      __builtin_amdgcn_raw_buffer_store_b128(xy, srs, sta + ro, 0, 2 /* nt */);
+      __builtin_amdgcn_raw_buffer_store_b64(z, srs, stb + ro, 0, 2);
+      if constexpr (EDGE) {
+        const u2 x = {static_cast<unsigned>(__double2loint(v.x)), static_cast<unsigned>(__double2hiint(v.x))};
+        __builtin_amdgcn_raw_buffer_store_b64(x, srs, stc + ro, 0, 2);
+      }
+    }
   };
 
   // Dirichlet rule (RULE only): a cell outside the interior on a side whose
@@ -163,98 +212,122 @@ __device__ __forceinline__ void run_strip(const Args& a, const double* __restric
   const bool gw = mask & 1, ge = mask & 2, gs = mask & 4, gn = mask & 8;
   const bool kx0 = (c0 < dx0 && !gw) || (c0 >= dx1 && !ge);
   const bool kx1 = (c0 + 1 < dx0 && !gw) || (c0 + 1 >= dx1 && !ge);
+  const bool kx2 = (c0 + 2 < dx0 && !gw) || (c0 + 2 >= dx1 && !ge);
 
-  auto level = [&](const d2& up_, const d2& c, const d2& dn, int64_t row) -> d2 {
+  auto level = [&](const d3& up_, const d3& c, const d3& dn, int64_t row) -> d3 {
 #pragma clang fp contract(off)
-    const double w = dpp_from_lower(c.y), e = dpp_from_upper(c.x);
-    d2 v;
+    const double w = dpp_from_lower(c.z), e = dpp_from_upper(c.x);
+    d3 v;
     if constexpr (EXACT) {
       v.x = quarter * ((w + c.y) + (up_.x + dn.x));
-      v.y = quarter * ((c.x + e) + (up_.y + dn.y));
+      v.y = quarter * ((c.x + c.z) + (up_.y + dn.y));
+      v.z = quarter * ((c.y + e) + (up_.z + dn.z));
     } else {
       v.x = (w + c.y) + (up_.x + dn.x);
-      v.y = (c.x + e) + (up_.y + dn.y);
+      v.y = (c.x + c.z) + (up_.y + dn.y);
+      v.z = (c.y + e) + (up_.z + dn.z);
     }
     if constexpr (RULE) {
       const bool rk = (row < dy0 && !gs) || (row >= dy1 && !gn);
       const double f = EXACT ? 1.0 : 4.0;  // a kept cell: V_p = 4 V_{p-1}
       v.x = (rk || kx0) ? c.x * f : v.x;
       v.y = (rk || kx1) ? c.y * f : v.y;
+      v.z = (rk || kx2) ? c.z * f : v.z;
     }
     return v;
   };
 
-  d2 W[K][3];  // W[p][slot], p = 1..K-1 (level 0 is the LDS ring)
+  constexpr int NL = PE - PB + 1;
+  d3 W[NL][3];  // W[p - PB][slot]: levels PB..PE-1 (PE is stored or handed off)
 #pragma unroll
-  for (int p = 0; p < K; ++p)
+  for (int p = 0; p < NL; ++p)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) W[p][j] = d2{0.0, 0.0};
+    for (int j = 0; j < 3; ++j) W[p][j] = d3{0.0, 0.0, 0.0};
 
-  // prologue: rows 0..P-1 in flight, each preceded by the (dropped) stores
-  // a steady-state step issues, so every wait below counts the same
-  // (SPS + 1) P + SPS younger memory operations (SPS stores + 1 DMA per step)
-  static_for<0, P>([&](auto I) {
-    store_step(0, d2{0.0, 0.0});  // row ys - 3K: out of range
-    dma(decltype(I)::value, decltype(I)::value);
-  });
+  // prologue: rows 0..P-1 in flight, each preceded by the (dropped) stores a
+  // steady-state step issues, so every wait below counts the same
+  // (SPS + DPS) P younger memory operations
+  if constexpr (kIn) {
+    static_for<0, kP>([&](auto I) {
+      store_step(0, d3{0.0, 0.0, 0.0});  // row ys - 3K: out of range
+      dma(decltype(I)::value, decltype(I)::value);
+    });
+  }
 
   auto step = [&](auto J, int s) {
     constexpr int j = decltype(J)::value;
     constexpr int cur = j % 3, s1 = (j + 2) % 3, s2 = (j + 1) % 3;  // slots of steps s (== s-3), s-1, s-2
-    d2 r0, r1, r2;  // level-0 rows s-3, s-2, s-1
-    static_for<0, K>([&](auto Q) {
-      constexpr int p = K - decltype(Q)::value;  // K .. 1, top-down
-      if constexpr (p == 3 || (K < 3 && p == K)) {
-        // the DMA of row s-1 (issued at step s-1-P) has landed once at most
-        // (SPS + 1) P + SPS younger memory operations are outstanding
-        if constexpr (p == K) {
-          wait_vmcnt<(SPS + 1) * P>();  // this step's stores are not issued yet
+    d3 r0, r1, r2;  // level PB-1, rows of steps s-3, s-2, s-1
+    static_for<0, NL>([&](auto Q) {
+      constexpr int p = PE - decltype(Q)::value;  // PE .. PB, top-down
+      if constexpr (p == RL) {
+        if constexpr (kIn) {
+          // the DMA of row s-1 (issued at step s-1-P) has landed once at most
+          // (SPS + DPS) P [+ SPS: this step's stores, issued at level K above]
+          // younger memory operations are outstanding
+          if constexpr (p == PE)
+            wait_vmcnt<(SPS + DPS) * kP>();
+          else
+            wait_vmcnt<(SPS + DPS) * kP + SPS>();
+          r0 = lds_row(ring + ((j + kU - 3) % kRS) * kSlotBytes, lane);
+          r1 = lds_row(ring + ((j + kU - 2) % kRS) * kSlotBytes, lane);
+          r2 = lds_row(ring + ((j + kU - 1) % kRS) * kSlotBytes, lane);
         } else {
-          wait_vmcnt<(SPS + 1) * P + SPS>();
+          r0 = lds_row(hand + ((j + kU - 3) % kHS) * kRowBytes, lane);
+          r1 = lds_row(hand + ((j + kU - 2) % kHS) * kRowBytes, lane);
+          r2 = lds_row(hand + ((j + kU - 1) % kHS) * kRowBytes, lane);
         }
-        r0 = ring[(j + U - 3) % RS][lane];
-        r1 = ring[(j + U - 2) % RS][lane];
-        r2 = ring[(j + U - 1) % RS][lane];
       }
       const int64_t row = yl + s - 2 * p;
-      d2 v;
-      if constexpr (p == 1)
+      d3 v;
+      if constexpr (p == PB)
         v = level(r0, r1, r2, row);
       else
-        v = level(W[p - 1][cur], W[p - 1][s2], W[p - 1][s1], row);
-      if constexpr (p == K) {
-        if constexpr (!EXACT) {
-          v.x = __builtin_amdgcn_ldexp(v.x, -2 * K);  // exact power-of-two unscale
-          v.y = __builtin_amdgcn_ldexp(v.y, -2 * K);
+        v = level(W[p - 1 - PB][cur], W[p - 1 - PB][s2], W[p - 1 - PB][s1], row);
+      if constexpr (p == PE) {
+        if constexpr (kOut) {
+          if constexpr (!EXACT) {
+            v.x = __builtin_amdgcn_ldexp(v.x, -2 * K);  // exact power-of-two unscale
+            v.y = __builtin_amdgcn_ldexp(v.y, -2 * K);
+            v.z = __builtin_amdgcn_ldexp(v.z, -2 * K);
+          }
+          store_step(s, v);  // issued every step (warm-up rows are out of range)
+        } else {
+          double* h = reinterpret_cast<double*>(hand + (j % kHS) * kRowBytes) + kNC * lane;
+          h[0] = v.x;
+          h[1] = v.y;
+          h[2] = v.z;
         }
-        store_step(s, v);  // issued every step (warm-up rows are out of range)
       } else {
-        W[p][cur] = v;
+        W[p - PB][cur] = v;
       }
       __builtin_amdgcn_sched_barrier(0);
     });
-    // the ring slot of row s-3 is free (its ds_reads completed before level 1
-    // used them): prefetch row s+P into it
-    dma(s + P, (j + P) % RS);
+    // the ring slot of row s-3 is free (its ds_reads completed before level
+    // PB used them): prefetch row s+P into it
+    dma(s + kP, (j + kP) % kRS);
+    if constexpr (SYNC) step_barrier();
   };
 
   // One loop for the whole segment: splitting off the pipeline's warm-up
   // and drain steps (to skip the levels nobody reads there) made the
-  // register allocator spill from K = 12 on (three loops carrying W).
-  for (int s0 = 0; s0 < a.nsteps; s0 += U) static_for<0, U>([&](auto J) { step(J, s0 + decltype(J)::value); });
+  // register allocator spill (three loops carrying W).
+  for (int s0 = 0; s0 < a.nsteps; s0 += kU) static_for<0, kU>([&](auto J) { step(J, s0 + decltype(J)::value); });
   // no LDS-DMA may land after the workgroup's LDS is released
   wait_vmcnt<0>();
 }
 
-// A workgroup = nw waves on nw adjacent 128-column strips of one segment
-// (adjacent strips share their 2K overlap columns in the CU's L1 / the XCD's
-// L2); every wave is independent (no barrier).
-template <int K, int P, bool EXACT, bool ODD>
-__global__ __launch_bounds__(kMaxWaves * kWave) __attribute__((amdgpu_waves_per_eu(2)))
+// A workgroup = nw adjacent strips of one segment row, G waves per strip
+// (adjacent strips share their overlap columns in the CU's L1 / the XCD's
+// L2).  G == 1: every wave is independent (no barrier).
+template <int K, bool EXACT, bool EDGE>
+__global__ __launch_bounds__(kMaxThreads) __attribute__((amdgpu_waves_per_eu(2)))
 void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__ un, int64_t nblocks) {
+  constexpr int G = n_stages(K);
   extern __shared__ d2 lds_dyn[];
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
+  const int sl = wave / G, stage = wave % G;
   const int64_t t = xcd_swizzle(blockIdx.x, nblocks);
   int k = 0;
   while (k + 1 < a.n && t >= a.tstart[k + 1]) ++k;
@@ -262,32 +335,50 @@ void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__
   const int64_t ngroups = (a.nstrip[k] + a.nw - 1) / a.nw;
   const int64_t nseg = (a.r[k][3] + a.seg - 1) / a.seg;
   // dispatch order of the segment rows: the first and the last (the only
-  // ones that can hold Dirichlet-rule waves at the top / bottom, ~40% more
-  // VALU per step) go first, so the launch's tail is made of fast waves
+  // ones that can hold Dirichlet-rule waves at the top / bottom) go first,
+  // so the launch's tail is made of fast waves
   const int64_t lseg = lt / ngroups;
   const int64_t seg = nseg < 2 || lseg == 0 ? lseg : (lseg == 1 ? nseg - 1 : lseg - 1);
-  const int64_t strip = (lt % ngroups) * a.nw + wave;
-  if (strip >= a.nstrip[k]) return;  // whole wave: no barrier anywhere
-  constexpr int64_t wout = kCols - 2 * K;
+  const int64_t strip = (lt % ngroups) * a.nw + sl;
+  if (strip >= a.nstrip[k]) {  // no strip for this wave
+    if constexpr (G > 1) {
+      for (int s = 0; s < a.nsteps; ++s) step_barrier();  // the workgroup's per-step barriers
+    }
+    return;
+  }
+  constexpr int64_t wout = strip_out(K);
   const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
   const int64_t ry1 = a.r[k][2] + a.r[k][3];
   int64_t xs = rx0 + strip * wout;
-  if (xs + wout > rx1) {  // last strip: shifted left to reach rx1 (even start, rounded up)
-    xs = (rx1 - wout + 1) & ~int64_t(1);
-    if (xs < rx0) xs = rx0;
-  }
+  if (xs + wout > rx1) xs = rx1 - wout > rx0 ? rx1 - wout : rx0;  // last strip: shifted left to end at rx1
   const int64_t xe = xs + wout < rx1 ? xs + wout : rx1;
   const int64_t ys = a.r[k][2] + seg * a.seg;
   const int64_t ye = ys + a.seg < ry1 ? ys + a.seg : ry1;
   // the rule path only where a computed cell can be a fixed ring cell
-  const int64_t cx0 = xs - K, cx1 = xs - K + kCols;
+  const int64_t cx0 = xs - ring_left(K), cx1 = cx0 + kCols;
   const bool rule = (cx0 < a.dom[0] && !(a.mask & 1)) || (cx1 > a.dom[0] + a.dom[1] && !(a.mask & 2)) ||
                     (ys - K < a.dom[2] && !(a.mask & 4)) || (ye + K > a.dom[2] + a.dom[3] && !(a.mask & 8));
-  d2(*ring)[kWave] = reinterpret_cast<d2(*)[kWave]>(lds_dyn + wave * (P + 3) * kWave);
-  if (rule)
-    run_strip<K, P, EXACT, ODD, true>(a, u, un, ring, lane, xs, xe, ys, ye);
-  else
-    run_strip<K, P, EXACT, ODD, false>(a, u, un, ring, lane, xs, xe, ys, ye);
+  char* ring = reinterpret_cast<char*>(lds_dyn) + sl * strip_lds(G);
+  char* hand = ring + kRS * kSlotBytes;
+  if constexpr (G == 1) {
+    if (rule)
+      run_stage<K, 1, K, EXACT, EDGE, true, false>(a, u, un, ring, hand, lane, xs, xe, ys, ye);
+    else
+      run_stage<K, 1, K, EXACT, EDGE, false, false>(a, u, un, ring, hand, lane, xs, xe, ys, ye);
+  } else {
+    constexpr int KA = stage0_levels(K);
+    if (stage == 0) {
+      if (rule)
+        run_stage<K, 1, KA, EXACT, EDGE, true, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye);
+      else
+        run_stage<K, 1, KA, EXACT, EDGE, false, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye);
+    } else {
+      if (rule)
+        run_stage<K, KA + 1, K, EXACT, EDGE, true, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye);
+      else
+        run_stage<K, KA + 1, K, EXACT, EDGE, false, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye);
+    }
+  }
 }
 
 }  // namespace tb
@@ -298,30 +389,29 @@ namespace {
 using namespace gmt;
 using namespace gmt::tb;
 
-// Output rows per wave.  Short segments measured fastest on 32768^2 even
-// though every segment pays the 3K-step pipeline warm-up (192-384 rows beat
-// 512-1024 by 5-20%, also with the boundary segment rows dispatched first;
-// gmt_kernel_bench --only=tb, profiles/r02_tb.md): K <= 12 -> 192,
-// K = 14 -> 256, K = 16 -> 384.  Small domains get shorter segments so the
-// launch still has ~4 waves per resident slot (8192^2: 96 rows).
+// Output rows per strip.  Short segments measured fastest on 32768^2 even
+// though every segment pays the 3K-step pipeline warm-up (profiles/r02_tb.md);
+// small domains get shorter segments so the launch still has ~4 waves per
+// resident slot.
 int64_t default_seg_rows(int K, int64_t rows_x_strips) {
-  const int64_t pref = K <= 12 ? 192 : (K <= 14 ? 256 : 384);
+  const int64_t pref = K <= 10 ? 192 : (K <= 14 ? 256 : 384);
   constexpr int64_t kTargetWaves = 4 * 2048;  // 4 x (2 waves/SIMD x 1024 SIMDs)
-  return std::max<int64_t>(64, std::min(pref, rows_x_strips / kTargetWaves));
+  return std::max<int64_t>(64, std::min(pref, rows_x_strips * n_stages(K) / kTargetWaves));
 }
 
-template <int K, int P, bool EXACT, bool ODD>
+template <int K, bool EXACT, bool EDGE>
 int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int64_t* dom, int mask, const double* u,
               double* un, int64_t ld, int64_t nrows, hipStream_t s) {
-  constexpr int U = lcm3(P + 3);
+  constexpr int G = n_stages(K);
+  constexpr int kMaxStrips = kMaxThreads / kWave / G;
   Args a{};
-  a.nw = o.wg_waves > 0 ? o.wg_waves : 4;
+  a.nw = std::min(o.wg_waves > 0 ? o.wg_waves : (G == 1 ? 4 : 2), kMaxStrips);
   a.ld = ld;
   a.last_row = nrows - 1;
   a.mask = mask;
   a.quarter = 0.25;
   for (int j = 0; j < 4; ++j) a.dom[j] = dom[j];
-  constexpr int64_t wout = kCols - 2 * K;
+  constexpr int64_t wout = strip_out(K);
   int64_t maxh = 0;
   for (int k = 0; k < n_rect; ++k) {
     const int64_t* r = rects + 4 * k;
@@ -332,20 +422,20 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     ++a.n;
   }
   if (a.n == 0) return 0;
-  // all strips of a rect narrower than nw strips: fewer waves per workgroup
+  // all strips of a rect narrower than nw strips: fewer strips per workgroup
   int64_t maxs = 0;
   for (int k = 0; k < a.n; ++k) maxs = std::max(maxs, a.nstrip[k]);
   if (a.nw > maxs) a.nw = static_cast<int>(maxs);
   // the kernel addresses a segment's rows through 32-bit buffer offsets:
   // (L + 3K + unroll + prefetch) rows of ld doubles must stay below 2^31
-  const int64_t lmax = std::min<int64_t>(1 << 20, (int64_t(1) << 31) / (ld * 8) - 3 * K - 2 * U - P);
+  const int64_t lmax = std::min<int64_t>(1 << 20, (int64_t(1) << 31) / (ld * 8) - 3 * K - 2 * kU - kP);
   if (lmax < 1) return static_cast<int>(hipErrorInvalidValue);
   int64_t rows_x_strips = 0;
   for (int k = 0; k < a.n; ++k) rows_x_strips += a.r[k][3] * a.nstrip[k];
   const int64_t L =
       std::min(std::min<int64_t>(o.seg_rows > 0 ? o.seg_rows : default_seg_rows(K, rows_x_strips), maxh), lmax);
   a.seg = static_cast<int>(L);
-  a.nsteps = static_cast<int>((L + 3 * K + U - 1) / U * U);
+  a.nsteps = static_cast<int>((L + 3 * K + kU - 1) / kU * kU);
   a.tstart[0] = 0;
   for (int k = 0; k < a.n; ++k) {
     const int64_t groups = (a.nstrip[k] + a.nw - 1) / a.nw;
@@ -353,57 +443,81 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   }
   for (int k = a.n + 1; k <= kMaxRect; ++k) a.tstart[k] = a.tstart[a.n];
   const int64_t nb = a.tstart[a.n];
-  const size_t smem = static_cast<size_t>(lds_bytes(a.nw, P));
-  jacobi5tb_kernel<K, P, EXACT, ODD><<<grid_1d(nb), a.nw * kWave, smem, s>>>(a, u, un, nb);
+  const size_t smem = static_cast<size_t>(a.nw * strip_lds(G));
+  if (smem > 65536) {  // above the default dynamic-LDS limit (gfx950 has 160 KB per CU)
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem));
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  jacobi5tb_kernel<K, EXACT, EDGE><<<grid_1d(nb), a.nw * G * kWave, smem, s>>>(a, u, un, nb);
   return static_cast<int>(hipGetLastError());
 }
 
-template <int K, int P>
+template <int K>
 int dispatch_k(const gmt_tb_opts& o, bool exact, int n_rect, const int64_t* rects, const int64_t* dom, int mask,
                const double* u, double* un, int64_t ld, int64_t nrows, hipStream_t s) {
-  bool odd = false;  // some rect ends at an odd column: one lane stores a single column
+  // a rect narrower than a strip whose width is 1 mod 3 ends inside a lane:
+  // that lane stores its first column alone (wider rects end on a lane
+  // boundary: their last strip is shifted to end at the rect's edge)
+  bool edge = false;
   for (int k = 0; k < n_rect; ++k)
-    if (rects[4 * k + 1] > 0 && rects[4 * k + 3] > 0 && ((rects[4 * k] + rects[4 * k + 1]) & 1)) odd = true;
-  if (odd)
-    return exact ? launch_tb<K, P, true, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s)
-                 : launch_tb<K, P, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s);
-  return exact ? launch_tb<K, P, true, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s)
-               : launch_tb<K, P, false, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s);
+    if (rects[4 * k + 1] > 0 && rects[4 * k + 3] > 0 && rects[4 * k + 1] < strip_out(K) && rects[4 * k + 1] % 3 == 1)
+      edge = true;
+  if (edge)
+    return exact ? launch_tb<K, true, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s)
+                 : launch_tb<K, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s);
+  return exact ? launch_tb<K, true, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s)
+               : launch_tb<K, false, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s);
 }
 
 }  // namespace
+
+extern "C" int gmt_jacobi5tb_supported(int sweeps) {
+  return (sweeps >= 1 && sweeps <= kMaxK1) || (sweeps > kMaxK1 && sweeps <= GMT_TB_MAX_SWEEPS && sweeps % 2 == 0);
+}
 
 extern "C" int gmt_jacobi5tb(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, const int64_t* dom,
                              int halo_mask, const double* u, double* un, int64_t ld, int64_t nrows, void* stream) {
   gmt_tb_opts o{};
   if (opts) o = *opts;
   const int K = o.sweeps;
-  if (K < 2 || K > GMT_TB_MAX_SWEEPS || (K % 2) != 0) return static_cast<int>(hipErrorInvalidValue);
+  if (!gmt_jacobi5tb_supported(K)) return static_cast<int>(hipErrorInvalidValue);
   if (n_rect < 0 || n_rect > kMaxRect) return static_cast<int>(hipErrorInvalidValue);
-  if (o.wg_waves < 0 || o.wg_waves > kMaxWaves || o.seg_rows < 0) return static_cast<int>(hipErrorInvalidValue);
-  if (!aligned16(u) || !aligned16(un) || (ld % 2) != 0 || ld <= 0) return static_cast<int>(hipErrorInvalidValue);
+  if (o.wg_waves < 0 || o.wg_waves > kMaxThreads / kWave || o.seg_rows < 0)
+    return static_cast<int>(hipErrorInvalidValue);
+  if ((reinterpret_cast<uintptr_t>(u) & 7u) || (reinterpret_cast<uintptr_t>(un) & 7u) || ld <= 0)
+    return static_cast<int>(hipErrorInvalidValue);
   if (static_cast<uint64_t>(ld) * 8u > 0xffffffffull) return static_cast<int>(hipErrorInvalidValue);
   for (int k = 0; k < n_rect; ++k) {
     const int64_t* r = rects + 4 * k;
     if (r[1] <= 0 || r[3] <= 0) continue;
-    // 16-B loads: even start; the K-wide ring left of / above the rect exists
-    if ((r[0] % 2) != 0 || r[0] < K || r[2] < K || r[0] + r[1] > ld || r[2] + r[3] + K > nrows)
+    // the K-wide ring around the rect exists
+    if (r[0] < K || r[2] < K || r[0] + r[1] + K > ld || r[2] + r[3] + K > nrows)
       return static_cast<int>(hipErrorInvalidValue);
   }
   const bool exact = o.exact != 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
   switch (K) {
-#define GMT_TB_CASE(KK)                                                                                   \
-  case KK:                                                                                                \
-    return dispatch_k<KK, 3>(o, exact, n_rect, rects, dom, halo_mask, u, un, ld, nrows, s);
+#define GMT_TB_CASE(KK) \
+  case KK:              \
+    return dispatch_k<KK>(o, exact, n_rect, rects, dom, halo_mask, u, un, ld, nrows, s);
+    GMT_TB_CASE(1)
     GMT_TB_CASE(2)
+    GMT_TB_CASE(3)
     GMT_TB_CASE(4)
+    GMT_TB_CASE(5)
     GMT_TB_CASE(6)
+    GMT_TB_CASE(7)
     GMT_TB_CASE(8)
+    GMT_TB_CASE(9)
     GMT_TB_CASE(10)
     GMT_TB_CASE(12)
     GMT_TB_CASE(14)
     GMT_TB_CASE(16)
+    GMT_TB_CASE(18)
+    GMT_TB_CASE(20)
+    GMT_TB_CASE(22)
+    GMT_TB_CASE(24)
 #undef GMT_TB_CASE
     default:
       return static_cast<int>(hipErrorInvalidValue);

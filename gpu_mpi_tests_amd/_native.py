@@ -71,8 +71,7 @@ _SIGS = {
         c_int,
         [c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_dbl, c_dbl, c_vp],
     ),
-    "gmt_jacobi5x2": (c_int, [c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
-    "gmt_jacobi5xk": (c_int, [c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_i64, c_int, c_vp]),
+    "gmt_jacobi5tb_supported": (c_int, [c_int]),
     "gmt_jacobi5tb": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_vp]),
     "gmt_jacobi5_set_variant": (None, [c_int]),
     "gmt_daxpy_set_variant": (None, [c_int]),

@@ -30,7 +30,7 @@ HIP_ENGINE = os.path.join(_HERE, "_lib", "libgmt_engine.so")
 HOST_ENGINE = os.path.join(_ROOT, "build", "lib-host", "libgmt_engine.so")
 
 LOCAL, RCCL = 0, 1
-MAX_TSTEPS = 16  # GMT_TB_MAX_SWEEPS (csrc/include/gmt/kernels.h)
+MAX_TSTEPS = 24  # GMT_TB_MAX_SWEEPS (csrc/include/gmt/kernels.h)
 _libs: dict[str, ctypes.CDLL] = {}
 
 

@@ -3,7 +3,8 @@
 Kernel inventory (SURVEY.md §2.3): K1/K2 ``daxpy``; K3 ``stencil5_1d``;
 K4/K5/K11 ``stencil5_2d``; K6/K7/K8 ``copy2d_batched`` (halo pack/unpack);
 K9 ``sum_axis``; K10/K12 ``diff_sq``/``diff_norm``; analytic ``fill_poly``;
-and the BASELINE 5-point Jacobi ``jacobi5`` / ``jacobi5_rects``.
+and the BASELINE 5-point Jacobi ``jacobi5`` / ``jacobi5_rects`` (single sweep)
+and ``jacobi5tb`` (K fused sweeps per memory pass).
 """
 from .kernels import (  # noqa: F401
     copy2d_batched,
@@ -13,11 +14,9 @@ from .kernels import (  # noqa: F401
     fill_poly,
     jacobi5,
     jacobi5_rects,
-    jacobi5x2,
     jacobi5xk,
     jacobi5tb,
-    XK_EXT,
-    XK_PIPE,
+    tb_supported,
     set_jacobi_variant,
     stencil5_1d,
     stencil5_2d,

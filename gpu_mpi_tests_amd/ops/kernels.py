@@ -255,68 +255,54 @@ def jacobi5_rects(u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, 
                                       _stream(u)), "gmt_jacobi5_rects")
 
 
-XK_PIPE = 0x40000000  # gmt_jacobi5xk tile flag: register-pipelined kernel (jacobi5pipe.hip)
-XK_EXT = 0x20000000   # with XK_PIPE: interior cells outside the rects may be rewritten (own values)
+TB_MAX_SWEEPS = 24  # GMT_TB_MAX_SWEEPS (csrc/include/gmt/kernels.h)
+
+
+def tb_supported(k: int) -> bool:
+    """Sweep counts the temporal-blocking kernel is built for: 1..10 (one wave
+    per strip) and even 12..24 (two waves per strip, levels split)."""
+    return 1 <= k <= 10 or (10 < k <= TB_MAX_SWEEPS and k % 2 == 0)
 
 
 def _check_xk_bounds(k: int, u: torch.Tensor, un: torch.Tensor, rects) -> None:
-    """Host-side guard before a K-sweep launch: the kernels read each rect plus a
-    K-wide ring (K rounded up to even on the x side) and the rule path may read up
-    to the last column of a row, so both tensors must be whole row-major arrays
-    holding that ring."""
+    """Host-side guard before a K-sweep launch: the kernel reads each rect plus a
+    K-wide ring, so both tensors must be whole row-major fp64 arrays holding
+    that ring."""
     if u.dim() != 2 or u.shape != un.shape or not (u.is_contiguous() and un.is_contiguous()):
-        raise ValueError("jacobi5xk: u and un must be contiguous 2-D tensors of one shape")
+        raise ValueError("jacobi5tb: u and un must be contiguous 2-D tensors of one shape")
     if u.dtype != torch.float64 or un.dtype != torch.float64:
-        raise ValueError("jacobi5xk: fp64 only")
-    kx = k + (k & 1)
+        raise ValueError("jacobi5tb: fp64 only")
     rows, cols = u.shape
     for x0, nx, y0, ny in rects:
-        if x0 % 2 or x0 - kx < 0 or y0 - k < 0 or x0 + nx + k > cols or y0 + ny + k > rows:
-            raise ValueError(f"jacobi5xk: rect {(x0, nx, y0, ny)} with its {k}-cell ring does not fit "
-                             f"a {rows}x{cols} array (x0 must be even)")
-
-
-def jacobi5xk(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, int, int, int]],
-              dom: tuple[int, int, int, int], halo_mask: int = 0, tile: int = 0) -> None:
-    """``k`` (2-14) fused Laplace Jacobi sweeps (temporal blocking): ``un = J^k(u)`` on
-    each output rect (absolute coordinates, x0 even).  ``dom`` is the interior; bits
-    of ``halo_mask`` (1 W, 2 E, 4 S, 8 N) mark ghost sides owned by a neighbour.
-    ``tile``: 0 = default (register-pipelined kernel for even k, LDS tiles for k = 3),
-    ``XK_PIPE | rows`` = pipelined kernel with ``rows`` output rows per wave,
-    ``(TX << 16) | TY`` = LDS-tiled kernel (k <= 4)."""
-    rects = [tuple(int(v) for v in r) for r in rects if r[1] > 0 and r[3] > 0]
-    if not rects:
-        return
-    if not _is_dev(u):
-        ref.jacobi5xk(k, u, un, rects, dom, halo_mask)
-        return
-    assert len(rects) <= 4 and u.stride(0) == un.stride(0)
-    _check_xk_bounds(k, u, un, rects)
-    L = _native.lib()
-    arr = (ctypes.c_int64 * (4 * len(rects)))(*[v for r in rects for v in r])
-    d = (ctypes.c_int64 * 4)(*[int(v) for v in dom])
-    _native.check(L.gmt_jacobi5xk(int(k), len(rects), ctypes.cast(arr, ctypes.c_void_p),
-                                  ctypes.cast(d, ctypes.c_void_p), int(halo_mask), u.data_ptr(),
-                                  un.data_ptr(), u.stride(0), int(tile), _stream(u)),
-                  "gmt_jacobi5xk")
+        if x0 - k < 0 or y0 - k < 0 or x0 + nx + k > cols or y0 + ny + k > rows:
+            raise ValueError(f"jacobi5tb: rect {(x0, nx, y0, ny)} with its {k}-cell ring does not fit "
+                             f"a {rows}x{cols} array")
 
 
 def jacobi5tb(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, int, int, int]],
               dom: tuple[int, int, int, int], halo_mask: int = 0, *, wg_waves: int = 0, seg_rows: int = 0,
               exact: bool = False) -> None:
-    """``k`` (even, 2-16) fused Laplace sweeps with the workgroup-cooperative
-    temporal-blocking kernel (csrc/kernels/jacobi5tb.hip): ``un = J^k(u)`` on up to
-    8 output rects (absolute coordinates, x0 even, x0 >= k, y0 >= k); the rest of
-    ``un`` is never written.  ``wg_waves``: independent 128-column waves per
-    workgroup (0 = 4), ``seg_rows``: output rows per wave (0 = default), ``exact``:
-    1/4 multiply per level instead of power-of-two scaled levels."""
+    """``k`` fused Laplace sweeps per memory pass with the temporal-blocking kernel
+    (csrc/kernels/jacobi5tb.hip): ``un = J^k(u)`` on up to 8 output rects (absolute
+    coordinates, each with its k-wide ring inside the array); the rest of ``un``
+    is never written.  ``dom`` is the interior; bits of ``halo_mask`` (1 W, 2 E,
+    4 S, 8 N) mark ghost sides owned by a neighbour (the others are fixed
+    Dirichlet rings).  ``k``: see :func:`tb_supported`.  ``wg_waves``: 192-column
+    strips per workgroup (0 = default), ``seg_rows``: output rows per strip (0 =
+    default), ``exact``: 1/4 multiply per level instead of power-of-two scaled
+    levels."""
     rects = [tuple(int(v) for v in r) for r in rects if r[1] > 0 and r[3] > 0]
+    if not tb_supported(k):
+        raise ValueError(f"jacobi5tb: {k} sweeps per pass is not built (1..10 or even 12..{TB_MAX_SWEEPS})")
     if not rects:
         return
+    if len(rects) > 8:
+        raise ValueError("jacobi5tb: at most 8 rects per launch")
     if not _is_dev(u):
         ref.jacobi5xk(k, u, un, rects, dom, halo_mask)
         return
-    assert len(rects) <= 8 and u.stride(0) == un.stride(0)
+    if u.stride(0) != un.stride(0):
+        raise ValueError("jacobi5tb: u and un must share a row pitch")
     _check_xk_bounds(k, u, un, rects)
     L = _native.lib()
     arr = (ctypes.c_int64 * (4 * len(rects)))(*[v for r in rects for v in r])
@@ -328,10 +314,10 @@ def jacobi5tb(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[i
                   "gmt_jacobi5tb")
 
 
-def jacobi5x2(u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, int, int, int]],
-              dom: tuple[int, int, int, int], halo_mask: int = 0, tile_rows: int = 0) -> None:
-    """Two fused Laplace Jacobi sweeps: ``jacobi5xk(2, ...)``."""
-    jacobi5xk(2, u, un, rects, dom, halo_mask, tile_rows)
+def jacobi5xk(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, int, int, int]],
+              dom: tuple[int, int, int, int], halo_mask: int = 0) -> None:
+    """``k`` fused Laplace sweeps with the default launch: :func:`jacobi5tb`."""
+    jacobi5tb(k, u, un, rects, dom, halo_mask)
 
 
 def set_jacobi_variant(v: int) -> None:

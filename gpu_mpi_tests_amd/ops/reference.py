@@ -87,7 +87,7 @@ def jacobi5(u: torch.Tensor, un: torch.Tensor, x0: int, nx: int, y0: int, ny: in
 
 def jacobi5xk(k: int, u: torch.Tensor, un: torch.Tensor, rects, dom, halo_mask: int = 0) -> None:
     """fp64 reference of k fused Laplace sweeps with the ghost-side rule of
-    csrc/kernels/jacobi5x2.hip: a ring cell outside ``dom`` gets an
+    csrc/kernels/jacobi5tb.hip: a ring cell outside ``dom`` gets an
     intermediate update only if its side's bit is set in ``halo_mask``."""
     dx0, dnx, dy0, dny = dom
     dx1, dy1 = dx0 + dnx, dy0 + dny
@@ -110,6 +110,3 @@ def jacobi5xk(k: int, u: torch.Tensor, un: torch.Tensor, rects, dom, halo_mask: 
             cur = nxt
 
 
-def jacobi5x2(u: torch.Tensor, un: torch.Tensor, rects, dom, halo_mask: int = 0) -> None:
-    """Two fused sweeps: ``jacobi5xk(2, ...)``."""
-    jacobi5xk(2, u, un, rects, dom, halo_mask)

@@ -275,141 +275,3 @@ def test_stream_semantics():
         ops.daxpy(2.0, x, y)
     s.synchronize()
     assert torch.equal(y, exp)
-
-
-@pytest.mark.parametrize("tile_rows", [0, 8, 16, 32, (64 << 16) | 4, (64 << 16) | 16, (128 << 16) | 4,
-                                       (256 << 16) | 8, (32 << 16) | 32, (64 << 16) | 24])
-@pytest.mark.parametrize("ny,nx", [(1, 2), (5, 7), (17, 130), (40, 256), (70, 515), (129, 1024)])
-@pytest.mark.parametrize("mask", [0, 15, 5, 10])
-def test_jacobi5x2_fused_two_sweeps(tile_rows, ny, nx, mask):
-    """Temporal blocking: bitwise equal to the fp64 two-sweep reference, incl.
-    partial tiles, odd widths and every ghost-side ownership pattern."""
-    g, xo = 2, 8
-    u = _rand(ny + 2 * g, (xo + nx + 9) // 2 * 2, seed=51)  # even row pitch (16-B rows)
-    dom = (xo, nx, g, ny)
-    un = torch.zeros_like(u)
-    ops.jacobi5x2(u, un, [(xo, nx, g, ny)], dom, mask, tile_rows)
-    exp = torch.zeros(u.shape, dtype=torch.float64)
-    ref.jacobi5x2(u.cpu(), exp, [(xo, nx, g, ny)], dom, mask)
-    torch.cuda.synchronize()
-    assert torch.equal(un[g:g + ny, xo:xo + nx].cpu(), exp[g:g + ny, xo:xo + nx])
-
-
-def test_jacobi5x2_frame_rects_match_full():
-    """core + 4 frame rects in two launches == one full-interior launch."""
-    g, xo, ny, nx = 2, 8, 64, 300
-    u = _rand(ny + 2 * g, xo + nx + 8, seed=52)
-    dom = (xo, nx, g, ny)
-    full = torch.zeros_like(u)
-    ops.jacobi5x2(u, full, [dom], dom, 15)
-    split = torch.zeros_like(u)
-    ops.jacobi5x2(u, split, [(xo + 2, nx - 4, g + 2, ny - 4)], dom, 15)
-    ops.jacobi5x2(u, split, [(xo, nx, g, 2), (xo, nx, g + ny - 2, 2), (xo, 2, g + 2, ny - 4),
-                             (xo + nx - 2, 2, g + 2, ny - 4)], dom, 15)
-    torch.cuda.synchronize()
-    assert torch.equal(split[g:g + ny, xo:xo + nx], full[g:g + ny, xo:xo + nx])
-
-
-@pytest.mark.parametrize("k", [3, 4])
-@pytest.mark.parametrize("tile", [0, (32 << 16) | 32, (64 << 16) | 8, (128 << 16) | 8])
-@pytest.mark.parametrize("ny,nx", [(1, 2), (6, 9), (33, 130), (70, 515)])
-@pytest.mark.parametrize("mask", [0, 15, 6])
-def test_jacobi5xk_fused_k_sweeps(k, tile, ny, nx, mask):
-    g, xo = k, 8
-    u = _rand(ny + 2 * g, (xo + nx + 9) // 2 * 2, seed=61)
-    dom = (xo, nx, g, ny)
-    un = torch.zeros_like(u)
-    ops.jacobi5xk(k, u, un, [(xo, nx, g, ny)], dom, mask, tile)
-    exp = torch.zeros(u.shape, dtype=torch.float64)
-    ref.jacobi5xk(k, u.cpu(), exp, [(xo, nx, g, ny)], dom, mask)
-    torch.cuda.synchronize()
-    assert torch.equal(un[g:g + ny, xo:xo + nx].cpu(), exp[g:g + ny, xo:xo + nx])
-
-
-@pytest.mark.parametrize("k", [2, 4, 6, 8, 10, 12, 14])
-@pytest.mark.parametrize("seg", [0, 1, 5, 64, (1 << 19) | 7, (1 << 19) | 64, (2 << 19) | 33, (2 << 19) | 3,
-                                 (1 << 21) | 16, (1 << 22) | 24])
-@pytest.mark.parametrize("ny,nx", [(1, 2), (7, 9), (40, 126), (33, 130), (70, 515), (301, 700)])
-@pytest.mark.parametrize("mask", [0, 15, 6, 9])
-def test_jacobi5xk_pipelined(k, seg, ny, nx, mask):
-    """Register-pipelined K-sweep kernel (jacobi5pipe.hip): bitwise equal to k
-    fp64 reference sweeps — partial strips (128 - 2k output columns per wave),
-    segments shorter than the pipeline depth, every ghost-side pattern; the
-    default launch (rule bands split off the fast core), the per-wave split
-    (bit 22) and the single-kernel launch (bit 21)."""
-    g, xo = k, max(8, k)  # the K-wide ghost ring fits left of the interior
-    u = _rand(ny + 2 * g, (xo + nx + max(9, k + 1)) // 2 * 2, seed=71)
-    dom = (xo, nx, g, ny)
-    un = torch.zeros_like(u)
-    ops.jacobi5xk(k, u, un, [(xo, nx, g, ny)], dom, mask, ops.XK_PIPE | seg)
-    exp = torch.zeros(u.shape, dtype=torch.float64)
-    ref.jacobi5xk(k, u.cpu(), exp, [(xo, nx, g, ny)], dom, mask)
-    torch.cuda.synchronize()
-    assert torch.equal(un[g:g + ny, xo:xo + nx].cpu(), exp[g:g + ny, xo:xo + nx])
-
-
-@pytest.mark.parametrize("k", [4, 8, 12, 14])
-def test_jacobi5xk_pipelined_frame_rects(k):
-    """core + 4 frame rects (the engine's overlapped block step) == full launch,
-    and the output never touches cells outside the rects."""
-    g, xo, ny, nx = k, max(8, k), 90, 400
-    u = _rand(ny + 2 * g, xo + nx + max(8, k), seed=72)
-    dom = (xo, nx, g, ny)
-    full = torch.zeros_like(u)
-    ops.jacobi5xk(k, u, full, [dom], dom, 15)
-    split = torch.full_like(u, 7.0)
-    ops.jacobi5xk(k, u, split, [(xo + k, nx - 2 * k, g + k, ny - 2 * k)], dom, 15)
-    ops.jacobi5xk(k, u, split, [(xo, nx, g, k), (xo, nx, g + ny - k, k), (xo, k, g + k, ny - 2 * k),
-                                (xo + nx - k, k, g + k, ny - 2 * k)], dom, 15)
-    torch.cuda.synchronize()
-    assert torch.equal(split[g:g + ny, xo:xo + nx], full[g:g + ny, xo:xo + nx])
-    outside = torch.ones_like(u, dtype=torch.bool)
-    outside[g:g + ny, xo:xo + nx] = False
-    assert bool((split[outside] == 7.0).all())
-
-
-def _engine_frame(k, xo, nx, g, ny, mask):
-    """The engine's overlapped block step (csrc/engine/jacobi.cpp
-    enqueue_block): core inset only on halo sides, K-wide frame bands along
-    the halo sides."""
-    ka = (k + 1) & ~1
-    hw, he, hs, hn = mask & 1, mask & 2, mask & 4, mask & 8
-    xr = (xo + nx - k) & ~1
-    cx0, cx1 = (xo + ka if hw else xo), (xr if he else xo + nx)
-    cy0, cy1 = (g + k if hs else g), (g + ny - k if hn else g + ny)
-    frame = []
-    if hs:
-        frame.append((xo, nx, g, k))
-    if hn:
-        frame.append((xo, nx, g + ny - k, k))
-    if hw:
-        frame.append((xo, ka, cy0, cy1 - cy0))
-    if he:
-        frame.append((xr, xo + nx - xr, cy0, cy1 - cy0))
-    return (cx0, cx1 - cx0, cy0, cy1 - cy0), frame
-
-
-@pytest.mark.parametrize("k", [2, 8, 12, 14])
-@pytest.mark.parametrize("mask", [15, 0, 1, 2, 5, 10, 12, 3])
-@pytest.mark.parametrize("ny,nx", [(90, 400), (130, 233), (64, 1031)])
-def test_jacobi5xk_pipelined_engine_frame_ext(k, mask, ny, nx):
-    """Mask-aware fast path + shifted last strips + GMT_XK_EXT frame bands
-    (strips reaching into the finished core) == one full launch, bitwise, and
-    nothing outside the interior is written."""
-    g, xo = k, max(8, k)
-    u = _rand(ny + 2 * g, (xo + nx + max(8, k) + 1) // 2 * 2, seed=73)
-    dom = (xo, nx, g, ny)
-    full = torch.zeros_like(u)
-    ops.jacobi5xk(k, u, full, [dom], dom, mask)
-    exp = torch.zeros(u.shape, dtype=torch.float64)
-    ref.jacobi5xk(k, u.cpu(), exp, [dom], dom, mask)
-    split = torch.full_like(u, 7.0)
-    core, frame = _engine_frame(k, xo, nx, g, ny, mask)
-    ops.jacobi5xk(k, u, split, [core], dom, mask)
-    ops.jacobi5xk(k, u, split, frame, dom, mask, ops.XK_PIPE | ops.XK_EXT)
-    torch.cuda.synchronize()
-    assert torch.equal(full[g:g + ny, xo:xo + nx].cpu(), exp[g:g + ny, xo:xo + nx])
-    assert torch.equal(split[g:g + ny, xo:xo + nx], full[g:g + ny, xo:xo + nx])
-    outside = torch.ones_like(u, dtype=torch.bool)
-    outside[g:g + ny, xo:xo + nx] = False
-    assert bool((split[outside] == 7.0).all())
