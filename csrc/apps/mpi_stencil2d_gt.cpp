@@ -6,12 +6,23 @@
 // timing semantics (exchange wall time summed over timed iterations and over
 // ranks, MPI_Reduce to rank 0).
 //
+// Where a TEST line's number is not measured the reference's way it says so
+// in a bracketed tag after the reference's fields:
+//   [persistent buffers]  the halo staging buffers and exchange plan are
+//                         created once; the reference allocates its buffers
+//                         inside every timed call (mpi_stencil2d_gt.cc:141-156;
+//                         --alloc-per-call re-creates them per call: no tag)
+//   [managed: host-resident, xnack off]  managed memory on a GPU running with
+//                         XNACK off is not migrated: those lines time
+//                         pinned-host memory over PCIe.
+//
 // Options (not in the reference):
 //   --transport=auto|mpi-host|mpi-direct|rccl|ipc   force one data plane
 //   --no-managed          skip the managed-memory variants (TEST_MANAGED off)
 //   --tests=deriv,sum     subset
 //   --host-init --host-verify   reference host loops instead of GPU fill/check
-//   --alloc-per-call      re-create halo buffers inside the timed region (gt parity)
+//   --alloc-per-call      re-create halo buffers inside the timed region (the
+//                         reference's semantics; default: persistent, tagged)
 //   --json=FILE           one JSON record per test (per-exchange µs, GB/s, transport)
 //   --dim=0|1 --mem=device|managed --buf=0|1   run one slice of the test matrix
 //   --iters=N --warmup=W  (positional n_iter still wins when given; warmup default 5)
@@ -40,6 +51,7 @@ int main(int argc, char** argv) {
   const int only_buf = static_cast<int>(cli.geti("buf", -1));
   const size_t n_global_other = static_cast<size_t>(cli.geti("n-other", 512 * 1024));
   const bool managed = !cli.flag("no-managed") && only_mem != "device";
+  const bool alloc_per_call = cli.flag("alloc-per-call");
   const std::string tests = cli.get("tests", "deriv,sum");
   const std::string json = cli.get("json", "");
 
@@ -57,6 +69,8 @@ int main(int argc, char** argv) {
     std::printf("n_global_other = %zu\n", n_global_other);
     std::printf("n_iter         = %d\n", n_iter);
     std::printf("n_warmup       = %d\n", n_warmup);
+    std::printf("# n_warmup: the reference prints its unused default 10 here; its tests run 5 "
+                "warm-up iterations (mpi_stencil2d_gt.cc:658,693), as this build does by default\n");
     std::printf("# backend=%s device=%s arch=%s managed_memory=%d xnack=%d\n",
                 gmt_rt_backend_name(), b.info.name, b.info.arch, b.info.managed_memory,
                 b.info.xnack);
@@ -67,6 +81,14 @@ int main(int argc, char** argv) {
   TransportPool& pool = *pool_owner;
   const comm::Kind want = comm::parse_kind(cli.get("transport", "auto"));
 
+  // bracketed tags after the reference's fields (see the header comment)
+  const bool host_resident_managed = gmt_rt_backend() != GMT_BACKEND_HOST && !b.info.xnack;
+  auto tags = [&](int space, bool exchange) {
+    std::string t;
+    if (exchange && !alloc_per_call) t += " [persistent buffers]";
+    if (space == GMT_SPACE_MANAGED && host_resident_managed) t += " [managed: host-resident, xnack off]";
+    return t;
+  };
   auto report = [&](const char* name, int dim, int space, bool buf, const DerivResult& r) {
     double time_sum = 0, err_sum = 0;
     MPI_Reduce(&r.total_time, &time_sum, 1, MPI_DOUBLE, MPI_SUM, 0, MPI_COMM_WORLD);
@@ -74,9 +96,9 @@ int main(int argc, char** argv) {
     double med = r.iters.median(), mx = 0;
     MPI_Allreduce(&med, &mx, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
     if (world_rank == 0) {
-      std::printf("TEST dim:%d, %s, buf:%d; %0.8f, err=%0.8f\n", dim,
+      std::printf("TEST dim:%d, %s, buf:%d; %0.8f, err=%0.8f%s\n", dim,
                   space == GMT_SPACE_MANAGED ? "managed" : "device ", buf ? 1 : 0, time_sum,
-                  err_sum);
+                  err_sum, tags(space, true).c_str());
       JsonRecord j;
       j.add("app", "mpi_stencil2d_gt").add("test", name).add("dim", dim)
           .add("mem", space == GMT_SPACE_MANAGED ? "managed" : "device").add("buf", buf)
@@ -84,7 +106,9 @@ int main(int argc, char** argv) {
           .add("n_other", n_global_other).add("iters", n_iter).add("time_sum_s", time_sum)
           .add("err_sum", err_sum).add("exchange_us_median_max_rank", mx * 1e6)
           .add("bytes_per_exchange", r.bytes_per_exchange)
-          .add("GBps_per_rank", mx > 0 ? r.bytes_per_exchange / mx / 1e9 : 0.0);
+          .add("GBps_per_rank", mx > 0 ? r.bytes_per_exchange / mx / 1e9 : 0.0)
+          .add("buffers", alloc_per_call ? "per-call" : "persistent")
+          .add("managed_host_resident", space == GMT_SPACE_MANAGED && host_resident_managed);
       j.append_to(json);
     }
     std::fflush(stdout);
@@ -108,7 +132,7 @@ int main(int argc, char** argv) {
           c.transport = want;
           c.host_init = cli.flag("host-init");
           c.host_verify = cli.flag("host-verify");
-          c.realloc_per_call = cli.flag("alloc-per-call");
+          c.realloc_per_call = alloc_per_call;
           DerivResult r = run_deriv(c, b, MPI_COMM_WORLD, pool);
           report("deriv", dim, c.space, buf, r);
         }
@@ -127,8 +151,8 @@ int main(int argc, char** argv) {
         MPI_Reduce(&r.total_time, &time_sum, 1, MPI_DOUBLE, MPI_SUM, 0, MPI_COMM_WORLD);
         MPI_Reduce(&err, &err_max, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
         if (world_rank == 0) {
-          std::printf("TEST dim:%d, %s, buf:0; allreduce=%0.8f\n", dim,
-                      m ? "managed" : "device ", time_sum);
+          std::printf("TEST dim:%d, %s, buf:0; allreduce=%0.8f%s\n", dim,
+                      m ? "managed" : "device ", time_sum, tags(space, false).c_str());
           if (err_max > 1e-9) std::printf("# WARNING allreduce value rel err %g\n", err_max);
           JsonRecord j;
           j.add("app", "mpi_stencil2d_gt").add("test", "sum").add("dim", dim)

@@ -1,5 +1,7 @@
 // MPI-based transports: mpi-host, mpi-direct, ipc, and the factory that
 // bootstraps rccl over MPI (gmt/comm.hpp, gmt/transport.hpp).
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
@@ -154,10 +156,29 @@ class MpiHostTransport : public MpiTransport {
 };
 
 // ---------------------------------------------------------------- mpi-direct
+// mpi-direct hands the buffers straight to MPI.  Device memory is legal only
+// with a GPU-aware MPI: refuse it otherwise, instead of letting a host-only
+// MPI (MPICH ch3 here) read device addresses as host memory.  Managed and
+// host memory always pass (MPI can read them).
+void require_mpi_readable(const void* p, const char* what) {
+  if (p == nullptr || gmt_rt_backend() == GMT_BACKEND_HOST) return;
+  int space = GMT_SPACE_UNREGISTERED;
+  if (gmt_rt_pointer_space(p, &space) != 0 || space != GMT_SPACE_DEVICE || mpi_gpu_aware()) return;
+  std::printf("ERROR: transport mpi-direct was given device memory (%s), but this MPI is not GPU-aware "
+              "(%s). Use --transport=mpi-host, rccl or ipc, or set GMT_MPI_GPU_AWARE=1 if the MPI "
+              "library can read device memory.\n",
+              what, mpi_gpu_aware_source());
+  std::fflush(stdout);
+  abort_job(EXIT_FAILURE);
+}
+
 class MpiDirectExchange : public Exchange {
  public:
   MpiDirectExchange(MPI_Comm c, std::vector<Msg> r, std::vector<Msg> s)
-      : c_(c), recvs_(std::move(r)), sends_(std::move(s)) {}
+      : c_(c), recvs_(std::move(r)), sends_(std::move(s)) {
+    for (auto& m : recvs_) require_mpi_readable(m.buf, "halo receive buffer");
+    for (auto& m : sends_) require_mpi_readable(m.buf, "halo send buffer");
+  }
   void start(gmt_stream_t s) override {
     // one sync covers both "send data produced" and "earlier readers of the
     // ghost cells are done" before MPI may write them
@@ -188,10 +209,13 @@ class MpiDirectTransport : public MpiTransport {
     return std::make_unique<MpiDirectExchange>(comm_, r, s);
   }
   void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override {
+    require_mpi_readable(buf, "all-reduce buffer");
     GMT_CHECK("allreduce sync", gmt_rt_stream_synchronize(s));
     GMT_MPI_CHECK(MPI_Allreduce(MPI_IN_PLACE, buf, static_cast<int>(n), MPI_DOUBLE, MPI_SUM, comm_));
   }
   void allgather(const void* send, void* recv, size_t bpr, gmt_stream_t s) override {
+    require_mpi_readable(send, "all-gather send buffer");
+    require_mpi_readable(recv, "all-gather receive buffer");
     GMT_CHECK("allgather sync", gmt_rt_stream_synchronize(s));
     MPI_Datatype t;
     int n;
@@ -416,9 +440,31 @@ Kind parse_kind(const std::string& s) {
   abort_job(EXIT_FAILURE);
 }
 
+// GMT_MPI_GPU_AWARE=1/0 decides when set; otherwise the MPI library is asked
+// through MPIX_Query_rocm_support (MPICH >= 4.1, Open MPI >= 5.0), looked up
+// with dlsym so the apps link against any MPI.  Neither: not GPU-aware.
+namespace {
+int query_rocm_support() {  // 1 / 0, or -1 when the library has no such query
+  using Query = int (*)(void);
+  void* sym = dlsym(RTLD_DEFAULT, "MPIX_Query_rocm_support");
+  return sym ? (reinterpret_cast<Query>(sym)() != 0 ? 1 : 0) : -1;
+}
+}  // namespace
+
 bool mpi_gpu_aware() {
   const char* e = std::getenv("GMT_MPI_GPU_AWARE");
-  return e && e[0] == '1';
+  if (e && e[0]) return e[0] == '1';
+  return query_rocm_support() == 1;
+}
+
+const char* mpi_gpu_aware_source() {
+  const char* e = std::getenv("GMT_MPI_GPU_AWARE");
+  if (e && e[0]) return e[0] == '1' ? "GMT_MPI_GPU_AWARE=1" : "GMT_MPI_GPU_AWARE=0";
+  switch (query_rocm_support()) {
+    case 1: return "MPIX_Query_rocm_support() = 1";
+    case 0: return "MPIX_Query_rocm_support() = 0";
+    default: return "no MPIX_Query_rocm_support in this MPI, GMT_MPI_GPU_AWARE unset";
+  }
 }
 
 Kind resolve(Kind k, const RankBinding& b, bool buffers_managed) {

@@ -16,8 +16,11 @@ namespace gmt {
 namespace comm {
 
 Kind parse_kind(const std::string& s);
-// GPU-aware MPI: GMT_MPI_GPU_AWARE=1/0 overrides; MPICH 3.3 ch3 here is not.
+// GPU-aware MPI: GMT_MPI_GPU_AWARE=1/0 overrides, else MPIX_Query_rocm_support
+// when the MPI library has it; MPICH 3.3 ch3 here has neither (not GPU-aware).
+// mpi-direct refuses device buffers unless this is true.
 bool mpi_gpu_aware();
+const char* mpi_gpu_aware_source();  // how mpi_gpu_aware() decided (for logs)
 // Resolve Auto for a device-resident exchange: rccl if one rank per GPU and
 // RCCL exists, else ipc; mpi-direct on the host backend, for managed
 // buffers or with a GPU-aware MPI.  GMT_TRANSPORT=<kind> overrides Auto.

@@ -136,8 +136,11 @@ def test_mpi_stencil_gt_divisibility_error():
     assert "must be divisor of domain size" in p.stdout
 
 
-_TEST_RE = re.compile(r"^TEST dim:(\d), (device |managed), buf:(\d); ([\d.]+), err=([\d.]+)$", re.M)
-_SUM_RE = re.compile(r"^TEST dim:(\d), (device |managed), buf:0; allreduce=([\d.]+)$", re.M)
+# the reference's fields, then optional bracketed tags where the timing
+# semantics differ from the reference's (csrc/apps/mpi_stencil2d_gt.cpp header)
+_TAGS = r"((?: \[[^\]]+\])*)"
+_TEST_RE = re.compile(r"^TEST dim:(\d), (device |managed), buf:(\d); ([\d.]+), err=([\d.]+)" + _TAGS + "$", re.M)
+_SUM_RE = re.compile(r"^TEST dim:(\d), (device |managed), buf:0; allreduce=([\d.]+)" + _TAGS + "$", re.M)
 
 
 @pytest.mark.parametrize("np_", [1, 2, 3])
@@ -147,14 +150,15 @@ def test_mpi_stencil2d_gt_all_variants(np_):
     assert f"n_global_deriv = {48 * np_}" in out and "n_global_other = 300" in out
     tests = _TEST_RE.findall(out)
     # 8 test_deriv lines in the reference order (mpi_stencil2d_gt.cc:692-716)
-    assert [(d, m, b) for d, m, b, _, _ in tests] == [
+    assert [(d, m, b) for d, m, b, _, _, _ in tests] == [
         ("0", "device ", "1"), ("0", "device ", "0"), ("0", "managed", "1"), ("0", "managed", "0"),
         ("1", "device ", "1"), ("1", "device ", "0"), ("1", "managed", "1"), ("1", "managed", "0")]
-    for *_, err in tests:
+    for *_, err, tags in tests:
         assert float(err) < 1e-5
+        assert tags == " [persistent buffers]"  # host backend: managed memory is plain host memory
     sums = _SUM_RE.findall(out)
-    assert [(d, m) for d, m, _ in sums] == [("0", "device "), ("0", "managed"),
-                                            ("1", "device "), ("1", "managed")]
+    assert [(d, m) for d, m, _, _ in sums] == [("0", "device "), ("0", "managed"),
+                                               ("1", "device "), ("1", "managed")]
     assert "WARNING" not in out  # all-reduce values checked against PI*n_other
 
 
@@ -164,7 +168,7 @@ def test_mpi_stencil2d_gt_transport_parity(transport):
                   f"--transport={transport}", "--host-init", "--host-verify", np=3).stdout
     tests = _TEST_RE.findall(out)
     assert len(tests) == 4
-    for *_, err in tests:
+    for *_, err, _tags in tests:
         assert float(err) < 1e-5
 
 
@@ -173,9 +177,18 @@ def test_mpi_stencil2d_gt_matrix_slice():
     out = run_app("mpi_stencil2d_gt", "32", "--iters=3", "--warmup=1", "--n-other=128", "--dim=1",
                   "--mem=managed", "--buf=0", np=2).stdout
     tests = _TEST_RE.findall(out)
-    assert [(d, m, b) for d, m, b, _, _ in tests] == [("1", "managed", "0")]
-    assert [(d, m) for d, m, _ in _SUM_RE.findall(out)] == [("1", "managed")]
+    assert [(d, m, b) for d, m, b, _, _, _ in tests] == [("1", "managed", "0")]
+    assert [(d, m) for d, m, _, _ in _SUM_RE.findall(out)] == [("1", "managed")]
     assert "n_iter         = 3" in out and "n_warmup       = 1" in out
+
+
+def test_mpi_stencil2d_gt_alloc_per_call_is_untagged():
+    """--alloc-per-call times the reference's per-call buffer creation: the TEST
+    lines then carry exactly the reference's fields."""
+    out = run_app("mpi_stencil2d_gt", "32", "3", "--n-other=128", "--no-managed", "--alloc-per-call",
+                  "--transport=mpi-host", np=2).stdout
+    tests = _TEST_RE.findall(out)
+    assert len(tests) == 4 and all(t[-1] == "" for t in tests)
 
 
 def test_mpi_stencil2d_gt_json(tmp_path):

@@ -109,6 +109,22 @@ def test_app_stencil2d_gt_err_norm(transport):
     assert len(re.findall(r"allreduce=", out)) >= 2
 
 
+def test_app_mpi_direct_refuses_device_memory():
+    """mpi-direct on hipMalloc buffers with this (non GPU-aware) MPICH is refused
+    with a clear error (the reference assumes Cray GTL / Spectrum
+    -gpu, /root/reference/CMakeLists.txt:42-47); managed buffers still pass."""
+    exe = os.path.join(BIN, "mpi_stencil2d_gt")
+    env = {k: v for k, v in os.environ.items() if k != "GMT_MPI_GPU_AWARE"}
+    p = subprocess.run([MPIRUN, "-np", "2", exe, "64", "3", "--tests=deriv", "--dim=0", "--mem=device",
+                        "--buf=0", "--transport=mpi-direct"], capture_output=True, text=True, timeout=120,
+                       cwd="/tmp", env=env)
+    assert p.returncode != 0, p.stdout
+    assert "mpi-direct was given device memory" in p.stdout and "not GPU-aware" in p.stdout, p.stdout
+    out = _app(["mpi_stencil2d_gt", "64", "3", "--tests=deriv", "--dim=0", "--mem=managed", "--buf=0",
+                "--n-other=300", "--transport=mpi-direct"], np_=2)
+    assert re.search(r"TEST dim:0, managed, buf:0; [0-9.]+, err=", out), out
+
+
 def test_app_mpi_daxpy_nvtx_sums():
     out = _app(["mpi_daxpy_nvtx_unmanaged", "--iters=2"], np_=2)
     assert len(re.findall(r"\d/2 ALLSUM", out)) == 2
