@@ -145,11 +145,16 @@ $(BINH)/%: $(OBJ)/apps/%.o $(COMM_OBJS) $(LIBH) $(LIBH_CCL)
 asan-host:
 	$(MAKE) BUILD=$(BUILD)/asan SAN="-fsanitize=address,undefined -fno-omit-frame-pointer -g" host-apps
 
-# tuning harness (standalone, not part of the libraries)
-sweep: $(BUILD)/bench/stream_sweep
+# tuning harnesses (standalone, not part of the libraries): stream_sweep, and
+# variant_bench — the A/B kernel variants checked and timed against libgmt
+sweep: $(BUILD)/bench/stream_sweep $(BUILD)/bench/variant_bench
 $(BUILD)/bench/stream_sweep: csrc/bench/stream_sweep.hip
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+$(BUILD)/bench/variant_bench: csrc/bench/variant_bench.hip $(KERNEL_HDRS) $(LIB)
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Icsrc/include -o $@ $< -L$(LIBDIR) -lgmt \
+	  -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
 .SECONDARY:
 

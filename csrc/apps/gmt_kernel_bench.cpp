@@ -82,13 +82,9 @@ int main(int argc, char** argv) {
     GMT_CHECK("fill", gmt_fill_poly(1, n, 1, 1.0, 1e-9, 0.0, 0.0, y.data(), n, s));
     char shape[64];
     std::snprintf(shape, sizeof(shape), "n=%zu", n);
-    for (int v = 1; v <= 6; ++v) {
-      gmt_daxpy_set_variant(v);
-      const double ms = time_ms(s, iters, [&] { GMT_CHECK("daxpy", gmt_daxpy(n, 1e-3, x.data(), y.data(), s)); });
-      report("daxpy", v, shape, ms, 24.0 * n);
-    }
-    gmt_daxpy_set_variant(0);
-    const double ms = time_ms(s, iters, [&] { GMT_CHECK("daxpy", gmt_blas_daxpy(n, 1e-3, x.data(), y.data(), s)); });
+    double ms = time_ms(s, iters, [&] { GMT_CHECK("daxpy", gmt_daxpy(n, 1e-3, x.data(), y.data(), s)); });
+    report("daxpy", 0, shape, ms, 24.0 * n);
+    ms = time_ms(s, iters, [&] { GMT_CHECK("daxpy", gmt_blas_daxpy(n, 1e-3, x.data(), y.data(), s)); });
     report("rocblas", 0, shape, ms, 24.0 * n);
   }
   if (only.find("hot") != std::string::npos) {
@@ -164,17 +160,11 @@ int main(int argc, char** argv) {
     GMT_CHECK("fill", gmt_fill_poly(0, ld, n + 2, 0.0, 1e-5, 0.0, 1e-5, un.data(), ld, s));
     char shape[64];
     std::snprintf(shape, sizeof(shape), "%lldx%lld", (long long)n, (long long)n);
-    // single-sweep kernel variants (the K-sweep kernel: --only=tb)
-    const std::string sec = cli.get("sections", "v");
-    for (int v = 1; v <= 9 && sec.find('v') != std::string::npos; ++v) {
-      if (v == 3 && n > 16384) continue;  // scalar reference kernel: too slow to matter
-      gmt_jacobi5_set_variant(v);
-      const double ms = time_ms(s, iters, [&] {
-        GMT_CHECK("jacobi", gmt_jacobi5(xo, n, 1, n, u.data(), un.data(), ld, nullptr, 0, 0.25, 0.0, nullptr, s));
-      });
-      report("jacobi5", v, shape, ms, 16.0 * n * n);
-    }
-    gmt_jacobi5_set_variant(0);
+    // single sweep (the K-sweep kernel: --only=tb; A/B variants: variant_bench)
+    const double ms = time_ms(s, iters, [&] {
+      GMT_CHECK("jacobi", gmt_jacobi5(xo, n, 1, n, u.data(), un.data(), ld, nullptr, 0, 0.25, 0.0, nullptr, s));
+    });
+    report("jacobi5", 0, shape, ms, 16.0 * n * n);
   }
   if (only.find("stencil") != std::string::npos) {
     // the reference's default deriv shapes: 1028 x 524288 (dim 0), 524288 x 1028 (dim 1)
@@ -182,18 +172,16 @@ int main(int argc, char** argv) {
     Buffer<double> in(static_cast<size_t>(a + 4) * b, GMT_SPACE_DEVICE), out(static_cast<size_t>(a) * b, GMT_SPACE_DEVICE);
     GMT_CHECK("fill", gmt_fill_poly(0, a + 4, b, 0.0, 1e-3, 0.0, 1e-3, in.data(), a + 4, s));
     const double c[5] = {1.0 / 12, -2.0 / 3, 0.0, 2.0 / 3, -1.0 / 12};
-    for (int v = 0; v <= 2; ++v) {
-      gmt_stencil5_set_variant(v);
-      double ms = time_ms(s, iters, [&] {
-        GMT_CHECK("d0", gmt_stencil5_2d(0, a, b, c, 128.0, in.data(), a + 4, out.data(), a, s));
-      });
-      report("stencil5", v, "dim0 1024x524288", ms, 16.0 * a * b);
-      ms = time_ms(s, iters, [&] {
-        GMT_CHECK("d1", gmt_stencil5_2d(1, b, a, c, 128.0, in.data(), b, out.data(), b, s));
-      });
-      report("stencil5", v, "dim1 524288x1024", ms, 16.0 * a * b);
-    }
-    gmt_stencil5_set_variant(0);
+    // bytes: the input (n + 4 rows / columns) read once, the output written once
+    const double bytes = 8.0 * ((a + 4) * b + a * b);
+    double ms = time_ms(s, iters, [&] {
+      GMT_CHECK("d0", gmt_stencil5_2d(0, a, b, c, 128.0, in.data(), a + 4, out.data(), a, s));
+    });
+    report("stencil5", 0, "dim0 1028->1024 x 524288", ms, bytes);
+    ms = time_ms(s, iters, [&] {
+      GMT_CHECK("d1", gmt_stencil5_2d(1, b, a, c, 128.0, in.data(), b, out.data(), b, s));
+    });
+    report("stencil5", 1, "dim1 524288 x 1028->1024", ms, bytes);
   }
   if (only.find("pack") != std::string::npos) {
     // dim-0 halo faces of the reference's field: 2 rows x 524288 columns, pitch 1028

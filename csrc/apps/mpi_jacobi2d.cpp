@@ -12,7 +12,7 @@
 //   --dims=PYxPX            process grid (default: minimise halo bytes)
 //   --transport=auto|rccl|ipc|mpi-host|mpi-direct
 //   --overlap=auto          time overlapped and serial passes once, keep the faster
-//   --no-overlap --graph --periodic --warmup=W --variant=V (1 reg, 2 lds, 3 scalar, 9 pt)
+//   --no-overlap --graph --periodic --warmup=W
 //   --tblock                temporal blocking (gmt_jacobi5tb): K sweeps per memory pass
 //                           and per (K-wide) halo exchange
 //   --tsteps=K              sweeps per fused pass with --tblock (2-24; default 2; odd
@@ -102,7 +102,6 @@ int main(int argc, char** argv) {
   c.overlap = !cli.flag("no-overlap");
   c.overlap_auto = cli.get("overlap", "") == "auto";  // --overlap=auto: time both, keep the faster
   c.graph = cli.flag("graph");
-  c.variant = static_cast<int>(cli.geti("variant", 0));
   c.tblock = cli.has("tblock") && cli.get("tblock", "1") != "0";
   if (c.tblock) c.tsteps = static_cast<int>(cli.geti("tsteps", 2));
   c.wg_waves = static_cast<int>(cli.geti("wg-strips", 0));

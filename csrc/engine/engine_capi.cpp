@@ -55,7 +55,6 @@ void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank,
   c.graph = o.graph != 0;
   c.tblock = o.tsteps > 1;
   c.tsteps = o.tsteps;
-  c.variant = o.variant;
   c.wg_waves = o.wg_waves;
   c.seg_rows = o.seg_rows;
   c.exact = o.exact;

@@ -96,7 +96,6 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   GMT_CHECK("event", gmt_rt_event_create(&ev_packed_, 0));
   const char* cap = std::getenv("GMT_CORE_AFTER_PACK");
   core_after_pack_ = !(cap && cap[0] == '0');
-  if (c.variant) gmt_jacobi5_set_variant(c.variant);
 
   // deterministic, decomposition-independent initial field and Dirichlet
   // ring: u(x, y) = x^3 + y^2 at global ghost-inclusive coordinates * h

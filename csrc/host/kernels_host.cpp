@@ -14,21 +14,12 @@
 
 #include "gmt/kernels.h"
 
-namespace {
-int g_variant = 0;
-int g_daxpy_variant = 0;
-}
-
 extern "C" {
 
 int gmt_daxpy(int64_t n, double a, const double* x, double* y, void*) {
   for (int64_t i = 0; i < n; ++i) y[i] = a * x[i] + y[i];
   return 0;
 }
-
-void gmt_daxpy_set_variant(int v) { g_daxpy_variant = v; }
-void gmt_stencil5_set_variant(int) {}
-int gmt_daxpy_get_variant(void) { return g_daxpy_variant; }
 
 int gmt_stencil5_1d(int64_t n_out, const double* c, double scale, const double* in, double* out,
                     void*) {
@@ -206,8 +197,6 @@ int gmt_jacobi5tb(const gmt_tb_opts* o, int n_rect, const int64_t* rects, const 
   return host_xk(K, n_rect, rects, dom, mask, u, un, ld);
 }
 
-void gmt_jacobi5_set_variant(int v) { g_variant = v; }
-int gmt_jacobi5_get_variant(void) { return g_variant; }
 
 const char* gmt_error_string(int err) {
   switch (err) {

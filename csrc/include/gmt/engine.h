@@ -26,7 +26,6 @@ typedef struct gmt_engine_opts {
   int overlap;  /* 0 off, 1 halo exchange overlapped with the core pass, 2 auto (time both once) */
   int graph;    /* 1: capture the per-parity passes into hipGraphs */
   int tsteps;   /* sweeps per fused pass and per halo exchange: 1 (or 0) = single sweeps, 2..16 */
-  int variant;  /* single-sweep kernel variant (gmt_jacobi5_set_variant; 0 = default) */
   int wg_waves; /* temporal-blocking kernel: waves per workgroup (0 = auto) */
   int seg_rows; /* temporal-blocking kernel: output rows per workgroup (0 = auto) */
   int exact;    /* -1 / 0: power-of-two scaled levels when the field bound allows (auto),

@@ -48,7 +48,6 @@ struct JacobiConfig {
   // one GPU: serial 4-8 % faster, profiles/r01_frame.md); measure it.
   bool overlap_auto = false;
   bool graph = false;
-  int variant = 0;                               // gmt_jacobi5_set_variant
   // temporal blocking: tsteps (2-24) sweeps per memory pass (gmt_jacobi5tb;
   // odd counts above 10 round down) and per halo exchange (ghost width
   // tsteps, corners in the same

@@ -24,9 +24,6 @@ extern "C" {
 
 /* ---- K1/K2: y <- a*x + y (fp64).  reference: daxpy.cu:73, mpi_daxpy_gt.cc:81 */
 int gmt_daxpy(int64_t n, double a, const double* x, double* y, void* stream);
-/* DAXPY kernel variant for A/B measurement (0 = default; see daxpy.hip) */
-void gmt_daxpy_set_variant(int variant);
-int gmt_daxpy_get_variant(void);
 
 /* ---- K3: 1-D 5-tap stencil, out[i] = scale * sum_k c[k]*in[i+k], k=0..4.
  *      `in` has n_out+4 elements.  reference: mpi_stencil_gt.cc:54-59 */
@@ -40,10 +37,6 @@ int gmt_stencil5_1d(int64_t n_out, const double* coef5, double scale,
 int gmt_stencil5_2d(int dim, int64_t nx_out, int64_t ny_out, const double* coef5,
                     double scale, const double* in, int64_t ld_in, double* out,
                     int64_t ld_out, void* stream);
-
-/* 0 = default (per-thread dim 0, register window dim 1), 1 = register-window
- * kernels, 2 = per-thread kernels (A/B) */
-void gmt_stencil5_set_variant(int variant);
 
 /* ---- K6/K7/K8: batched strided 2-D copy (halo pack / unpack, fused L+R).
  *      Each descriptor copies `height` rows of `width` elements of
@@ -129,12 +122,8 @@ int gmt_jacobi5tb_supported(int sweeps);
 int gmt_jacobi5tb(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, const int64_t* dom,
                   int halo_mask, const double* u, double* un, int64_t ld, int64_t nrows, void* stream);
 
-/* Kernel variant selection for A/B measurement: 0 = auto, 1 = register
- * sliding window (vector x2, W/E from L1), 2 = LDS-tiled, 3 = scalar
- * reference kernel, 4-8 = register window with lane-exchanged W/E
- * neighbours (DPP / shfl, 32-128 rows per tile, see jacobi5.hip). */
-void gmt_jacobi5_set_variant(int variant);
-int gmt_jacobi5_get_variant(void);
+/* One kernel per entry point: the variants the defaults were chosen against
+ * are measured by csrc/bench/variant_bench.hip, not shipped in this ABI. */
 
 /* ---- misc */
 const char* gmt_error_string(int err);

@@ -248,8 +248,10 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   // steady-state step issues, so every wait below counts the same
   // (SPS + DPS) P younger memory operations
   if constexpr (kIn) {
+    // (each dummy store gets its own out-of-range row — rows ys - 3K - P ..
+    // ys - 3K - 1 — so the compiler cannot merge identical stores)
     static_for<0, kP>([&](auto I) {
-      store_step(0, d3{0.0, 0.0, 0.0});  // row ys - 3K: out of range
+      store_step(decltype(I)::value - kP, d3{0.0, 0.0, 0.0});
       dma(decltype(I)::value, decltype(I)::value);
     });
   }

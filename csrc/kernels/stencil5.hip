@@ -8,17 +8,21 @@
 //
 // Layout: x contiguous ("dim 0"), y strided ("dim 1") — see gmt/kernels.h.
 //
-// dim 0 (taps along the contiguous axis): each lane produces 2 outputs from
-// three overlapping 16-B loads (in[2t..2t+5]); the overlap is served by L1,
-// so HBM sees each input byte once.  A block covers 512 outputs of ROWS0 rows.
+// dim 0 (taps along the contiguous axis): stencil5_pt<0>, one output pair
+// per thread, the overlapping loads served by L1 (6.34 TB/s effective).
 //
-// Variant 1 (kept for A/B; variant 2, below, is the default):
-// dim 1 (taps along the strided axis): each lane owns 2 adjacent columns and
-// walks down ROWS1 rows keeping a 5-row register window, so every input row
-// is loaded once per column strip (+4 halo rows per strip => (R+4)/R reads).
-// No LDS: the reuse is in registers, exactly where a row-walking lane needs it.
+// dim 1 (taps along the strided axis): stencil5_d1_dma.  One wave owns a
+// strip of 128 * CPL columns and walks down a segment of L output rows with
+// a 5-row register window; input rows arrive by buffer->LDS DMA into a ring
+// of P + 1 slots, P rows ahead (the jacobi5tb.hip memory pipeline).  The
+// round-1 register-window kernel (now in csrc/bench/variant_bench.hip) issued
+// its unrolled loads in bursts and drained them to vmcnt(0..3) every 8 rows:
+// 85% of wave cycles waiting (rocprofv3 --pmc, profiles/r02_pmc/), 4.92 TB/s.
 #include "common.hpp"
 #include "gmt/kernels.h"
+#include "stencil5_d1.hpp"
+
+#include <algorithm>
 
 namespace gmt {
 
@@ -26,83 +30,8 @@ struct Coef5 {
   double c[5];
 };
 
-constexpr int ROWS0 = 4;   // rows per block, dim-0 kernel
-constexpr int ROWS1 = 32;  // rows per column strip, dim-1 kernel
 
-__global__ __launch_bounds__(kBlock) void stencil5_d0_vec(int64_t nx_out, int64_t ny,
-                                                          Coef5 cf, double scale,
-                                                          const double* __restrict__ in,
-                                                          int64_t ld_in,
-                                                          double* __restrict__ out,
-                                                          int64_t ld_out, int64_t nbx) {
-  const int64_t b = blockIdx.x;
-  const int64_t bx = b % nbx, by = b / nbx;
-  const int64_t x = (bx * kBlock + threadIdx.x) * 2;
-  if (x >= nx_out) return;
-  const double c0 = cf.c[0] * scale, c1 = cf.c[1] * scale, c2 = cf.c[2] * scale,
-               c3 = cf.c[3] * scale, c4 = cf.c[4] * scale;
-  const int64_t y0 = by * ROWS0;
-  const bool full = (x + 1 < nx_out);
-#pragma unroll
-  for (int r = 0; r < ROWS0; ++r) {
-    const int64_t y = y0 + r;
-    if (y >= ny) break;
-    const double* p = in + y * ld_in + x;
-    if (full) {
-      const d2 a = ld2(p), m = ld2(p + 2), e = ld2(p + 4);
-      d2 o;
-      o.x = c0 * a.x + c1 * a.y + c2 * m.x + c3 * m.y + c4 * e.x;
-      o.y = c0 * a.y + c1 * m.x + c2 * m.y + c3 * e.x + c4 * e.y;
-      st2(out + y * ld_out + x, o);
-    } else {
-      out[y * ld_out + x] = c0 * p[0] + c1 * p[1] + c2 * p[2] + c3 * p[3] + c4 * p[4];
-    }
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void stencil5_d1_vec(int64_t nx, int64_t ny_out,
-                                                          Coef5 cf, double scale,
-                                                          const double* __restrict__ in,
-                                                          int64_t ld_in,
-                                                          double* __restrict__ out,
-                                                          int64_t ld_out, int64_t nbx) {
-  const int64_t b = blockIdx.x;
-  const int64_t bx = b % nbx, by = b / nbx;
-  const int64_t x = (bx * kBlock + threadIdx.x) * 2;
-  if (x >= nx) return;
-  const double c0 = cf.c[0] * scale, c1 = cf.c[1] * scale, c2 = cf.c[2] * scale,
-               c3 = cf.c[3] * scale, c4 = cf.c[4] * scale;
-  const int64_t y0 = by * ROWS1;
-  const int64_t nrows = (ny_out - y0) < ROWS1 ? (ny_out - y0) : ROWS1;
-  const double* p = in + y0 * ld_in + x;
-  double* q = out + y0 * ld_out + x;
-  if (x + 1 < nx) {
-    d2 w0 = ld2(p), w1 = ld2(p + ld_in), w2 = ld2(p + 2 * ld_in), w3 = ld2(p + 3 * ld_in);
-    if (nrows == ROWS1) {
-#pragma unroll 8
-      for (int r = 0; r < ROWS1; ++r) {
-        const d2 w4 = ld2(p + (r + 4) * ld_in);
-        st2_nt(q + r * ld_out, c0 * w0 + c1 * w1 + c2 * w2 + c3 * w3 + c4 * w4);
-        w0 = w1; w1 = w2; w2 = w3; w3 = w4;
-      }
-    } else {
-      for (int64_t r = 0; r < nrows; ++r) {
-        const d2 w4 = ld2(p + (r + 4) * ld_in);
-        st2_nt(q + r * ld_out, c0 * w0 + c1 * w1 + c2 * w2 + c3 * w3 + c4 * w4);
-        w0 = w1; w1 = w2; w2 = w3; w3 = w4;
-      }
-    }
-  } else {  // odd last column
-    double w0 = p[0], w1 = p[ld_in], w2 = p[2 * ld_in], w3 = p[3 * ld_in];
-    for (int64_t r = 0; r < nrows; ++r) {
-      const double w4 = p[(r + 4) * ld_in];
-      q[r * ld_out] = c0 * w0 + c1 * w1 + c2 * w2 + c3 * w3 + c4 * w4;
-      w0 = w1; w1 = w2; w2 = w3; w3 = w4;
-    }
-  }
-}
-
-// Per-thread kernels (variant 2; default for dim 0): one output pair per thread, 64 x 4 threads per
+// Per-thread kernels (dim 0 default; dim 1 fallback): one output pair per thread, 64 x 4 threads per
 // block (128 columns x 4 rows), XCD-swizzled so the tiles that share input
 // rows sit on one XCD's L2, nontemporal stores (the derivative is written
 // once and not re-read by this kernel).  Same structure as the measured
@@ -138,8 +67,6 @@ __global__ __launch_bounds__(kBlock) void stencil5_pt(int64_t nx_out, int64_t ny
   }
 }
 
-static int g_stencil_variant = 0;
-
 // Generic fallback for unaligned views: one output per lane.
 __global__ __launch_bounds__(kBlock) void stencil5_scalar(int dim, int64_t nx_out,
                                                           int64_t ny_out, Coef5 cf,
@@ -165,7 +92,30 @@ static Coef5 make_coef(const double* c5) {
 
 }  // namespace gmt
 
-extern "C" void gmt_stencil5_set_variant(int v) { gmt::g_stencil_variant = v; }
+namespace {
+
+// dim 1 through the DMA pipeline: segment rows per wave, chunks per lane
+template <int CPL, bool ODD>
+int launch_d1(int64_t nx, int64_t ny_out, const gmt::Coef5& cf, double scale, const double* in, int64_t ld_in,
+              double* out, int64_t ld_out, int64_t L, hipStream_t s) {
+  using namespace gmt::d1;
+  Args a{};
+  a.nx = nx;
+  a.ny_out = ny_out;
+  a.ld_in = ld_in;
+  a.ld_out = ld_out;
+  for (int k = 0; k < 5; ++k) a.c[k] = cf.c[k] * scale;
+  a.nstrip = (nx + 128 * CPL - 1) / (128 * CPL);
+  a.seg = static_cast<int>(L);
+  a.nseg = (ny_out + L - 1) / L;
+  a.nsteps = static_cast<int>((L + 4 + kU - 1) / kU * kU);
+  const int64_t nb = (a.nstrip + kNW - 1) / kNW * a.nseg;
+  const size_t smem = static_cast<size_t>(kNW) * kRS * CPL * gmt::kWave * 16;
+  gmt::d1::stencil5_d1_dma<CPL, ODD><<<gmt::grid_1d(nb), kNW * gmt::kWave, smem, s>>>(a, in, out, nb);
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // namespace
 
 extern "C" int gmt_stencil5_2d(int dim, int64_t nx_out, int64_t ny_out, const double* coef5,
                                double scale, const double* in, int64_t ld_in, double* out,
@@ -176,11 +126,20 @@ extern "C" int gmt_stencil5_2d(int dim, int64_t nx_out, int64_t ny_out, const do
   hipStream_t s = static_cast<hipStream_t>(stream);
   const Coef5 cf = make_coef(coef5);
   const bool vec_ok = aligned16(in) && aligned16(out) && (ld_in % 2 == 0) && (ld_out % 2 == 0);
-  // default: per-thread kernel for dim 0 (taps along the contiguous axis,
-  // 6.34 TB/s), register window for dim 1 (a 5-row window per lane beats
-  // five L2-served row loads per thread: 1.87 vs 2.05 ms at 1024 x 524288)
-  const bool pt = g_stencil_variant == 2 || (g_stencil_variant == 0 && dim == 0);
-  if (vec_ok && pt) {
+  if (dim == 1 && vec_ok) {
+    // segment rows: the 32-bit buffer offsets must reach (L + 4 + P + U) rows
+    // of the wider pitch; 128 rows amortise the 4-row input halo to 3 %
+    const int64_t ld = ld_in > ld_out ? ld_in : ld_out;
+    const int64_t lmax = (int64_t(1) << 31) / (ld * 8) - 4 - d1::kP - d1::kU;
+    const int64_t L = std::min<int64_t>(std::min<int64_t>(128, ny_out), lmax);
+    if (L >= 8) {
+      if (nx_out % 2) return launch_d1<1, true>(nx_out, ny_out, cf, scale, in, ld_in, out, ld_out, L, s);
+      return launch_d1<1, false>(nx_out, ny_out, cf, scale, in, ld_in, out, ld_out, L, s);
+    }
+  }
+  if (vec_ok) {
+    // one output pair per thread (dim 0: the default; dim 1: rows too long for
+    // the DMA pipeline's 32-bit offsets)
     const int64_t nbx = (nx_out + 2 * kWave - 1) / (2 * kWave);
     const int64_t nb = nbx * ((ny_out + kBlock / kWave - 1) / (kBlock / kWave));
     if (dim == 0)
@@ -189,17 +148,6 @@ extern "C" int gmt_stencil5_2d(int dim, int64_t nx_out, int64_t ny_out, const do
     else
       stencil5_pt<1><<<grid_1d(nb), kBlock, 0, s>>>(nx_out, ny_out, cf, scale, in, ld_in, out,
                                                     ld_out, nbx, nb);
-  } else if (vec_ok) {
-    const int64_t nbx = (nx_out + 2 * kBlock - 1) / (2 * kBlock);
-    if (dim == 0) {
-      const int64_t nby = (ny_out + ROWS0 - 1) / ROWS0;
-      stencil5_d0_vec<<<grid_1d(nbx * nby), kBlock, 0, s>>>(nx_out, ny_out, cf, scale, in,
-                                                             ld_in, out, ld_out, nbx);
-    } else {
-      const int64_t nby = (ny_out + ROWS1 - 1) / ROWS1;
-      stencil5_d1_vec<<<grid_1d(nbx * nby), kBlock, 0, s>>>(nx_out, ny_out, cf, scale, in,
-                                                             ld_in, out, ld_out, nbx);
-    }
   } else {
     const int64_t nb = (nx_out * ny_out + kBlock - 1) / kBlock;
     stencil5_scalar<<<grid_1d(nb), kBlock, 0, s>>>(dim, nx_out, ny_out, cf, scale, in, ld_in,

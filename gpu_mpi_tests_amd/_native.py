@@ -73,11 +73,6 @@ _SIGS = {
     ),
     "gmt_jacobi5tb_supported": (c_int, [c_int]),
     "gmt_jacobi5tb": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_vp]),
-    "gmt_jacobi5_set_variant": (None, [c_int]),
-    "gmt_daxpy_set_variant": (None, [c_int]),
-    "gmt_stencil5_set_variant": (None, [c_int]),
-    "gmt_daxpy_get_variant": (c_int, []),
-    "gmt_jacobi5_get_variant": (c_int, []),
     "gmt_error_string": (ctypes.c_char_p, [c_int]),
     "gmt_device_synchronize": (c_int, []),
     "gmt_build_info": (ctypes.c_char_p, []),

@@ -37,7 +37,7 @@ _libs: dict[str, ctypes.CDLL] = {}
 class EngineOpts(ctypes.Structure):
     """gmt_engine_opts (csrc/include/gmt/engine.h)."""
     _fields_ = [(n, ctypes.c_int) for n in
-                ("periodic", "overlap", "graph", "tsteps", "variant", "wg_waves", "seg_rows", "exact")]
+                ("periodic", "overlap", "graph", "tsteps", "wg_waves", "seg_rows", "exact")]
 
 
 class EngineError(RuntimeError):
@@ -131,7 +131,7 @@ class NativeJacobi:
 
     def __init__(self, ny: int, nx: int, env: "gdist.DistEnv | None" = None,
                  dims: tuple[int, int] | None = None, periodic: bool = False,
-                 overlap: "bool | str" = True, graph: bool = True, variant: int = 0,
+                 overlap: "bool | str" = True, graph: bool = True,
                  tblock: bool | int = False, wg_waves: int = 0, seg_rows: int = 0, exact: int = -1,
                  transport: str = "auto"):
         from .parallel.decomp import choose_dims
@@ -170,7 +170,7 @@ class NativeJacobi:
         # overlap: True / False / "auto" (time both once, every rank keeps the faster)
         auto = overlap == "auto"
         opts = EngineOpts(periodic=int(bool(periodic)), overlap=2 if auto else int(bool(overlap)),
-                          graph=int(bool(graph)), tsteps=ks, variant=int(variant), wg_waves=int(wg_waves),
+                          graph=int(bool(graph)), tsteps=ks, wg_waves=int(wg_waves),
                           seg_rows=int(seg_rows), exact=int(exact))
         with _StdoutToStderr():
             self.h = self.lib.gmt_engine_jacobi_create(ny, nx, py, px, e.rank, e.world_size, transport,

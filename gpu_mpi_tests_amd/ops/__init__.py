@@ -17,7 +17,6 @@ from .kernels import (  # noqa: F401
     jacobi5xk,
     jacobi5tb,
     tb_supported,
-    set_jacobi_variant,
     stencil5_1d,
     stencil5_2d,
     sum_axis,

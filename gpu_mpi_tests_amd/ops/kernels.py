@@ -318,9 +318,3 @@ def jacobi5xk(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[i
               dom: tuple[int, int, int, int], halo_mask: int = 0) -> None:
     """``k`` fused Laplace sweeps with the default launch: :func:`jacobi5tb`."""
     jacobi5tb(k, u, un, rects, dom, halo_mask)
-
-
-def set_jacobi_variant(v: int) -> None:
-    """0 auto, 1 register window (W/E from L1), 2 LDS-tiled, 3 scalar, 4-8 lane-exchange
-    register windows (DPP / shfl, 32-128 rows per tile) — A/B measurement."""
-    _native.lib().gmt_jacobi5_set_variant(int(v))
