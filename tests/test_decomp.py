@@ -2,7 +2,7 @@ import pytest
 
 from gpu_mpi_tests_amd.parallel.decomp import CartDecomp, choose_dims
 from gpu_mpi_tests_amd.parallel.dist import select_device
-from gpu_mpi_tests_amd.parallel.field import Field2D
+from torch_ref.field import Field2D
 
 
 def test_choose_dims_prefers_row_splits():

@@ -10,8 +10,8 @@ from mp_util import run_dist
 
 def _halo_check(env, ny, nx, dims, gy, gx, staging):
     from gpu_mpi_tests_amd.parallel.decomp import CartDecomp
-    from gpu_mpi_tests_amd.parallel.field import Field2D
-    from gpu_mpi_tests_amd.parallel.halo import HaloExchanger
+    from torch_ref.field import Field2D
+    from torch_ref.halo import HaloExchanger
 
     d = CartDecomp.create(env.world_size, env.rank, ny, nx, dims)
     (oy, ly), (ox, lx) = d.local_y, d.local_x
@@ -56,7 +56,7 @@ def test_halo_exchange_staged(staging, port):
 
 
 def _jacobi_run(env, n, dims, overlap, steps, rhs):
-    from gpu_mpi_tests_amd.models.jacobi import Jacobi2D
+    from torch_ref.jacobi import Jacobi2D
 
     s = Jacobi2D(n, n + 6, env=env, dims=dims, overlap=overlap, rhs=rhs)
     s.run(steps)
@@ -75,7 +75,7 @@ def test_jacobi_distributed_equals_serial(world, dims, overlap, port):
     g_dist, res_dist = outs[0]
     # serial reference with the same initial data: assemble the per-rank seeded init globally
     from gpu_mpi_tests_amd.parallel.decomp import CartDecomp
-    from gpu_mpi_tests_amd.parallel.field import Field2D
+    from torch_ref.field import Field2D
     from gpu_mpi_tests_amd.ops import reference as ref
 
     nx = n + 6

@@ -226,7 +226,7 @@ def test_jacobi5_rects_frame():
 
 
 def test_jacobi_model_single_gpu_matches_cpu():
-    from gpu_mpi_tests_amd.models.jacobi import Jacobi2D
+    from torch_ref.jacobi import Jacobi2D
     from gpu_mpi_tests_amd.parallel import dist as gdist
 
     env_gpu = gdist.DistEnv(device=torch.device("cuda", 0), n_devices=1)

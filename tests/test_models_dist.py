@@ -14,7 +14,7 @@ def _port():
 
 
 def _deriv(env, dim, n_local, n_other):
-    from gpu_mpi_tests_amd.models import deriv
+    from torch_ref import deriv
 
     r = deriv.run_deriv(dim, n_local, n_other, n_iter=3, n_warmup=1, env=env)
     t, err = deriv.run_sum(dim, n_local, n_other, n_iter=3, n_warmup=1, env=env)
@@ -35,7 +35,7 @@ def test_deriv_distributed_exact(world, dim):
 
 
 def _daxpy(env, n_per_node):
-    from gpu_mpi_tests_amd.models import daxpy_dist
+    from torch_ref import daxpy_dist
 
     r = daxpy_dist.run(n_per_node, env=env)
     return r.n, r.sum, r.allsum, r.lines(env.rank, env.world_size)

@@ -17,9 +17,9 @@ from dataclasses import dataclass
 import torch
 import torch.distributed as dist
 
-from .. import ops
-from ..parallel import dist as gdist
-from ..utils.trace import range_ctx
+from gpu_mpi_tests_amd import ops
+from gpu_mpi_tests_amd.parallel import dist as gdist
+from gpu_mpi_tests_amd.utils.trace import range_ctx
 
 MB = 1024 * 1024
 

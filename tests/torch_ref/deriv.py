@@ -22,12 +22,12 @@ from dataclasses import dataclass, field
 import torch
 import torch.distributed as dist
 
-from .. import ops
-from ..ops.reference import DERIV5
-from ..parallel import dist as gdist
-from ..parallel.decomp import CartDecomp
-from ..parallel.field import Field2D
-from ..parallel.halo import HaloExchanger
+from gpu_mpi_tests_amd import ops
+from gpu_mpi_tests_amd.ops.reference import DERIV5
+from gpu_mpi_tests_amd.parallel import dist as gdist
+from gpu_mpi_tests_amd.parallel.decomp import CartDecomp
+from .field import Field2D
+from .halo import HaloExchanger
 
 PI = 3.141592653598793  # the reference's constant (mpi_stencil2d_gt.cc:30)
 

@@ -34,8 +34,8 @@ from dataclasses import dataclass
 import torch
 import torch.distributed as dist
 
-from .. import ops
-from .decomp import CartDecomp
+from gpu_mpi_tests_amd import ops
+from gpu_mpi_tests_amd.parallel.decomp import CartDecomp
 from .field import Field2D
 
 TAG_LOW, TAG_HIGH, TAG_Y = 456, 123, 1000

@@ -25,11 +25,11 @@ from __future__ import annotations
 
 import torch
 
-from .. import ops
-from ..parallel import dist as gdist
-from ..parallel.decomp import CartDecomp
-from ..parallel.field import Field2D
-from ..parallel.halo import HaloExchanger
+from gpu_mpi_tests_amd import ops
+from gpu_mpi_tests_amd.parallel import dist as gdist
+from gpu_mpi_tests_amd.parallel.decomp import CartDecomp
+from .field import Field2D
+from .halo import HaloExchanger
 
 
 class Jacobi2D:
