@@ -96,47 +96,127 @@ class MpiTransport : public Transport {
 };
 
 // ------------------------------------------------------------------ mpi-host
+// Host-staged exchange, pipelined in chunks (reference: the staged path of
+// mpi_stencil2d_sycl.cc:248-283 and mpi_stencil2d_gt.cc:147-176,229-252).
+//   start: post every receive (one MPI_Irecv per chunk into pinned staging)
+//          and enqueue every D2H chunk copy on the caller's stream, an event
+//          after each; no host wait, so the caller's kernels queue right away.
+//   wait:  send each chunk as soon as its D2H event has completed (MPI keeps
+//          the chunks of one message in order: same peer, tag, communicator),
+//          and enqueue each received chunk's H2D copy as soon as it lands, so
+//          D2H, the wire and H2D of different chunks overlap.
+// Receive staging is double-buffered across exchanges: the next exchange's
+// receives never wait for this one's H2D copies to drain.
 class MpiHostExchange : public Exchange {
  public:
+  static constexpr size_t kChunk = size_t(1) << 20;
+
   MpiHostExchange(MPI_Comm c, std::vector<Msg> r, std::vector<Msg> s)
       : c_(c), recvs_(std::move(r)), sends_(std::move(s)) {
-    for (auto& m : recvs_) rstage_.emplace_back(m.bytes, GMT_SPACE_PINNED);
+    for (int set = 0; set < 2; ++set)
+      for (auto& m : recvs_) rstage_[set].emplace_back(m.bytes, GMT_SPACE_PINNED);
     for (auto& m : sends_) sstage_.emplace_back(m.bytes, GMT_SPACE_PINNED);
-    GMT_CHECK("event", gmt_rt_event_create(&h2d_done_, 0));
-  }
-  ~MpiHostExchange() override { gmt_rt_event_destroy(h2d_done_); }
-  void start(gmt_stream_t s) override {
-    // the previous exchange's H2D copies must have drained the recv staging
-    if (armed_) GMT_CHECK("staging reuse", gmt_rt_event_synchronize(h2d_done_));
-    for (size_t i = 0; i < recvs_.size(); ++i) {
-      reqs_.emplace_back();
-      irecv(rstage_[i].data(), recvs_[i].bytes, recvs_[i].peer, recvs_[i].tag, c_, &reqs_.back());
-    }
     for (size_t i = 0; i < sends_.size(); ++i)
-      GMT_CHECK("stage D2H", gmt_rt_memcpy_async(sstage_[i].data(), sends_[i].buf,
-                                                 sends_[i].bytes, s));
-    GMT_CHECK("stage sync", gmt_rt_stream_synchronize(s));
-    for (size_t i = 0; i < sends_.size(); ++i) {
-      reqs_.emplace_back();
-      isend(sstage_[i].data(), sends_[i].bytes, sends_[i].peer, sends_[i].tag, c_, &reqs_.back());
+      for (size_t off = 0; off < sends_[i].bytes || off == 0; off += kChunk) {
+        schunks_.push_back({i, off, std::min(kChunk, sends_[i].bytes - off)});
+        if (sends_[i].bytes == 0) break;
+      }
+    for (size_t i = 0; i < recvs_.size(); ++i)
+      for (size_t off = 0; off < recvs_[i].bytes || off == 0; off += kChunk) {
+        rchunks_.push_back({i, off, std::min(kChunk, recvs_[i].bytes - off)});
+        if (recvs_[i].bytes == 0) break;
+      }
+    events_.resize(schunks_.size(), nullptr);
+    for (auto& e : events_) GMT_CHECK("event", gmt_rt_event_create(&e, 0));
+    for (auto& e : h2d_done_) GMT_CHECK("event", gmt_rt_event_create(&e, 0));
+  }
+  ~MpiHostExchange() override {
+    for (auto& e : events_) gmt_rt_event_destroy(e);
+    for (auto& e : h2d_done_) gmt_rt_event_destroy(e);
+  }
+  void start(gmt_stream_t s) override {
+    cur_ ^= 1;
+    // the exchange before last drained this staging set with its H2D copies
+    if (armed_[cur_]) GMT_CHECK("staging reuse", gmt_rt_event_synchronize(h2d_done_[cur_]));
+    rreqs_.assign(rchunks_.size(), MPI_REQUEST_NULL);
+    for (size_t k = 0; k < rchunks_.size(); ++k) {
+      const Chunk& ch = rchunks_[k];
+      const Msg& m = recvs_[ch.msg];
+      irecv(rstage_[cur_][ch.msg].data() + ch.off, ch.len, m.peer, m.tag, c_, &rreqs_[k]);
+    }
+    for (size_t k = 0; k < schunks_.size(); ++k) {
+      const Chunk& ch = schunks_[k];
+      const Msg& m = sends_[ch.msg];
+      if (ch.len)
+        GMT_CHECK("stage D2H", gmt_rt_memcpy_async(sstage_[ch.msg].data() + ch.off,
+                                                   static_cast<const char*>(m.buf) + ch.off, ch.len, s));
+      GMT_CHECK("event", gmt_rt_event_record(events_[k], s));
     }
   }
   void wait(gmt_stream_t s) override {
-    waitall(reqs_, "mpi-host exchange");
-    for (size_t i = 0; i < recvs_.size(); ++i)
-      GMT_CHECK("stage H2D", gmt_rt_memcpy_async(recvs_[i].buf, rstage_[i].data(),
-                                                 recvs_[i].bytes, s));
-    GMT_CHECK("event", gmt_rt_event_record(h2d_done_, s));
-    armed_ = true;
+    std::vector<MPI_Request> sreqs;
+    sreqs.reserve(schunks_.size());
+    size_t next = 0, pending = rchunks_.size();
+    std::vector<int> idx(rchunks_.size() ? rchunks_.size() : 1);
+    auto land = [&](int n) {
+      for (int q = 0; q < n; ++q) {
+        const Chunk& ch = rchunks_[idx[q]];
+        if (ch.len)
+          GMT_CHECK("stage H2D", gmt_rt_memcpy_async(static_cast<char*>(recvs_[ch.msg].buf) + ch.off,
+                                                     rstage_[cur_][ch.msg].data() + ch.off, ch.len, s));
+      }
+      pending -= static_cast<size_t>(n);
+    };
+    auto send = [&](size_t k) {
+      const Chunk& ch = schunks_[k];
+      const Msg& m = sends_[ch.msg];
+      sreqs.emplace_back();
+      isend(sstage_[ch.msg].data() + ch.off, ch.len, m.peer, m.tag, c_, &sreqs.back());
+    };
+    while (next < schunks_.size() || pending > 0) {
+      bool progress = false;
+      while (next < schunks_.size() && gmt_rt_event_query(events_[next]) == 0) {
+        send(next++);
+        progress = true;
+      }
+      if (pending > 0) {
+        int n = 0;
+        GMT_MPI_CHECK(MPI_Testsome(static_cast<int>(rreqs_.size()), rreqs_.data(), &n, idx.data(),
+                                   MPI_STATUSES_IGNORE));
+        if (n > 0 && n != MPI_UNDEFINED) {
+          land(n);
+          progress = true;
+        }
+      }
+      if (progress) continue;
+      if (next < schunks_.size()) {  // nothing landed: block on the next D2H chunk
+        GMT_CHECK("stage D2H wait", gmt_rt_event_synchronize(events_[next]));
+        send(next++);
+      } else {  // every chunk is sent: block on the receives
+        int n = 0;
+        GMT_MPI_CHECK(MPI_Waitsome(static_cast<int>(rreqs_.size()), rreqs_.data(), &n, idx.data(),
+                                   MPI_STATUSES_IGNORE));
+        if (n > 0 && n != MPI_UNDEFINED) land(n);
+      }
+    }
+    waitall(sreqs, "mpi-host exchange");
+    GMT_CHECK("event", gmt_rt_event_record(h2d_done_[cur_], s));
+    armed_[cur_] = true;
   }
 
  private:
+  struct Chunk {
+    size_t msg, off, len;
+  };
   MPI_Comm c_;
   std::vector<Msg> recvs_, sends_;
-  std::vector<Buffer<char>> rstage_, sstage_;
-  std::vector<MPI_Request> reqs_;
-  gmt_event_t h2d_done_ = nullptr;
-  bool armed_ = false;
+  std::vector<Buffer<char>> rstage_[2], sstage_;
+  std::vector<Chunk> schunks_, rchunks_;
+  std::vector<gmt_event_t> events_;
+  std::vector<MPI_Request> rreqs_;
+  gmt_event_t h2d_done_[2] = {nullptr, nullptr};
+  bool armed_[2] = {false, false};
+  int cur_ = 1;
 };
 
 class MpiHostTransport : public MpiTransport {

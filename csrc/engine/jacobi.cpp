@@ -282,9 +282,9 @@ void JacobiSolver::step_block() {
 
 // Measured cost of one fused pass of K sweeps (ms; gmt_kernel_bench
 // --only=tb --sustained=1: back-to-back launches with the default launch
-// shape, MI355X, profiles/r02_tb4.md) on two domain sizes.  One-wave strips
-// (K <= 10) run near the HBM floor (~3.8-4.1 ms at 32768^2); two-stage strips
-// (K >= 12) are VALU bound from K ~ 14.  K = 1 is the single-sweep kernel;
+// shape and segment plan, Dirichlet sides, MI355X, profiles/r02_tb5/) on two
+// domain sizes.  One-wave strips (K <= 10) run at ~3.9-4.4 ms at 32768^2;
+// two-stage strips (K >= 12) are VALU bound from K ~ 16.  K = 1 is the single-sweep kernel;
 // 0 = no kernel for that K (odd K > 10).
 namespace {
 struct PassCosts {
@@ -292,12 +292,12 @@ struct PassCosts {
   double ms[GMT_TB_MAX_SWEEPS + 1];
 };
 constexpr PassCosts kCostLarge = {32768.0 * 32768.0,
-                                  {0,    3.05, 3.94, 4.23, 4.03, 4.07, 4.13, 4.40, 3.88, 4.10, 3.81, 0,    3.55,
-                                   0,    3.98, 0,    4.39, 0,    4.93, 0,    5.59, 0,    6.37, 0,    6.97}};
+                                  {0,    3.05, 4.27, 4.12, 4.09, 3.93, 3.97, 4.38, 4.25, 4.33, 3.93, 0,    3.59,
+                                   0,    3.52, 0,    4.31, 0,    4.72, 0,    5.02, 0,    5.43, 0,    5.84}};
 constexpr PassCosts kCostSmall = {8192.0 * 8192.0,
-                                  {0,     0.20,  0.268, 0.283, 0.267, 0.275, 0.275, 0.286, 0.274,
-                                   0.284, 0.279, 0,     0.270, 0,     0.300, 0,     0.368, 0,
-                                   0.408, 0,     0.502, 0,     0.579, 0,     0.644}};
+                                  {0,     0.20,  0.285, 0.293, 0.282, 0.284, 0.289, 0.296, 0.282,
+                                   0.308, 0.291, 0,     0.262, 0,     0.275, 0,     0.318, 0,
+                                   0.364, 0,     0.410, 0,     0.481, 0,     0.525}};
 constexpr double kLaunchMs = 0.015;    // host launch + dispatch per pass
 constexpr double kExchangeMs = 0.035;  // a halo exchange not hidden by the overlap
 }  // namespace

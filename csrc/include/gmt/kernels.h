@@ -112,8 +112,9 @@ typedef struct gmt_tb_opts {
   int sweeps;   /* K, see gmt_jacobi5tb_supported */
   int wg_waves; /* 192-column strips per workgroup, 1..8 (0 = default; at
                    most 4 when K > 10) */
-  int seg_rows; /* output rows per strip (0 = default: 192-384 by K, fewer
-                   for small domains) */
+  int seg_rows; /* output rows per strip segment (0 = default: short edge
+                   segments where a rect touches a Dirichlet row, interior
+                   segments sized to fill the device's resident workgroups) */
   int exact;    /* 1: multiply by 1/4 per level (bitwise for any magnitude);
                    0: power-of-two scaled levels (bitwise unless a value is
                    subnormal or |u| * 4^K overflows) */

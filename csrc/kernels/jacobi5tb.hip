@@ -48,6 +48,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <utility>
 
 #include "common.hpp"
@@ -88,9 +89,11 @@ struct Args {
   int64_t last_row;              // last allocated row (load clamp)
   int n;                         // rects
   int mask;                      // halo sides: bit0..3 = W/E/S/N
+  // segments of rect k: an optional top edge segment of e0[k] rows and a
+  // bottom one of e1[k] rows (short: the only ones whose waves can need the
+  // Dirichlet rule in y), then nmid[k] interior segments of lmid[k] rows
+  int64_t e0[kMaxRect], e1[kMaxRect], nmid[kMaxRect], lmid[kMaxRect];
   int nw;                        // strips per workgroup
-  int seg;                       // output rows per segment
-  int nsteps;                    // steps per segment, padded to the unroll
   double quarter;                // 0.25 (EXACT): an SGPR operand
 };
 
@@ -146,7 +149,7 @@ __device__ __forceinline__ d3 lds_row(const char* slot, int lane) {
 template <int K, int PB, int PE, bool EXACT, bool EDGE, bool RULE, bool SYNC>
 __device__ __forceinline__ void run_stage(const Args& a, const double* __restrict__ u, double* __restrict__ un,
                                           char* ring, char* hand, int lane, int64_t xs, int64_t xe, int64_t ys,
-                                          int64_t ye) {
+                                          int64_t ye, int nsteps) {
   constexpr bool kIn = PB == 1;
   constexpr bool kOut = PE == K;
   constexpr int SPS = kOut ? (EDGE ? 3 : 2) : 0;  // global stores per step
@@ -314,7 +317,7 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   // One loop for the whole segment: splitting off the pipeline's warm-up
   // and drain steps (to skip the levels nobody reads there) made the
   // register allocator spill (three loops carrying W).
-  for (int s0 = 0; s0 < a.nsteps; s0 += kU) static_for<0, kU>([&](auto J) { step(J, s0 + decltype(J)::value); });
+  for (int s0 = 0; s0 < nsteps; s0 += kU) static_for<0, kU>([&](auto J) { step(J, s0 + decltype(J)::value); });
   // no LDS-DMA may land after the workgroup's LDS is released
   wait_vmcnt<0>();
 }
@@ -335,27 +338,54 @@ void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__
   while (k + 1 < a.n && t >= a.tstart[k + 1]) ++k;
   const int64_t lt = t - a.tstart[k];
   const int64_t ngroups = (a.nstrip[k] + a.nw - 1) / a.nw;
-  const int64_t nseg = (a.r[k][3] + a.seg - 1) / a.seg;
-  // dispatch order of the segment rows: the first and the last (the only
-  // ones that can hold Dirichlet-rule waves at the top / bottom) go first,
-  // so the launch's tail is made of fast waves
-  const int64_t lseg = lt / ngroups;
-  const int64_t seg = nseg < 2 || lseg == 0 ? lseg : (lseg == 1 ? nseg - 1 : lseg - 1);
-  const int64_t strip = (lt % ngroups) * a.nw + sl;
+  // Dispatch order: every workgroup that can hold Dirichlet-rule waves
+  // (~1.5x the VALU per step) goes first, so the launch's tail is made of
+  // fast ones: (A) the edge segments, all strip groups; (B) the interior
+  // segments' first and last strip groups; (C) the rest.
+  const int64_t ry0 = a.r[k][2], ry1 = a.r[k][2] + a.r[k][3];
+  const int64_t e0 = a.e0[k], e1 = a.e1[k];
+  const int64_t nedge = (e0 > 0) + (e1 > 0), nbnd = ngroups < 2 ? ngroups : 2;
+  int64_t j, gi;
+  if (lt < nedge * ngroups) {
+    j = lt / ngroups;
+    gi = lt % ngroups;
+  } else if (lt < nedge * ngroups + a.nmid[k] * nbnd) {
+    const int64_t l2 = lt - nedge * ngroups;
+    j = nedge + l2 / nbnd;
+    gi = l2 % nbnd == 0 ? 0 : ngroups - 1;
+  } else {
+    const int64_t l3 = lt - nedge * ngroups - a.nmid[k] * nbnd;
+    j = nedge + l3 / (ngroups - 2);
+    gi = 1 + l3 % (ngroups - 2);
+  }
+  int64_t ys, ye;
+  if (e0 > 0 && j == 0) {
+    ys = ry0;
+    ye = ry0 + e0;
+  } else {
+    if (e0 > 0) --j;
+    if (e1 > 0 && j == 0) {
+      ys = ry1 - e1;
+      ye = ry1;
+    } else {
+      if (e1 > 0) --j;
+      ys = ry0 + e0 + j * a.lmid[k];
+      ye = ys + a.lmid[k] < ry1 - e1 ? ys + a.lmid[k] : ry1 - e1;
+    }
+  }
+  const int nsteps = static_cast<int>((ye - ys + 3 * K + kU - 1) / kU * kU);
+  const int64_t strip = gi * a.nw + sl;
   if (strip >= a.nstrip[k]) {  // no strip for this wave
     if constexpr (G > 1) {
-      for (int s = 0; s < a.nsteps; ++s) step_barrier();  // the workgroup's per-step barriers
+      for (int s = 0; s < nsteps; ++s) step_barrier();  // the workgroup's per-step barriers
     }
     return;
   }
   constexpr int64_t wout = strip_out(K);
   const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
-  const int64_t ry1 = a.r[k][2] + a.r[k][3];
   int64_t xs = rx0 + strip * wout;
   if (xs + wout > rx1) xs = rx1 - wout > rx0 ? rx1 - wout : rx0;  // last strip: shifted left to end at rx1
   const int64_t xe = xs + wout < rx1 ? xs + wout : rx1;
-  const int64_t ys = a.r[k][2] + seg * a.seg;
-  const int64_t ye = ys + a.seg < ry1 ? ys + a.seg : ry1;
   // the rule path only where a computed cell can be a fixed ring cell
   const int64_t cx0 = xs - ring_left(K), cx1 = cx0 + kCols;
   const bool rule = (cx0 < a.dom[0] && !(a.mask & 1)) || (cx1 > a.dom[0] + a.dom[1] && !(a.mask & 2)) ||
@@ -364,21 +394,21 @@ void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__
   char* hand = ring + kRS * kSlotBytes;
   if constexpr (G == 1) {
     if (rule)
-      run_stage<K, 1, K, EXACT, EDGE, true, false>(a, u, un, ring, hand, lane, xs, xe, ys, ye);
+      run_stage<K, 1, K, EXACT, EDGE, true, false>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
     else
-      run_stage<K, 1, K, EXACT, EDGE, false, false>(a, u, un, ring, hand, lane, xs, xe, ys, ye);
+      run_stage<K, 1, K, EXACT, EDGE, false, false>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
   } else {
     constexpr int KA = stage0_levels(K);
     if (stage == 0) {
       if (rule)
-        run_stage<K, 1, KA, EXACT, EDGE, true, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye);
+        run_stage<K, 1, KA, EXACT, EDGE, true, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
       else
-        run_stage<K, 1, KA, EXACT, EDGE, false, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye);
+        run_stage<K, 1, KA, EXACT, EDGE, false, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
     } else {
       if (rule)
-        run_stage<K, KA + 1, K, EXACT, EDGE, true, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye);
+        run_stage<K, KA + 1, K, EXACT, EDGE, true, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
       else
-        run_stage<K, KA + 1, K, EXACT, EDGE, false, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye);
+        run_stage<K, KA + 1, K, EXACT, EDGE, false, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
     }
   }
 }
@@ -391,14 +421,60 @@ namespace {
 using namespace gmt;
 using namespace gmt::tb;
 
-// Output rows per strip.  Short segments measured fastest on 32768^2 even
-// though every segment pays the 3K-step pipeline warm-up (profiles/r02_tb.md);
-// small domains get shorter segments so the launch still has ~4 waves per
-// resident slot.
-int64_t default_seg_rows(int K, int64_t rows_x_strips) {
-  const int64_t pref = K <= 10 ? 192 : (K <= 14 ? 256 : 384);
-  constexpr int64_t kTargetWaves = 4 * 2048;  // 4 x (2 waves/SIMD x 1024 SIMDs)
-  return std::max<int64_t>(64, std::min(pref, rows_x_strips * n_stages(K) / kTargetWaves));
+// Segment plan (rows per strip).  Every segment pays a 3K-step pipeline
+// warm-up, so interior segments should be long; but a wave whose segment
+// touches a Dirichlet row runs the rule path (~1.5x the VALU per step) for
+// the whole segment, and the launch ends with its slowest round.  Measured
+// (profiles/r02_tb4.md, K = 20, 32768^2): all-halo sides 4.41M MLUPS at 384
+// rows and 4.61M at 1024-2048; with Dirichlet sides 3.78M at 384, falling
+// to 2.38M at 4096.  So: short edge segments (max(64, K) rows) where the
+// rect touches a Dirichlet row, and interior segments whose length L
+// minimises rounds(L) x (L + 3K), rounds = ceil(workgroups / resident
+// workgroups), over L in [128, 2048].
+struct SegPlan {
+  int64_t e0[kMaxRect], e1[kMaxRect], nmid[kMaxRect], lmid[kMaxRect];
+};
+
+template <int K>
+SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t resident_wgs) {
+  SegPlan p{};
+  const int64_t edge = std::max<int64_t>(64, K);
+  auto fill = [&](int64_t L, int64_t* wgs) {
+    int64_t w = 0;
+    for (int k = 0; k < a.n; ++k) {
+      const int64_t ny = a.r[k][3], ry0 = a.r[k][2], ry1 = ry0 + ny;
+      const bool top = seg_rows == 0 && ry0 - K < a.dom[2] && !(a.mask & 4);
+      const bool bot = seg_rows == 0 && ry1 + K > a.dom[2] + a.dom[3] && !(a.mask & 8);
+      p.e0[k] = p.e1[k] = 0;
+      if (ny > 2 * edge + 64) {  // room for edges and an interior
+        p.e0[k] = top ? edge : 0;
+        p.e1[k] = bot ? edge : 0;
+      }
+      const int64_t mid = ny - p.e0[k] - p.e1[k];
+      p.nmid[k] = (mid + L - 1) / L;
+      p.lmid[k] = (mid + p.nmid[k] - 1) / p.nmid[k];  // balanced lengths
+      w += ((a.nstrip[k] + a.nw - 1) / a.nw) * (p.nmid[k] + (p.e0[k] > 0) + (p.e1[k] > 0));
+    }
+    *wgs = w;
+  };
+  int64_t wgs = 0;
+  if (seg_rows > 0) {
+    fill(std::min<int64_t>(seg_rows, lmax), &wgs);
+    return p;
+  }
+  int64_t best_l = 128;
+  double best = 1e300;
+  for (int64_t L = 128; L <= std::min<int64_t>(2048, lmax); L += 32) {
+    fill(L, &wgs);
+    const double rounds = static_cast<double>((wgs + resident_wgs - 1) / resident_wgs);
+    const double cost = rounds * static_cast<double>(L + 3 * K);
+    if (cost < best) {
+      best = cost;
+      best_l = L;
+    }
+  }
+  fill(std::min<int64_t>(best_l, lmax), &wgs);
+  return p;
 }
 
 template <int K, bool EXACT, bool EDGE>
@@ -432,25 +508,39 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   // (L + 3K + unroll + prefetch) rows of ld doubles must stay below 2^31
   const int64_t lmax = std::min<int64_t>(1 << 20, (int64_t(1) << 31) / (ld * 8) - 3 * K - 2 * kU - kP);
   if (lmax < 1) return static_cast<int>(hipErrorInvalidValue);
-  int64_t rows_x_strips = 0;
-  for (int k = 0; k < a.n; ++k) rows_x_strips += a.r[k][3] * a.nstrip[k];
-  const int64_t L =
-      std::min(std::min<int64_t>(o.seg_rows > 0 ? o.seg_rows : default_seg_rows(K, rows_x_strips), maxh), lmax);
-  a.seg = static_cast<int>(L);
-  a.nsteps = static_cast<int>((L + 3 * K + kU - 1) / kU * kU);
-  a.tstart[0] = 0;
-  for (int k = 0; k < a.n; ++k) {
-    const int64_t groups = (a.nstrip[k] + a.nw - 1) / a.nw;
-    a.tstart[k + 1] = a.tstart[k] + groups * ((a.r[k][3] + L - 1) / L);
-  }
-  for (int k = a.n + 1; k <= kMaxRect; ++k) a.tstart[k] = a.tstart[a.n];
-  const int64_t nb = a.tstart[a.n];
+  (void)maxh;
   const size_t smem = static_cast<size_t>(a.nw * strip_lds(G));
   if (smem > 65536) {  // above the default dynamic-LDS limit (gfx950 has 160 KB per CU)
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem));
     if (e != hipSuccess) return static_cast<int>(e);
   }
+  // resident workgroups on the device for this shape (registers, LDS);
+  // queried once per kernel and strips-per-workgroup (an idempotent cache)
+  static std::atomic<int> resident[kMaxThreads / kWave + 1] = {};
+  int per_cu = resident[a.nw].load(std::memory_order_relaxed);
+  if (per_cu <= 0) {
+    int occ = 0, dev = 0, cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE>),
+                                                     a.nw * G * kWave, smem) != hipSuccess || occ < 1)
+      occ = 1;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    per_cu = occ * cus;
+    resident[a.nw].store(per_cu, std::memory_order_relaxed);
+  }
+  const SegPlan sp = plan_segments<K>(a, o.seg_rows, lmax, per_cu);
+  a.tstart[0] = 0;
+  for (int k = 0; k < a.n; ++k) {
+    a.e0[k] = sp.e0[k];
+    a.e1[k] = sp.e1[k];
+    a.nmid[k] = sp.nmid[k];
+    a.lmid[k] = sp.lmid[k];
+    const int64_t groups = (a.nstrip[k] + a.nw - 1) / a.nw;
+    a.tstart[k + 1] = a.tstart[k] + groups * (sp.nmid[k] + (sp.e0[k] > 0) + (sp.e1[k] > 0));
+  }
+  for (int k = a.n + 1; k <= kMaxRect; ++k) a.tstart[k] = a.tstart[a.n];
+  const int64_t nb = a.tstart[a.n];
   jacobi5tb_kernel<K, EXACT, EDGE><<<grid_1d(nb), a.nw * G * kWave, smem, s>>>(a, u, un, nb);
   return static_cast<int>(hipGetLastError());
 }
