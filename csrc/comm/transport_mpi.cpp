@@ -109,10 +109,16 @@ class MpiTransport : public Transport {
 // receives never wait for this one's H2D copies to drain.
 class MpiHostExchange : public Exchange {
  public:
-  static constexpr size_t kChunk = size_t(1) << 20;
+  // pipeline chunk: 1 MiB (GMT_HOST_CHUNK_KB overrides, for measurement)
+  static size_t chunk_bytes() {
+    const char* e = std::getenv("GMT_HOST_CHUNK_KB");
+    const long kb = e ? std::atol(e) : 0;
+    return kb > 0 ? static_cast<size_t>(kb) << 10 : size_t(1) << 20;
+  }
 
   MpiHostExchange(MPI_Comm c, std::vector<Msg> r, std::vector<Msg> s)
       : c_(c), recvs_(std::move(r)), sends_(std::move(s)) {
+    const size_t kChunk = chunk_bytes();
     for (int set = 0; set < 2; ++set)
       for (auto& m : recvs_) rstage_[set].emplace_back(m.bytes, GMT_SPACE_PINNED);
     for (auto& m : sends_) sstage_.emplace_back(m.bytes, GMT_SPACE_PINNED);
@@ -306,7 +312,9 @@ class MpiDirectTransport : public MpiTransport {
 };
 
 // ----------------------------------------------------------------------- ipc
-constexpr int kHandleTag = 30000, kReadyTag = 10000, kDoneTag = 20000;
+// handle-exchange tags: one offset per wire kind, so a pair of ranks that
+// exchange messages with the same tag in both directions cannot mismatch them
+constexpr int kStageTag = 10000, kFlagTag = 20000, kReadyTag = 30000;
 
 struct IpcWire {
   gmt_ipc_handle h;
@@ -345,135 +353,155 @@ class IpcCache {
   std::map<std::string, E> map_;
 };
 
+// Stream-ordered exchange over IPC-mapped memory (csrc/kernels/ipc.hip has
+// the protocol).  Every send message gets two staging slots in the sender's
+// memory; the receiver pulls the current slot once the sender's "ready" flag
+// (in the receiver's flag memory) reaches the exchange's epoch, then marks the
+// slot consumed (in the sender's flag memory).  start() and wait() are one
+// kernel launch each on the caller's stream: no host synchronisation, no MPI
+// traffic after construction, so the exchange can be captured into a graph.
+// Several ranks may share a GPU (the IPC mappings are then same-device).
 class IpcExchange : public Exchange {
  public:
-  IpcExchange(MPI_Comm c, int rank, IpcCache* cache, gmt_stream_t copy_stream, std::vector<Msg> r,
-              std::vector<Msg> s)
-      : c_(c), rank_(rank), cache_(cache), cs_(copy_stream), recvs_(std::move(r)),
-        sends_(std::move(s)) {
-    // export every receive buffer to the rank that will write it
-    std::vector<IpcWire> out(recvs_.size()), in(sends_.size());
+  IpcExchange(MPI_Comm c, int rank, IpcCache* cache, std::vector<Msg> r, std::vector<Msg> s)
+      : c_(c), rank_(rank), cache_(cache), recvs_(std::move(r)), sends_(std::move(s)) {
+    const size_t nr = recvs_.size(), ns = sends_.size();
+    // flags: ready[j] per receive (written by its sender), consumed[i] per send
+    // (written by its receiver); control: epoch, 2 launch counters, error word
+    flags_ = Buffer<uint64_t>(nr + ns + 1, GMT_SPACE_FLAGS);
+    ctl_ = Buffer<uint64_t>(4, GMT_SPACE_DEVICE);  // epoch | 3 x u32 counters + u32 error
+    GMT_CHECK("ipc ctl", gmt_rt_memset_async(ctl_.data(), 0, ctl_.bytes(), nullptr));
+    GMT_CHECK("ipc ctl", gmt_rt_stream_synchronize(nullptr));
+    for (auto& m : sends_) stage_.emplace_back(2 * (m.bytes ? m.bytes : 1), GMT_SPACE_DEVICE);
+
+    // wiring: the receiver of send i learns {its staging, its consumed flag};
+    // the sender of receive j learns {its ready flag}
+    auto wire = [](void* p) {
+      IpcWire w;
+      size_t off = 0;
+      GMT_CHECK("ipc get handle", gmt_rt_ipc_get_handle(&w.h, &off, p));
+      w.offset = off;
+      return w;
+    };
+    std::vector<IpcWire> out_stage(ns), out_cflag(ns), out_rflag(nr), in_stage(nr), in_cflag(nr), in_rflag(ns);
     std::vector<MPI_Request> reqs;
-    for (size_t i = 0; i < sends_.size(); ++i) {
+    for (size_t j = 0; j < nr; ++j) {
+      if (recvs_[j].peer == rank_) continue;
+      reqs.emplace_back();
+      GMT_MPI_CHECK(MPI_Irecv(&in_stage[j], sizeof(IpcWire), MPI_BYTE, recvs_[j].peer, recvs_[j].tag + kStageTag,
+                              c_, &reqs.back()));
+      reqs.emplace_back();
+      GMT_MPI_CHECK(MPI_Irecv(&in_cflag[j], sizeof(IpcWire), MPI_BYTE, recvs_[j].peer, recvs_[j].tag + kFlagTag,
+                              c_, &reqs.back()));
+      out_rflag[j] = wire(flags_.data() + j);
+      reqs.emplace_back();
+      GMT_MPI_CHECK(MPI_Isend(&out_rflag[j], sizeof(IpcWire), MPI_BYTE, recvs_[j].peer, recvs_[j].tag + kReadyTag,
+                              c_, &reqs.back()));
+    }
+    for (size_t i = 0; i < ns; ++i) {
       if (sends_[i].peer == rank_) continue;
       reqs.emplace_back();
-      GMT_MPI_CHECK(MPI_Irecv(&in[i], sizeof(IpcWire), MPI_BYTE, sends_[i].peer,
-                              sends_[i].tag + kHandleTag, c_, &reqs.back()));
-    }
-    for (size_t i = 0; i < recvs_.size(); ++i) {
-      if (recvs_[i].peer == rank_) continue;
-      size_t off = 0;
-      GMT_CHECK("ipc get handle", gmt_rt_ipc_get_handle(&out[i].h, &off, recvs_[i].buf));
-      out[i].offset = off;
+      GMT_MPI_CHECK(MPI_Irecv(&in_rflag[i], sizeof(IpcWire), MPI_BYTE, sends_[i].peer, sends_[i].tag + kReadyTag,
+                              c_, &reqs.back()));
+      out_stage[i] = wire(stage_[i].data());
+      out_cflag[i] = wire(flags_.data() + nr + i);
       reqs.emplace_back();
-      GMT_MPI_CHECK(MPI_Isend(&out[i], sizeof(IpcWire), MPI_BYTE, recvs_[i].peer,
-                              recvs_[i].tag + kHandleTag, c_, &reqs.back()));
+      GMT_MPI_CHECK(MPI_Isend(&out_stage[i], sizeof(IpcWire), MPI_BYTE, sends_[i].peer, sends_[i].tag + kStageTag,
+                              c_, &reqs.back()));
+      reqs.emplace_back();
+      GMT_MPI_CHECK(MPI_Isend(&out_cflag[i], sizeof(IpcWire), MPI_BYTE, sends_[i].peer, sends_[i].tag + kFlagTag,
+                              c_, &reqs.back()));
     }
     waitall(reqs, "ipc handle exchange");
-    remote_.resize(sends_.size(), nullptr);
-    for (size_t i = 0; i < sends_.size(); ++i) {
-      if (sends_[i].peer == rank_) {
-        // a message to ourselves (periodic single rank): local copy
-        for (auto& m : recvs_)
-          if (m.peer == rank_ && m.tag == sends_[i].tag) remote_[i] = m.buf;
-        if (!remote_[i]) {
-          std::printf("ipc: no self-receive for tag %d\n", sends_[i].tag);
-          abort_job(2);
-        }
-        continue;
-      }
-      void* base = cache_->open(in[i].h);
+    auto open = [&](const IpcWire& w) {
+      void* base = cache_->open(w.h);
       opened_.push_back(base);
-      remote_[i] = static_cast<char*>(base) + in[i].offset;
+      return static_cast<char*>(base) + w.offset;
+    };
+    // self messages (periodic single rank): the matching local buffers
+    auto self_send = [&](int tag) -> int {
+      for (size_t i = 0; i < ns; ++i)
+        if (sends_[i].peer == rank_ && sends_[i].tag == tag) return static_cast<int>(i);
+      std::printf("ipc: no self-send for tag %d\n", tag);
+      abort_job(2);
+    };
+    auto self_recv = [&](int tag) -> int {
+      for (size_t j = 0; j < nr; ++j)
+        if (recvs_[j].peer == rank_ && recvs_[j].tag == tag) return static_cast<int>(j);
+      std::printf("ipc: no self-receive for tag %d\n", tag);
+      abort_job(2);
+    };
+    for (size_t i = 0; i < ns; ++i) {
+      const Msg& m = sends_[i];
+      gmt_ipc_chan ch{};
+      ch.src = m.buf;
+      ch.dst = stage_[i].data();
+      ch.bytes = static_cast<int64_t>(m.bytes);
+      ch.dst_stride = static_cast<int64_t>(m.bytes ? m.bytes : 1);
+      ch.wait = flags_.data() + nr + i;  // the receiver has consumed slot e & 1 (exchange e - 2)
+      ch.signal = m.peer == rank_ ? flags_.data() + self_recv(m.tag)
+                                  : reinterpret_cast<uint64_t*>(open(in_rflag[i]));
+      send_.push_back(ch);
+    }
+    for (size_t j = 0; j < nr; ++j) {
+      const Msg& m = recvs_[j];
+      gmt_ipc_chan ch{};
+      if (m.peer == rank_) {
+        const int i = self_send(m.tag);
+        ch.src = stage_[i].data();
+        ch.signal = flags_.data() + nr + i;
+      } else {
+        ch.src = open(in_stage[j]);
+        ch.signal = reinterpret_cast<uint64_t*>(open(in_cflag[j]));
+      }
+      ch.src_stride = static_cast<int64_t>(m.bytes ? m.bytes : 1);
+      ch.dst = m.buf;
+      ch.bytes = static_cast<int64_t>(m.bytes);
+      ch.wait = flags_.data() + j;  // the sender's slot for this exchange is ready
+      recv_.push_back(ch);
+    }
+    if (send_.size() > GMT_IPC_MAX_CHAN || recv_.size() > GMT_IPC_MAX_CHAN) {
+      std::printf("ipc: %zu sends / %zu receives exceed %d channels per launch\n", send_.size(), recv_.size(),
+                  GMT_IPC_MAX_CHAN);
+      abort_job(2);
     }
   }
   ~IpcExchange() override {
     for (void* b : opened_) cache_->close(b);
   }
+  // one launch per exchange (send and receive channels in the same grid)
   void start(gmt_stream_t s) override {
-    // (1) our send data is produced and every earlier reader of our ghost
-    //     cells has finished, so (2) we may grant our writers access
-    GMT_CHECK("ipc sync", gmt_rt_stream_synchronize(s));
-    std::vector<MPI_Request> ready;
-    for (auto& m : recvs_)
-      if (m.peer != rank_) {
-        ready.emplace_back();
-        GMT_MPI_CHECK(MPI_Isend(&token_, 0, MPI_BYTE, m.peer, m.tag + kReadyTag, c_, &ready.back()));
-      }
-    for (auto& m : sends_)
-      if (m.peer != rank_) {
-        ready.emplace_back();
-        GMT_MPI_CHECK(MPI_Irecv(&token_, 0, MPI_BYTE, m.peer, m.tag + kReadyTag, c_, &ready.back()));
-      }
-    waitall(ready, "ipc ready");
-    // (3) write straight into the neighbours' receive buffers (xGMI / same GPU)
-    copy_out();
-    GMT_CHECK("ipc copy sync", gmt_rt_stream_synchronize(cs_));
-    // (4) tell the receivers their data has landed
-    for (auto& m : sends_)
-      if (m.peer != rank_) {
-        done_.emplace_back();
-        GMT_MPI_CHECK(MPI_Isend(&token_, 0, MPI_BYTE, m.peer, m.tag + kDoneTag, c_, &done_.back()));
-      }
-    for (auto& m : recvs_)
-      if (m.peer != rank_) {
-        done_.emplace_back();
-        GMT_MPI_CHECK(MPI_Irecv(&token_, 0, MPI_BYTE, m.peer, m.tag + kDoneTag, c_, &done_.back()));
-      }
+    if (send_.empty() && recv_.empty()) return;
+    GMT_CHECK("ipc exchange", gmt_ipc_exchange(static_cast<int>(send_.size()), send_.data(),
+                                               static_cast<int>(recv_.size()), recv_.data(), epoch(), counters(),
+                                               err(), s));
   }
-  void wait(gmt_stream_t) override { waitall(done_, "ipc done"); }
+  void wait(gmt_stream_t) override {}  // stream order: the launch in start() completes first
+  bool graph_capturable() const override { return true; }
 
  private:
-  // All sends in one launch of the fused copy kernel (remote stores over
-  // xGMI, or same-device stores): no SDMA-engine setup latency, which on
-  // MI355X dominates for halo-sized messages.  GMT_IPC_COPY=sdma restores
-  // hipMemcpyAsync.
-  void copy_out() {
-    static const bool sdma = [] {
-      const char* e = std::getenv("GMT_IPC_COPY");
-      return e && std::string(e) == "sdma";
-    }();
-    gmt_copy2d_desc d[GMT_MAX_COPY2D];
-    int n = 0;
-    for (size_t i = 0; i < sends_.size(); ++i) {
-      const size_t b = sends_[i].bytes;
-      if (sdma || b % 8 != 0) {
-        GMT_CHECK("ipc copy", gmt_rt_memcpy_async(remote_[i], sends_[i].buf, b, cs_));
-        continue;
-      }
-      const int64_t w = static_cast<int64_t>(b / 8);
-      d[n++] = {sends_[i].buf, remote_[i], w, w, w, 1};
-      if (n == GMT_MAX_COPY2D) {
-        GMT_CHECK("ipc copy kernel", gmt_copy2d_batched(n, d, 8, cs_));
-        n = 0;
-      }
-    }
-    if (n) GMT_CHECK("ipc copy kernel", gmt_copy2d_batched(n, d, 8, cs_));
-  }
+  uint64_t* epoch() { return ctl_.data(); }
+  unsigned* counters() { return reinterpret_cast<unsigned*>(ctl_.data() + 1); }  // 3 words
+  unsigned* err() { return reinterpret_cast<unsigned*>(ctl_.data() + 3); }
 
   MPI_Comm c_;
   int rank_;
   IpcCache* cache_;
-  gmt_stream_t cs_;
   std::vector<Msg> recvs_, sends_;
-  std::vector<void*> remote_, opened_;
-  std::vector<MPI_Request> done_;
-  char token_ = 0;
+  Buffer<uint64_t> flags_, ctl_;
+  std::vector<Buffer<char>> stage_;
+  std::vector<gmt_ipc_chan> send_, recv_;
+  std::vector<void*> opened_;
 };
 
 class IpcTransport : public MpiTransport {
  public:
-  explicit IpcTransport(MPI_Comm c) : MpiTransport(c) {
-    GMT_CHECK("ipc copy stream", gmt_rt_stream_create(&cs_, 1));
-  }
-  ~IpcTransport() override {
-    gathers_.clear();
-    gmt_rt_stream_destroy(cs_);
-  }
+  explicit IpcTransport(MPI_Comm c) : MpiTransport(c) {}
+  ~IpcTransport() override { gathers_.clear(); }
   Kind kind() const override { return Kind::Ipc; }
   const char* name() const override { return "ipc"; }
   std::unique_ptr<Exchange> plan(const std::vector<Msg>& r, const std::vector<Msg>& s) override {
-    return std::make_unique<IpcExchange>(comm_, rank_, &cache_, cs_, r, s);
+    return std::make_unique<IpcExchange>(comm_, rank_, &cache_, r, s);
   }
   void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override {
     staged_allreduce(comm_, buf, n, s);
@@ -502,7 +530,6 @@ class IpcTransport : public MpiTransport {
 
  private:
   static constexpr int kGatherTag = 777;
-  gmt_stream_t cs_ = nullptr;
   IpcCache cache_;
   std::map<std::tuple<const void*, void*, size_t>, std::unique_ptr<Exchange>> gathers_;
 };

@@ -9,6 +9,8 @@
 // purpose: several MPI ranks share the CPU in the tests, and a rank-local
 // thread pool would only oversubscribe it.
 #include <cmath>
+#include <sched.h>
+
 #include <cstring>
 #include <vector>
 
@@ -197,6 +199,39 @@ int gmt_jacobi5tb(const gmt_tb_opts* o, int n_rect, const int64_t* rects, const 
   return host_xk(K, n_rect, rects, dom, mask, u, un, ld);
 }
 
+
+// CPU backend of csrc/kernels/ipc.hip: the same protocol on memfd-shared
+// memory between processes (flags through __atomic builtins): sends first,
+// their "ready" signals, then the receives.
+int gmt_ipc_exchange(int n_send, const gmt_ipc_chan* sends, int n_recv, const gmt_ipc_chan* recvs, uint64_t* epoch,
+                     unsigned* counters, unsigned* err, void*) {
+  if (n_send < 0 || n_recv < 0 || n_send > GMT_IPC_MAX_CHAN || n_recv > GMT_IPC_MAX_CHAN || n_send + n_recv < 1 ||
+      !epoch || !counters || !err)
+    return 1;
+  const uint64_t e = __atomic_load_n(epoch, __ATOMIC_ACQUIRE) + 1;
+  auto run = [&](int n, const gmt_ipc_chan* cs, uint64_t lag) {
+    for (int k = 0; k < n; ++k) {
+      const gmt_ipc_chan& c = cs[k];
+      if (c.wait && e > lag) {
+        for (long it = 0; __atomic_load_n(c.wait, __ATOMIC_ACQUIRE) < e - lag; ++it) {
+          if (it > 20000000) {  // tens of seconds of polling: give up like the GPU kernel
+            __atomic_fetch_or(err, 1u, __ATOMIC_RELAXED);
+            break;
+          }
+          if (it > 1000) sched_yield();
+        }
+      }
+      std::memcpy(static_cast<char*>(c.dst) + (e & 1) * c.dst_stride,
+                  static_cast<const char*>(c.src) + (e & 1) * c.src_stride, static_cast<size_t>(c.bytes));
+    }
+    for (int k = 0; k < n; ++k)
+      if (cs[k].signal) __atomic_store_n(cs[k].signal, e, __ATOMIC_RELEASE);
+  };
+  run(n_send, sends, 2);
+  run(n_recv, recvs, 0);
+  __atomic_store_n(epoch, e, __ATOMIC_RELEASE);
+  return 0;
+}
 
 const char* gmt_error_string(int err) {
   switch (err) {

@@ -124,7 +124,8 @@ int gmt_rt_device_reset(void) { return kOk; }
 int gmt_rt_malloc(void** p, size_t bytes, int space) {
   *p = nullptr;
   if (bytes == 0) bytes = 1;
-  if (space == GMT_SPACE_DEVICE || space == GMT_SPACE_MANAGED) {
+  if (space == GMT_SPACE_DEVICE || space == GMT_SPACE_MANAGED || space == GMT_SPACE_FLAGS) {
+    // memfd pages start zeroed (GMT_SPACE_FLAGS relies on it)
     const int fd = memfd_create("gmt_dev", MFD_CLOEXEC);
     if (fd < 0) return kNoMem;
     if (ftruncate(fd, static_cast<off_t>(bytes)) != 0) {

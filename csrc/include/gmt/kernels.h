@@ -123,6 +123,30 @@ int gmt_jacobi5tb_supported(int sweeps);
 int gmt_jacobi5tb(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, const int64_t* dom,
                   int halo_mask, const double* u, double* un, int64_t ld, int64_t nrows, void* stream);
 
+/* ---- Stream-ordered IPC exchange (csrc/kernels/ipc.hip), one launch:
+ *      e = *epoch + 1.  Send channel: wait until *wait >= e - 2 (receiver done
+ *      with the slot), copy src -> dst + (e & 1) * dst_stride.  Receive
+ *      channel: wait until *wait >= e (sender's slot ready), copy
+ *      src + (e & 1) * src_stride -> dst.  When all send (receive) channels
+ *      are copied, e is stored into each of their non-NULL *signal flags
+ *      (system-scope release); when everything is done, *epoch = e.
+ *      counters: 3 device words, zero between launches; a wait that times
+ *      out (~0.5 s) sets *err and gives up.  Flags: GMT_SPACE_FLAGS memory;
+ *      wait flags local, signal flags may be IPC-mapped memory of another
+ *      process or device. */
+#define GMT_IPC_MAX_CHAN 16
+typedef struct gmt_ipc_chan {
+  const void* src;
+  void* dst;
+  int64_t bytes;
+  int64_t src_stride; /* parity offsets (bytes): slot e & 1 */
+  int64_t dst_stride;
+  const uint64_t* wait;
+  uint64_t* signal;
+} gmt_ipc_chan;
+int gmt_ipc_exchange(int n_send, const gmt_ipc_chan* sends, int n_recv, const gmt_ipc_chan* recvs,
+                     uint64_t* epoch, unsigned* counters, unsigned* err, void* stream);
+
 /* One kernel per entry point: the variants the defaults were chosen against
  * are measured by csrc/bench/variant_bench.hip, not shipped in this ABI. */
 

@@ -38,6 +38,9 @@ enum gmt_space {
   GMT_SPACE_DEVICE = 1,  /* device HBM (hipMalloc)                          */
   GMT_SPACE_PINNED = 2,  /* page-locked host memory (hipHostMalloc)         */
   GMT_SPACE_MANAGED = 3, /* unified/managed memory (hipMallocManaged)       */
+  GMT_SPACE_FLAGS = 4,   /* device memory for cross-process flags: uncached
+                            (every access reaches memory), zeroed, exportable
+                            by IPC (hipExtMallocWithFlags Uncached)       */
   GMT_SPACE_UNREGISTERED = -1
 };
 

@@ -83,6 +83,11 @@ int gmt_rt_malloc(void** p, size_t bytes, int space) {
     case GMT_SPACE_DEVICE: RT_RET(hipMalloc(p, bytes));
     case GMT_SPACE_PINNED: RT_RET(hipHostMalloc(p, bytes, hipHostMallocDefault));
     case GMT_SPACE_MANAGED: RT_RET(hipMallocManaged(p, bytes, hipMemAttachGlobal));
+    case GMT_SPACE_FLAGS: {
+      hipError_t e = hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+      if (e == hipSuccess) e = hipMemset(*p, 0, bytes);
+      RT_RET(e);
+    }
     case GMT_SPACE_HOST: {
       // 64-B aligned so host staging buffers keep 16-B vector alignment
       if (posix_memalign(p, 64, bytes) != 0) return static_cast<int>(hipErrorOutOfMemory);
@@ -96,6 +101,7 @@ int gmt_rt_free(void* p, int space) {
   if (!p) return 0;
   switch (space) {
     case GMT_SPACE_DEVICE:
+    case GMT_SPACE_FLAGS:
     case GMT_SPACE_MANAGED: RT_RET(hipFree(p));
     case GMT_SPACE_PINNED: RT_RET(hipHostFree(p));
     case GMT_SPACE_HOST: free(p); return 0;

@@ -98,6 +98,25 @@ def test_app_jacobi_check(np_, transport):
     assert float(m.group(1)) < 1e-12, out
 
 
+@pytest.mark.parametrize("np_", [2, 3])
+def test_app_jacobi_ipc_graph_matches_serial(np_):
+    """Stream-ordered IPC (csrc/kernels/ipc.hip): the exchange is two kernel
+    launches on the compute stream, so the engine captures whole passes into
+    hipGraphs with several ranks sharing the GPU; bitwise vs the serial run."""
+    out = _app(["mpi_jacobi2d", "301", "23", "--check", "--tblock", "--tsteps=4", "--warmup=3", "--graph",
+                "--transport=ipc"], np_=np_)
+    assert re.search(r"transport = ipc overlap=\d graph=1", out), out
+    m = re.search(r"check\s*: max\|diff\| vs serial = ([0-9.eE+-]+) OK", out)
+    assert m and float(m.group(1)) == 0.0, out
+
+
+def test_app_ipc_halo_latency():
+    """16-B IPC exchange between two ranks on one GPU, stream-ordered."""
+    out = _app(["mpi_halo_bench", "16", "4096", "50", "--transport=ipc"], np_=2)
+    rows = re.findall(r"^\s+(\d+)\s+2\s+([\d.]+)\s+([\d.]+)\s+[\d.]+$", out, re.M)
+    assert [int(r[0]) for r in rows] == [16 << k for k in range(9)], out
+
+
 @pytest.mark.parametrize("transport", ["ipc", "mpi-host"])
 def test_app_stencil2d_gt_err_norm(transport):
     # both dims share the reference's spacing 8/n_global_deriv, so the
