@@ -6,7 +6,12 @@
 // transport on a 1-D ring (each rank exchanges with rank-1 and rank+1, both
 // directions at once; a single rank exchanges with itself) and reports the
 // median time per exchange and the bandwidth per rank — the BASELINE
-// "halo-exchange latency" metric as a curve.
+// "halo-exchange latency" metric as a curve.  Each exchange is timed
+// blocking (barrier, exchange, stream synchronize: the host round trip is
+// part of it).  For stream-ordered transports (rccl, ipc, local) the
+// us_stream column is the per-exchange time of `iters` exchanges enqueued
+// back to back with one synchronize — what a solver loop that never waits
+// on the host sees.
 //
 // CLI: mpi_halo_bench [min_bytes] [max_bytes] [iters]   (16 B .. 64 MiB, 50)
 //      --transport=auto|rccl|ipc|mpi-host|mpi-direct|local  --json=FILE
@@ -39,7 +44,7 @@ int main(int argc, char** argv) {
   const int left = (rank + world - 1) % world, right = (rank + 1) % world;
   if (rank == 0)
     std::printf("# halo exchange sweep: %d ranks, transport=%s, backend=%s, ring neighbours, %d iters\n"
-                "# bytes_per_msg  msgs  us_median  us_min  GB/s_per_rank(sent+recv)\n",
+                "# bytes_per_msg  msgs  us_median  us_min  GB/s_per_rank(sent+recv)  us_stream\n",
                 world, tr->name(), gmt_rt_backend_name(), iters);
   gmt_stream_t s = nullptr;
   GMT_CHECK("stream", gmt_rt_stream_create(&s, 1));
@@ -59,6 +64,15 @@ int main(int argc, char** argv) {
       GMT_CHECK("sync", gmt_rt_stream_synchronize(s));
       if (k >= 5) st.add(wtime() - t0);
     }
+    double streamed = -1.0;
+    if (ex->graph_capturable()) {
+      MPI_Barrier(MPI_COMM_WORLD);
+      const double t0 = wtime();
+      for (int k = 0; k < iters; ++k) ex->run(s);
+      GMT_CHECK("sync", gmt_rt_stream_synchronize(s));
+      streamed = (wtime() - t0) / iters;
+      MPI_Allreduce(MPI_IN_PLACE, &streamed, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+    }
     // correctness: rl holds the left neighbour's "send right" (2), rr its right's "send left" (1)
     char a = 0, c = 0;
     GMT_CHECK("chk", gmt_rt_memcpy(&a, rl.data() + bytes - 1, 1));
@@ -70,12 +84,14 @@ int main(int argc, char** argv) {
     MPI_Allreduce(MPI_IN_PLACE, &mn, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
     if (rank == 0) {
       const double gbps = 4.0 * bytes / med / 1e9;
-      std::printf("%14zu  %4d  %9.2f  %7.2f  %8.2f%s\n", bytes, 2, med * 1e6, mn * 1e6, gbps,
+      char stream_col[32] = "        -";
+      if (streamed > 0) std::snprintf(stream_col, sizeof(stream_col), "%9.2f", streamed * 1e6);
+      std::printf("%14zu  %4d  %9.2f  %7.2f  %8.2f  %s%s\n", bytes, 2, med * 1e6, mn * 1e6, gbps, stream_col,
                   bad ? "  DATA MISMATCH" : "");
       JsonRecord j;
       j.add("app", "mpi_halo_bench").add("ranks", world).add("transport", tr->name())
           .add("bytes", bytes).add("us_median", med * 1e6).add("us_min", mn * 1e6)
-          .add("GBps_per_rank", gbps).add("ok", !bad);
+          .add("GBps_per_rank", gbps).add("us_stream", streamed > 0 ? streamed * 1e6 : -1.0).add("ok", !bad);
       j.append_to(cli.get("json", ""));
     }
     if (bad) {

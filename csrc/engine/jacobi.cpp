@@ -282,7 +282,7 @@ void JacobiSolver::step_block() {
 
 // Measured cost of one fused pass of K sweeps (ms; gmt_kernel_bench
 // --only=tb --sustained=1: back-to-back launches with the default launch
-// shape and segment plan, Dirichlet sides, MI355X, profiles/r02_tb5/) on two
+// shape and segment plan, Dirichlet sides, MI355X, profiles/r02_tb6/) on two
 // domain sizes.  One-wave strips (K <= 10) run at ~3.9-4.4 ms at 32768^2;
 // two-stage strips (K >= 12) are VALU bound from K ~ 16.  K = 1 is the single-sweep kernel;
 // 0 = no kernel for that K (odd K > 10).
@@ -292,12 +292,12 @@ struct PassCosts {
   double ms[GMT_TB_MAX_SWEEPS + 1];
 };
 constexpr PassCosts kCostLarge = {32768.0 * 32768.0,
-                                  {0,    3.05, 4.27, 4.12, 4.09, 3.93, 3.97, 4.38, 4.25, 4.33, 3.93, 0,    3.59,
-                                   0,    3.52, 0,    4.31, 0,    4.72, 0,    5.02, 0,    5.43, 0,    5.84}};
+                                  {0,    3.05, 4.27, 4.26, 4.15, 4.17, 4.19, 4.17, 4.23, 4.02, 3.53, 0,    3.62,
+                                   0,    3.91, 0,    4.44, 0,    4.91, 0,    4.87, 0,    5.39, 0,    5.78}};
 constexpr PassCosts kCostSmall = {8192.0 * 8192.0,
-                                  {0,     0.20,  0.285, 0.293, 0.282, 0.284, 0.289, 0.296, 0.282,
-                                   0.308, 0.291, 0,     0.262, 0,     0.275, 0,     0.318, 0,
-                                   0.364, 0,     0.410, 0,     0.481, 0,     0.525}};
+                                  {0,     0.20,  0.279, 0.286, 0.277, 0.277, 0.281, 0.290, 0.312,
+                                   0.316, 0.290, 0,     0.261, 0,     0.289, 0,     0.299, 0,
+                                   0.318, 0,     0.351, 0,     0.417, 0,     0.486}};
 constexpr double kLaunchMs = 0.015;    // host launch + dispatch per pass
 constexpr double kExchangeMs = 0.035;  // a halo exchange not hidden by the overlap
 }  // namespace

@@ -93,6 +93,9 @@ struct Args {
   // bottom one of e1[k] rows (short: the only ones whose waves can need the
   // Dirichlet rule in y), then nmid[k] interior segments of lmid[k] rows
   int64_t e0[kMaxRect], e1[kMaxRect], nmid[kMaxRect], lmid[kMaxRect];
+  // the first and last strip groups (rule waves where a Dirichlet column is
+  // in reach) use their own, shorter interior segments
+  int64_t nmid_b[kMaxRect], lmid_b[kMaxRect];
   int nw;                        // strips per workgroup
   double quarter;                // 0.25 (EXACT): an SGPR operand
 };
@@ -349,15 +352,16 @@ void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__
   if (lt < nedge * ngroups) {
     j = lt / ngroups;
     gi = lt % ngroups;
-  } else if (lt < nedge * ngroups + a.nmid[k] * nbnd) {
+  } else if (lt < nedge * ngroups + a.nmid_b[k] * nbnd) {
     const int64_t l2 = lt - nedge * ngroups;
     j = nedge + l2 / nbnd;
     gi = l2 % nbnd == 0 ? 0 : ngroups - 1;
   } else {
-    const int64_t l3 = lt - nedge * ngroups - a.nmid[k] * nbnd;
+    const int64_t l3 = lt - nedge * ngroups - a.nmid_b[k] * nbnd;
     j = nedge + l3 / (ngroups - 2);
     gi = 1 + l3 % (ngroups - 2);
   }
+  const int64_t lmid = (gi == 0 || gi == ngroups - 1) ? a.lmid_b[k] : a.lmid[k];
   int64_t ys, ye;
   if (e0 > 0 && j == 0) {
     ys = ry0;
@@ -369,8 +373,8 @@ void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__
       ye = ry1;
     } else {
       if (e1 > 0) --j;
-      ys = ry0 + e0 + j * a.lmid[k];
-      ye = ys + a.lmid[k] < ry1 - e1 ? ys + a.lmid[k] : ry1 - e1;
+      ys = ry0 + e0 + j * lmid;
+      ye = ys + lmid < ry1 - e1 ? ys + lmid : ry1 - e1;
     }
   }
   const int nsteps = static_cast<int>((ye - ys + 3 * K + kU - 1) / kU * kU);
@@ -432,7 +436,7 @@ using namespace gmt::tb;
 // minimises rounds(L) x (L + 3K), rounds = ceil(workgroups / resident
 // workgroups), over L in [128, 2048].
 struct SegPlan {
-  int64_t e0[kMaxRect], e1[kMaxRect], nmid[kMaxRect], lmid[kMaxRect];
+  int64_t e0[kMaxRect], e1[kMaxRect], nmid[kMaxRect], lmid[kMaxRect], nmid_b[kMaxRect], lmid_b[kMaxRect];
 };
 
 template <int K>
@@ -453,7 +457,17 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
       const int64_t mid = ny - p.e0[k] - p.e1[k];
       p.nmid[k] = (mid + L - 1) / L;
       p.lmid[k] = (mid + p.nmid[k] - 1) / p.nmid[k];  // balanced lengths
-      w += ((a.nstrip[k] + a.nw - 1) / a.nw) * (p.nmid[k] + (p.e0[k] > 0) + (p.e1[k] > 0));
+      // strip groups that can reach a Dirichlet column run the rule path
+      // (~2x the VALU per step): half-length segments, so they finish with
+      // the others instead of ending the launch
+      const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
+      const bool xrule = seg_rows == 0 && ((rx0 - ring_left(K) < a.dom[0] && !(a.mask & 1)) ||
+                                           (rx1 + ring_left(K) > a.dom[0] + a.dom[1] && !(a.mask & 2)));
+      const int64_t lb = xrule ? std::max<int64_t>(64, p.lmid[k] / 2) : p.lmid[k];
+      p.nmid_b[k] = (mid + lb - 1) / lb;
+      p.lmid_b[k] = (mid + p.nmid_b[k] - 1) / p.nmid_b[k];
+      const int64_t groups = (a.nstrip[k] + a.nw - 1) / a.nw, nbnd = groups < 2 ? groups : 2;
+      w += groups * ((p.e0[k] > 0) + (p.e1[k] > 0)) + nbnd * p.nmid_b[k] + (groups - nbnd) * p.nmid[k];
     }
     *wgs = w;
   };
@@ -536,8 +550,11 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     a.e1[k] = sp.e1[k];
     a.nmid[k] = sp.nmid[k];
     a.lmid[k] = sp.lmid[k];
-    const int64_t groups = (a.nstrip[k] + a.nw - 1) / a.nw;
-    a.tstart[k + 1] = a.tstart[k] + groups * (sp.nmid[k] + (sp.e0[k] > 0) + (sp.e1[k] > 0));
+    a.nmid_b[k] = sp.nmid_b[k];
+    a.lmid_b[k] = sp.lmid_b[k];
+    const int64_t groups = (a.nstrip[k] + a.nw - 1) / a.nw, nbnd = groups < 2 ? groups : 2;
+    a.tstart[k + 1] = a.tstart[k] + groups * ((sp.e0[k] > 0) + (sp.e1[k] > 0)) + nbnd * sp.nmid_b[k] +
+                      (groups - nbnd) * sp.nmid[k];
   }
   for (int k = a.n + 1; k <= kMaxRect; ++k) a.tstart[k] = a.tstart[a.n];
   const int64_t nb = a.tstart[a.n];
