@@ -115,10 +115,14 @@ def check_engine(env, dims, tsteps, graph):
     reference.  Returns the max |difference| over both runs (0 = bitwise)."""
     from gpu_mpi_tests_amd.engine import NativeJacobi, serial_jacobi
 
+    from gpu_mpi_tests_amd.engine import group_cols
+
     py, px = dims
     k = max(1, tsteps)
-    # every rank at least 4K+8 cells each way: the overlapped core/frame split runs
-    ny, nx = py * (4 * k + 11) + 3, px * (8 * k + 37) + 5
+    # every rank big enough for the overlapped (band-first) pass: K-deep
+    # bands plus an interior in y, three workgroup-wide strips in x
+    wb = group_cols(k, 0, "cuda" if env.is_gpu else "cpu") if k > 1 else 0
+    ny, nx = py * (4 * k + 75) + 3, px * (3 * wb + 8 * k + 37) + 5
     steps = 2 * k + 3  # full passes, a remainder pass and (odd) single sweeps
     ref = serial_jacobi(ny, nx, steps) if env.rank == 0 else None
     worst = 0.0

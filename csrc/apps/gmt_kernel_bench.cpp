@@ -116,7 +116,10 @@ int main(int argc, char** argv) {
     // --only=tb: temporal-blocking kernel (jacobi5tb.hip),
     // --tb-k=12,14,16 --tb-nw=1,2,4,8 --tb-seg=0 --jacobi-n=32768
     // --tb-mask=0 (Dirichlet everywhere: rule workgroups at the edges)
+    // --jacobi-ny=8192 --jacobi-nx=16384 (default: n x n)
     const int64_t n = cli.geti("jacobi-n", 32768);
+    // --jacobi-ny / --jacobi-nx: a rectangular domain (a strong-scaling share)
+    const int64_t ny = cli.geti("jacobi-ny", n), nx = cli.geti("jacobi-nx", n);
     auto list = [&](const char* key, const char* def) {
       std::vector<int> v;
       std::string str = cli.get(key, def);
@@ -132,11 +135,11 @@ int main(int argc, char** argv) {
     const int mask = static_cast<int>(cli.geti("tb-mask", 0));
     for (int K : list("tb-k", "12,14,16")) {
       const int64_t g = K, xk = ((g + 7) / 8) * 8;
-      const int64_t ld2 = ((xk + n + g + 63) / 64) * 64, rows = n + 2 * g;
+      const int64_t ld2 = ((xk + nx + g + 63) / 64) * 64, rows = ny + 2 * g;
       Buffer<double> a(static_cast<size_t>(ld2) * rows, GMT_SPACE_DEVICE), b(a.size(), GMT_SPACE_DEVICE);
       GMT_CHECK("fill", gmt_fill_poly(0, ld2, rows, 0.0, 1e-5, 0.0, 1e-5, a.data(), ld2, s));
       GMT_CHECK("fill", gmt_fill_poly(0, ld2, rows, 0.0, 1e-5, 0.0, 1e-5, b.data(), ld2, s));
-      const int64_t rect[4] = {xk, n, g, n};
+      const int64_t rect[4] = {xk, nx, g, ny};
       for (int nw : list("tb-nw", "0"))
         for (int P : list("tb-p", "3"))
           for (int seg : list("tb-seg", "0")) {
@@ -145,10 +148,14 @@ int main(int argc, char** argv) {
               GMT_CHECK("tb", gmt_jacobi5tb(&o, 1, rect, rect, mask, a.data(), b.data(), ld2, rows, s));
             });
             char tag[96];
-            std::snprintf(tag, sizeof(tag), "%lldx%lld x%d nw%d P%d seg%d m%d", (long long)n, (long long)n, K, nw,
+            std::snprintf(tag, sizeof(tag), "%lldx%lld x%d nw%d P%d seg%d m%d", (long long)ny, (long long)nx, K, nw,
                           P, seg, mask);
-            report("jacobi5tb", K, tag, ms, K * 16.0 * n * n);
-            std::printf("%-10s    %-30s %9.1f MLUPS\n", "", tag, K * double(n) * n / (ms * 1e-3) / 1e6);
+            report("jacobi5tb", K, tag, ms, K * 16.0 * ny * nx);
+            int64_t pi[6] = {};
+            GMT_CHECK("plan", gmt_jacobi5tb_plan(&o, 1, rect, rect, mask, ld2, rows, pi));
+            std::printf("%-10s    %-30s %9.1f MLUPS  (wgs %lld resident %lld threads %lld seg %lld x %lld vgpr %lld)\n",
+                        "", tag, K * double(ny) * nx / (ms * 1e-3) / 1e6, (long long)pi[0], (long long)pi[1],
+                        (long long)pi[2], (long long)pi[3], (long long)pi[4], (long long)pi[5]);
           }
     }
   }

@@ -113,13 +113,14 @@ int main(int argc, char** argv) {
   auto tr = comm::make_transport(comm::resolve(kind, b), MPI_COMM_WORLD, b);
 
   double t_step = 0, resid = 0, halo_us = 0, max_diff = -1;
-  bool graph = false, overlap = false;
+  bool graph = false, overlap = false, band = false;
   size_t hbytes = 0, hmsgs = 0;
   int64_t lnx = 0, lny = 0;
   {
     JacobiSolver solver(*tr, c);
     graph = solver.graph_active();
     overlap = solver.overlap_active();
+    band = solver.band_first();
     hbytes = solver.bytes_per_exchange();
     hmsgs = solver.messages();
     lnx = solver.nx();
@@ -182,8 +183,8 @@ int main(int argc, char** argv) {
     std::printf("grid      = %dx%d (py x px)\n", c.py, c.px);
     std::printf("global    = %lld x %lld\n", (long long)c.ny_global, (long long)c.nx_global);
     std::printf("local     = %lld x %lld (rank 0)\n", (long long)lny, (long long)lnx);
-    std::printf("transport = %s overlap=%d graph=%d periodic=%d tblock=%d backend=%s\n", tr->name(),
-                overlap, graph, c.periodic, c.tblock, gmt_rt_backend_name());
+    std::printf("transport = %s overlap=%d%s graph=%d periodic=%d tblock=%d backend=%s\n", tr->name(),
+                overlap, band ? " (band-first)" : "", graph, c.periodic, c.tblock, gmt_rt_backend_name());
     std::printf("steps     = %d (warmup %d)\n", n_iter, n_warmup);
     std::printf("TIME step : %0.6f ms\n", t_step * 1e3);
     std::printf("MLUPS     : %0.1f (per GPU %0.1f, %0.1f GB/s per GPU at 16 B/pt)\n", mlups,

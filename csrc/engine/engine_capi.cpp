@@ -102,6 +102,7 @@ int gmt_engine_jacobi_info(void* p, int64_t* out) {
   out[11] = static_cast<int64_t>(s.tuned_overlap_s() * 1e9);  // overlap_auto timings, ns per pass
   out[12] = static_cast<int64_t>(s.tuned_serial_s() * 1e9);
   out[13] = s.exact();
+  out[14] = s.band_first();
   return 0;
 }
 int gmt_engine_jacobi_plan(void* p, int steps, int* out, int max) {

@@ -93,15 +93,14 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   GMT_CHECK("comm stream", gmt_rt_stream_create(&cs_, cp && cp[0] == '0' ? 0 : 1));
   GMT_CHECK("event", gmt_rt_event_create(&ev_start_, 0));
   GMT_CHECK("event", gmt_rt_event_create(&ev_halo_, 0));
-  GMT_CHECK("event", gmt_rt_event_create(&ev_packed_, 0));
-  const char* cap = std::getenv("GMT_CORE_AFTER_PACK");
-  core_after_pack_ = !(cap && cap[0] == '0');
 
   // deterministic, decomposition-independent initial field and Dirichlet
   // ring: u(x, y) = x^3 + y^2 at global ghost-inclusive coordinates * h
   for (int b = 0; b < 2; ++b) buf_[b] = Buffer<double>(elems, GMT_SPACE_DEVICE);
   init_field();
   resid_ws_ = Buffer<double>(gmt_jacobi_resid_workspace(nx_, ny_) + 1, GMT_SPACE_DEVICE);
+  // band-first passes: arrival counter, signal, waiter's count, error word
+  sig_ = Buffer<uint64_t>(4, GMT_SPACE_FLAGS);
   for (int b = 0; b < 2; ++b) {
     Span2D<double> f(buf_[b].data() + (xo_ - g_), nx_ + 2 * g_, ny_ + 2 * g_, ld_);
     halo_[b] = std::make_unique<Halo2D>(t_, f, g_, g_, nb_, false, GMT_SPACE_DEVICE, ks_ > 1);
@@ -120,6 +119,7 @@ void JacobiSolver::init_field() {
   }
   GMT_CHECK("init sync", gmt_rt_stream_synchronize(s_));
   parity_ = 0;
+  fresh_[0] = fresh_[1] = false;  // periodic / neighbour ghosts come from an exchange
 }
 
 void JacobiSolver::autotune_overlap() {
@@ -158,7 +158,6 @@ JacobiSolver::~JacobiSolver() {
   for (auto& g : graph2_) gmt_rt_graph_destroy(g);
   gmt_rt_event_destroy(ev_start_);
   gmt_rt_event_destroy(ev_halo_);
-  gmt_rt_event_destroy(ev_packed_);
   halo_[0].reset();
   halo_[1].reset();
   gmt_rt_stream_destroy(cs_);
@@ -173,6 +172,7 @@ void JacobiSolver::sweep_full(int parity, double* resid) {
 
 void JacobiSolver::enqueue_step(int parity) {
   Halo2D& h = *halo_[parity];
+  fresh_[parity ^ 1] = false;
   if (!h.active()) {
     sweep_full(parity, nullptr);
     return;
@@ -208,75 +208,107 @@ int JacobiSolver::halo_mask() const {
          (nb_.north >= 0 ? 8 : 0);
 }
 
-void JacobiSolver::xk_launch(int K, int n, const int64_t* rects, int parity, bool frame) {
+void JacobiSolver::xk_launch(int K, int n, const int64_t* rects, int parity, int sig_rects) {
   const double* u = buf_[parity].data();
   double* un = buf_[parity ^ 1].data();
   const int64_t dom[4] = {xo_, nx_, yo_, ny_};
   const int mask = halo_mask();
-  // the frame bands are at most K wide or K tall: one-strip workgroups
-  gmt_tb_opts o{K, frame ? 1 : cfg_.wg_waves, cfg_.seg_rows, exact_ ? 1 : 0};
+  unsigned* count = reinterpret_cast<unsigned*>(sig_.data());
+  gmt_tb_opts o{K,         cfg_.wg_waves, cfg_.seg_rows, exact_ ? 1 : 0, sig_rects, sig_rects ? count : nullptr,
+                sig_rects ? sig_.data() + 1 : nullptr};
   GMT_CHECK("jacobi tb", gmt_jacobi5tb(&o, n, rects, dom, mask, u, un, ld_, ny_ + 2 * g_, s_));
 }
 
-// ks_ sweeps u(t) -> u(t+ks) in one pass: the ks-wide halo (corners included)
-// travels on the comm stream while the fused kernel updates the core whose
-// ks-step dependency cone stays inside the interior; the ks-wide frame
-// follows once the halo has landed.
+// Output rects of a band-first pass: the bands along the halo sides (deep
+// enough for the g_-wide faces and corners the next exchange sends) first,
+// then the interior.  False when the domain is too small for an interior.
+bool JacobiSolver::band_rects(int K, int64_t* rects, int* n_bands) const {
+  const int mask = halo_mask();
+  const bool hw = mask & 1, he = mask & 2, hs = mask & 4, hn = mask & 8;
+  // W/E bands: one workgroup's strips wide, so their workgroups are full
+  const int64_t wb = std::max<int64_t>(gmt_jacobi5tb_group_cols(K, cfg_.wg_waves), g_);
+  const int64_t hb = g_;
+  const int64_t x0 = xo_ + (hw ? wb : 0), x1 = xo_ + nx_ - (he ? wb : 0);
+  const int64_t y0 = yo_ + (hs ? hb : 0), y1 = yo_ + ny_ - (hn ? hb : 0);
+  if (wb <= 0 || x1 - x0 < wb || y1 - y0 < 2 * hb + 64) return false;
+  int n = 0;
+  auto add = [&](int64_t ax, int64_t anx, int64_t ay, int64_t any) {
+    const int64_t r[4] = {ax, anx, ay, any};
+    std::copy(r, r + 4, rects + 4 * n++);
+  };
+  if (hs) add(xo_, nx_, yo_, hb);
+  if (hn) add(xo_, nx_, y1, hb);
+  if (hw) add(xo_, wb, y0, y1 - y0);
+  if (he) add(x1, wb, y0, y1 - y0);
+  *n_bands = n;
+  add(x0, x1 - x0, y0, y1 - y0);
+  return n > 0;
+}
+
+void JacobiSolver::exchange_now(int parity) {
+  Halo2D& h = *halo_[parity];
+  h.start(s_);
+  h.finish(s_);
+  fresh_[parity] = true;
+}
+
+// ks_ (or fewer) sweeps u(t) -> u(t+K) in one pass.
+//   serial:     exchange the halo of u, then one fused launch;
+//   overlap:    band-first — one launch whose boundary bands are dispatched
+//               first and raise a completion signal; the comm stream waits
+//               for it (gmt_signal_wait) and exchanges the halo of u(t+K)
+//               while the interior workgroups still run.  The pass leaves
+//               its output's halo current (fresh_), so the next pass starts
+//               without an exchange.
+// Every workgroup is one the serial pass would run too (plus short band
+// segments): no frame pass, no redundant work (the core/frame scheme of
+// round 1 cost 2-11 % per pass, profiles/r02_shares.md).
 void JacobiSolver::enqueue_block(int parity, int K) {
   Halo2D& h = *halo_[parity];
   const int64_t dom[4] = {xo_, nx_, yo_, ny_};
-  const int mask = halo_mask();
   if (!h.active()) {
-    xk_launch(K, 1, dom, parity, false);
+    xk_launch(K, 1, dom, parity, 0);
     return;
   }
-  if (!cfg_.overlap || nx_ < 4 * K + 2 || ny_ < 4 * K) {
-    h.start(s_);
-    h.finish(s_);
-    xk_launch(K, 1, dom, parity, false);
+  if (!fresh_[parity]) exchange_now(parity);
+  int64_t rects[4 * 5];
+  int nb = 0;
+  if (!cfg_.overlap || !band_rects(K, rects, &nb)) {
+    xk_launch(K, 1, dom, parity, 0);
+    fresh_[parity ^ 1] = false;
     return;
   }
-  // The core is inset only on the sides whose ghost ring is a neighbour's
-  // halo (a Dirichlet side does not wait for the exchange; the kernel's rule
-  // path handles it).  The frame — the K-wide bands along the halo sides —
-  // follows once the halo has landed.
-  const bool hw = mask & 1, he = mask & 2, hs = mask & 4, hn = mask & 8;
-  const int64_t xr = xo_ + nx_ - K;
-  const int64_t cx0 = hw ? xo_ + K : xo_, cx1 = he ? xr : xo_ + nx_;
-  const int64_t cy0 = hs ? yo_ + K : yo_, cy1 = hn ? yo_ + ny_ - K : yo_ + ny_;
-  const int64_t core[4] = {cx0, cx1 - cx0, cy0, cy1 - cy0};
+  // the comm stream forks before the launch (so it never waits for the whole
+  // pass), and its wait kernel is enqueued after it
   GMT_CHECK("event", gmt_rt_event_record(ev_start_, s_));
   GMT_CHECK("wait", gmt_rt_stream_wait_event(cs_, ev_start_));
-  // the core waits for the (few-us) halo pack: the transfer kernels are then
-  // dispatched together with the core's first waves and find free CUs —
-  // queued behind a GPU-filling core they waited ~1/3 of it for a slot and
-  // their late start stalled the core's dispatch (rocprofv3, profiles/r01_frame.md).
-  // GMT_CORE_AFTER_PACK=0 launches the core at once (A/B).
-  h.start(cs_, core_after_pack_ ? ev_packed_ : nullptr);
-  if (core_after_pack_) GMT_CHECK("wait", gmt_rt_stream_wait_event(s_, ev_packed_));
-  xk_launch(K, 1, core, parity, false);
-  h.finish(cs_);
+  xk_launch(K, nb + 1, rects, parity, nb);
+  GMT_CHECK("signal wait", gmt_signal_wait(sig_.data() + 1, sig_.data() + 2,
+                                           reinterpret_cast<unsigned*>(sig_.data() + 3), cs_));
+  Halo2D& hn = *halo_[parity ^ 1];
+  hn.start(cs_);
+  hn.finish(cs_);
   GMT_CHECK("event", gmt_rt_event_record(ev_halo_, cs_));
   GMT_CHECK("wait", gmt_rt_stream_wait_event(s_, ev_halo_));
-  int64_t frame[16];
-  int nf = 0;
-  auto add = [&](int64_t x0, int64_t nx, int64_t y0, int64_t ny) {
-    if (nx <= 0 || ny <= 0) return;
-    const int64_t r[4] = {x0, nx, y0, ny};
-    std::copy(r, r + 4, frame + 4 * nf++);
-  };
-  if (hs) add(xo_, nx_, yo_, K);
-  if (hn) add(xo_, nx_, yo_ + ny_ - K, K);
-  if (hw) add(xo_, K, cy0, cy1 - cy0);
-  if (he) add(xr, K, cy0, cy1 - cy0);
-  xk_launch(K, nf, frame, parity, true);
+  fresh_[parity ^ 1] = true;
+}
+
+bool JacobiSolver::band_mode(int K) const {
+  int64_t rects[4 * 5];
+  int nb = 0;
+  return cfg_.overlap && halo_[0] && halo_[0]->active() && band_rects(K, rects, &nb);
 }
 
 void JacobiSolver::step_block() {
-  if (graph2_[parity_])
+  if (graph2_[parity_]) {
+    // a band-first graph starts from a current halo (it was captured so)
+    const bool band = band_mode(ks_);
+    if (band && !fresh_[parity_]) exchange_now(parity_);
     GMT_CHECK("graph launch", gmt_rt_graph_launch(graph2_[parity_], s_));
-  else
+    fresh_[parity_ ^ 1] = band;
+  } else {
     enqueue_block(parity_, ks_);
+  }
   parity_ ^= 1;  // u(t+ks) lives in the other buffer
 }
 
@@ -377,8 +409,12 @@ void JacobiSolver::capture_graphs() {
     halo_[b]->finish(cs_);
   }
   GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));
+  const bool saved[2] = {fresh_[0], fresh_[1]};
   for (int p = 0; p < 4; ++p) {
     if (p >= 2 && ks_ < 2) break;
+    // serial passes capture their exchange, band-first ones start from a
+    // current halo (step_block makes sure of it)
+    fresh_[0] = fresh_[1] = p >= 2 && band_mode(ks_);
     int e = gmt_rt_stream_begin_capture(s_);
     if (e == 0) {
       if (p < 2)
@@ -387,6 +423,8 @@ void JacobiSolver::capture_graphs() {
         enqueue_block(p - 2, ks_);
       e = gmt_rt_stream_end_capture(s_, p < 2 ? &graph_[p] : &graph2_[p - 2]);
     }
+    fresh_[0] = saved[0];
+    fresh_[1] = saved[1];
     if (e != 0) {
       std::printf("# jacobi: hipGraph capture unavailable (%s); running eagerly\n",
                   gmt_rt_error_string(e));
@@ -405,20 +443,27 @@ void JacobiSolver::step() {
     GMT_CHECK("graph launch", gmt_rt_graph_launch(graph_[parity_], s_));
   else
     enqueue_step(parity_);
+  fresh_[parity_ ^ 1] = false;
   parity_ ^= 1;
 }
 
 void JacobiSolver::synchronize() {
   GMT_CHECK("sync", gmt_rt_stream_synchronize(s_));
   GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));
+  uint64_t err = 0;
+  GMT_CHECK("signal D2H", gmt_rt_memcpy(&err, sig_.data() + 3, sizeof(err)));
+  if (err != 0) {
+    std::printf("JacobiSolver: a band-first pass timed out waiting for its boundary bands (error %llu)\n",
+                static_cast<unsigned long long>(err));
+    abort_job(EXIT_FAILURE);
+  }
   watchdog_kick("jacobi synchronize");
 }
 
 double JacobiSolver::residual() {
-  Halo2D& h = *halo_[parity_];
-  h.start(s_);
-  h.finish(s_);
+  if (!fresh_[parity_]) exchange_now(parity_);
   sweep_full(parity_, resid_ws_.data());
+  fresh_[parity_ ^ 1] = false;
   t_.allreduce_sum(resid_ws_.data(), 1, s_);
   double r = 0.0;
   GMT_CHECK("resid D2H", gmt_rt_memcpy_async(&r, resid_ws_.data(), sizeof(double), s_));
@@ -436,6 +481,7 @@ void JacobiSolver::exchange_only() {
   h.start(cs_);
   h.finish(cs_);
   GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));
+  fresh_[parity_] = true;
 }
 
 void JacobiSolver::copy_interior(double* host) const {

@@ -8,6 +8,7 @@
 // arguments are ignored — every call completes before returning.  Serial on
 // purpose: several MPI ranks share the CPU in the tests, and a rank-local
 // thread pool would only oversubscribe it.
+#include <algorithm>
 #include <cmath>
 #include <sched.h>
 
@@ -196,7 +197,41 @@ int gmt_jacobi5tb(const gmt_tb_opts* o, int n_rect, const int64_t* rects, const 
     if (r[1] <= 0 || r[3] <= 0) continue;
     if (r[0] < K || r[2] < K || r[0] + r[1] + K > ld || r[2] + r[3] + K > nrows) return 1;
   }
-  return host_xk(K, n_rect, rects, dom, mask, u, un, ld);
+  if (o->signal_rects < 0 || o->signal_rects > n_rect || (o->signal_rects > 0 && (!o->signal_count || !o->signal)))
+    return 1;
+  for (int k = 0; k < o->signal_rects; ++k)
+    if (rects[4 * k + 1] <= 0 || rects[4 * k + 3] <= 0) return 1;
+  const int rc = host_xk(K, n_rect, rects, dom, mask, u, un, ld);
+  if (rc == 0 && o->signal_rects > 0) __atomic_fetch_add(o->signal, uint64_t{1}, __ATOMIC_RELEASE);
+  return rc;
+}
+
+int64_t gmt_jacobi5tb_group_cols(int sweeps, int wg_waves) {
+  if (!gmt_jacobi5tb_supported(sweeps)) return 0;
+  // the GPU kernel's strip geometry: 192 - 2 * ceil3(K) columns per strip
+  const int G = sweeps <= 10 ? 1 : 2, cap = 8 / G;
+  const int nw = std::min(wg_waves > 0 ? wg_waves : (G == 1 ? 4 : 2), cap);
+  return static_cast<int64_t>(nw) * (192 - 2 * ((sweeps + 2) / 3 * 3));
+}
+
+// in-order CPU streams: the signal was raised before this call runs
+int gmt_signal_wait(const uint64_t* signal, uint64_t* seen, unsigned* err, void*) {
+  if (!signal || !seen || !err) return 1;
+  const uint64_t want = __atomic_load_n(seen, __ATOMIC_RELAXED) + 1;
+  if (__atomic_load_n(signal, __ATOMIC_ACQUIRE) < want) __atomic_fetch_or(err, 2u, __ATOMIC_RELAXED);
+  __atomic_store_n(seen, want, __ATOMIC_RELAXED);
+  return 0;
+}
+
+// the CPU backend runs every rect as one "workgroup" of one thread
+int gmt_jacobi5tb_plan(const gmt_tb_opts* o, int n_rect, const int64_t* rects, const int64_t*, int, int64_t ld,
+                       int64_t nrows, int64_t info[6]) {
+  const int K = o ? o->sweeps : 0;
+  if (!info || !gmt_jacobi5tb_supported(K) || n_rect < 0 || n_rect > 8 || ld <= 0 || nrows <= 0) return 1;
+  const int64_t rows0 = n_rect > 0 ? rects[3] : 0;
+  const int64_t v[6] = {n_rect, 1, 1, rows0, 1, 0};
+  for (int j = 0; j < 6; ++j) info[j] = v[j];
+  return 0;
 }
 
 

@@ -9,10 +9,13 @@
 //   * 2-D Cartesian decomposition (py x px ranks), ghost width 1 (2 with
 //     tblock), fp64;
 //   * one step = halo exchange of u + one Jacobi sweep u -> un + swap;
-//   * overlap: the interior "core" sweep runs on the compute stream while
-//     the halo (fused pack kernel + RCCL/IPC/MPI transfer + unpack) runs on a
-//     high-priority comm stream; the 1-2 cell boundary frame is swept after
-//     the halo lands (gmt_jacobi5_rects);
+//   * overlap: single sweeps — the interior "core" sweep runs on the compute
+//     stream while the halo (fused pack kernel + RCCL/IPC/MPI transfer +
+//     unpack) runs on a high-priority comm stream; the 1-2 cell boundary
+//     frame is swept after the halo lands (gmt_jacobi5_rects).  Fused
+//     passes run band-first: the boundary bands of the pass finish first
+//     and signal, and the exchange of the pass's OUTPUT runs under the rest
+//     of it (enqueue_block);
 //   * graph: with a stream-ordered transport (rccl, local) both step parities
 //     are captured into hipGraphs and replayed — one host call per step, so
 //     small per-GPU domains (strong scaling at 8 GPUs) are not launch-bound.
@@ -98,6 +101,8 @@ class JacobiSolver {
   int tsteps() const { return ks_; }
   int ghost() const { return g_; }
   bool overlap_active() const { return cfg_.overlap && halo_[0] && halo_[0]->active(); }
+  // the fused passes overlap band-first (enqueue_block)
+  bool band_first() const { return ks_ > 1 && band_mode(ks_); }
   const Neighbors& neighbors() const { return nb_; }
   // overlap_auto: seconds per pass measured {overlap, serial} (mean over ranks), 0 if not tuned
   double tuned_overlap_s() const { return tune_s_[0]; }
@@ -108,7 +113,10 @@ class JacobiSolver {
   void enqueue_step(int parity);
   void enqueue_block(int parity, int k);  // k <= ks_ fused sweeps
   // one fused k-sweep launch on `n` output rects (gmt_jacobi5tb)
-  void xk_launch(int k, int n, const int64_t* rects, int parity, bool frame);
+  void xk_launch(int k, int n, const int64_t* rects, int parity, int sig_rects);
+  bool band_rects(int k, int64_t* rects, int* n_bands) const;
+  bool band_mode(int k) const;  // the fused k-sweep pass runs band-first (overlap)
+  void exchange_now(int parity);  // blocking-order halo exchange of buf_[parity] on the compute stream
   void step_block();
   void sweep_full(int parity, double* resid);
   void capture_graphs();
@@ -127,9 +135,10 @@ class JacobiSolver {
   Buffer<double> buf_[2];
   std::unique_ptr<Halo2D> halo_[2];
   Buffer<double> resid_ws_;
+  Buffer<uint64_t> sig_;  // band-first completion signal (GMT_SPACE_FLAGS)
+  bool fresh_[2] = {false, false};  // buf_[b]'s ghost ring holds the neighbours' current values
   gmt_stream_t s_ = nullptr, cs_ = nullptr;
-  gmt_event_t ev_start_ = nullptr, ev_halo_ = nullptr, ev_packed_ = nullptr;
-  bool core_after_pack_ = true;
+  gmt_event_t ev_start_ = nullptr, ev_halo_ = nullptr;
   gmt_graph_t graph_[2] = {nullptr, nullptr};   // single sweep, per parity
   gmt_graph_t graph2_[2] = {nullptr, nullptr};  // fused ks_-sweep block, per parity
   int parity_ = 0;  // buf_[parity_] holds the current u

@@ -118,10 +118,33 @@ typedef struct gmt_tb_opts {
   int exact;    /* 1: multiply by 1/4 per level (bitwise for any magnitude);
                    0: power-of-two scaled levels (bitwise unless a value is
                    subnormal or |u| * 4^K overflows) */
+  /* Completion signal (0 = none): the workgroups of rects[0 .. signal_rects)
+     — non-empty rects, given short segments — are dispatched first, and the
+     last of them to finish adds 1 to *signal once their output is visible
+     device-wide, while the rest of the launch still runs.  A stream can wait
+     for it with gmt_signal_wait.  signal_count: a zeroed arrival counter
+     (reset by the last arrival); both in GMT_SPACE_FLAGS memory. */
+  int signal_rects;
+  unsigned* signal_count;
+  uint64_t* signal;
 } gmt_tb_opts;
 int gmt_jacobi5tb_supported(int sweeps);
 int gmt_jacobi5tb(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, const int64_t* dom,
                   int halo_mask, const double* u, double* un, int64_t ld, int64_t nrows, void* stream);
+/* The launch gmt_jacobi5tb would make, without launching: info = {workgroups,
+ * resident workgroups on the device, threads per workgroup, rows per interior
+ * segment and interior segments of rects[0], VGPRs per lane}. */
+/* Output columns one workgroup of the fused kernel covers (strips per
+ * workgroup x output columns per strip) for `sweeps` and wg_waves (0 = default). */
+int64_t gmt_jacobi5tb_group_cols(int sweeps, int wg_waves);
+int gmt_jacobi5tb_plan(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, const int64_t* dom,
+                       int halo_mask, int64_t ld, int64_t nrows, int64_t info[6]);
+
+/* One-workgroup kernel on `stream`: waits until *signal > *seen (a
+ * gmt_tb_opts completion signal), then advances *seen by one — a stream
+ * ordered wait that replays correctly in a hipGraph.  Gives up after about a
+ * second and sets *err.  All three in GMT_SPACE_FLAGS memory. */
+int gmt_signal_wait(const uint64_t* signal, uint64_t* seen, unsigned* err, void* stream);
 
 /* ---- Stream-ordered IPC exchange (csrc/kernels/ipc.hip), one launch:
  *      e = *epoch + 1.  Send channel: wait until *wait >= e - 2 (receiver done

@@ -18,6 +18,9 @@
 // system-scope release writes its L2 back before the flag store, and the
 // receiver's system-scope acquire invalidates its caches before it reads
 // remote memory; nothing writes into another device's cached memory.
+// gmt_signal_wait (below) is the same kind of stream-ordered wait for a
+// completion signal raised inside another stream's kernel (gmt_tb_opts).
+//
 // The epoch lives in device memory (read at the start, advanced by the last
 // workgroup of the recv step), so replayed graphs stay in step.
 //
@@ -114,8 +117,30 @@ __global__ __launch_bounds__(kBlock) void ipc_exchange_kernel(Args a) {
   }
 }
 
+// gmt_signal_wait: thread 0 polls the signal (uncached memory) with sleeps
+__global__ __launch_bounds__(kWave) void signal_wait_kernel(const uint64_t* signal, uint64_t* seen, unsigned* err) {
+  if (threadIdx.x != 0) return;
+  const uint64_t want = __hip_atomic_load(seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  unsigned it = 0;
+  while (__hip_atomic_load(const_cast<uint64_t*>(signal), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < want) {
+    __builtin_amdgcn_s_sleep(2);
+    if (++it == kSpinLimit) {
+      __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+  __hip_atomic_store(seen, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace ipc
 }  // namespace gmt
+
+extern "C" int gmt_signal_wait(const uint64_t* signal, uint64_t* seen, unsigned* err, void* stream) {
+  using namespace gmt;
+  if (!signal || !seen || !err) return static_cast<int>(hipErrorInvalidValue);
+  ipc::signal_wait_kernel<<<1, kWave, 0, static_cast<hipStream_t>(stream)>>>(signal, seen, err);
+  GMT_RET_LAUNCH();
+}
 
 extern "C" int gmt_ipc_exchange(int n_send, const gmt_ipc_chan* sends, int n_recv, const gmt_ipc_chan* recvs,
                                 uint64_t* epoch, unsigned* counters, unsigned* err, void* stream) {

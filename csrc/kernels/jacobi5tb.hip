@@ -98,6 +98,12 @@ struct Args {
   int64_t nmid_b[kMaxRect], lmid_b[kMaxRect];
   int nw;                        // strips per workgroup
   double quarter;                // 0.25 (EXACT): an SGPR operand
+  // completion signal of the leading workgroups (gmt_tb_opts.signal_rects):
+  // workgroups t < sig_wgs are dispatched first, unswizzled; the last of
+  // them to finish adds 1 to *signal once its stores are visible device-wide
+  int64_t sig_wgs;
+  unsigned* sig_count;
+  uint64_t* signal;
 };
 
 struct d3 {
@@ -329,14 +335,13 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
 // (adjacent strips share their overlap columns in the CU's L1 / the XCD's
 // L2).  G == 1: every wave is independent (no barrier).
 template <int K, bool EXACT, bool EDGE>
-__global__ __launch_bounds__(kMaxThreads) __attribute__((amdgpu_waves_per_eu(2)))
-void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__ un, int64_t nblocks) {
+__device__ __forceinline__ void tb_block(const Args& a, const double* __restrict__ u, double* __restrict__ un,
+                                         int64_t t) {
   constexpr int G = n_stages(K);
   extern __shared__ d2 lds_dyn[];
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
   const int sl = wave / G, stage = wave % G;
-  const int64_t t = xcd_swizzle(blockIdx.x, nblocks);
   int k = 0;
   while (k + 1 < a.n && t >= a.tstart[k + 1]) ++k;
   const int64_t lt = t - a.tstart[k];
@@ -417,6 +422,29 @@ void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__
   }
 }
 
+template <int K, bool EXACT, bool EDGE>
+__global__ __launch_bounds__(kMaxThreads) __attribute__((amdgpu_waves_per_eu(2)))
+void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__ un, int64_t nblocks) {
+  const int64_t ns = a.sig_wgs;
+  const int64_t b = blockIdx.x;
+  // signalling workgroups first, in dispatch order over all XCDs; the rest
+  // XCD-contiguous
+  const int64_t t = b < ns ? b : ns + xcd_swizzle(b - ns, nblocks - ns);
+  tb_block<K, EXACT, EDGE>(a, u, un, t);
+  if (t < ns) {
+    // every wave's stores written back past its XCD's L2, then one arrival
+    // per workgroup (vector atomics on uncached memory)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(a.sig_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+            static_cast<unsigned>(ns - 1)) {
+      __hip_atomic_store(a.sig_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(a.signal, uint64_t{1}, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 }  // namespace tb
 }  // namespace gmt
 
@@ -439,14 +467,25 @@ struct SegPlan {
   int64_t e0[kMaxRect], e1[kMaxRect], nmid[kMaxRect], lmid[kMaxRect], nmid_b[kMaxRect], lmid_b[kMaxRect];
 };
 
+// Signalling rects (k < sig_rects: the boundary bands of a pass whose halo
+// exchange overlaps the rest of it) get short segments, max(128, L/3) rows
+// and no edge split: their workgroups must finish early in the launch.
 template <int K>
-SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t resident_wgs) {
+SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t resident_wgs, int sig_rects) {
   SegPlan p{};
   const int64_t edge = std::max<int64_t>(64, K);
   auto fill = [&](int64_t L, int64_t* wgs) {
     int64_t w = 0;
     for (int k = 0; k < a.n; ++k) {
       const int64_t ny = a.r[k][3], ry0 = a.r[k][2], ry1 = ry0 + ny;
+      if (k < sig_rects) {
+        const int64_t lb = std::min<int64_t>(std::max<int64_t>(128, L / 3), lmax);
+        p.e0[k] = p.e1[k] = 0;
+        p.nmid[k] = p.nmid_b[k] = (ny + lb - 1) / lb;
+        p.lmid[k] = p.lmid_b[k] = (ny + p.nmid[k] - 1) / p.nmid[k];
+        w += (a.nstrip[k] + a.nw - 1) / a.nw * p.nmid[k];
+        continue;
+      }
       const bool top = seg_rows == 0 && ry0 - K < a.dom[2] && !(a.mask & 4);
       const bool bot = seg_rows == 0 && ry1 + K > a.dom[2] + a.dom[3] && !(a.mask & 8);
       p.e0[k] = p.e1[k] = 0;
@@ -491,9 +530,12 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
   return p;
 }
 
+// Fills the kernel arguments and the launch shape; info (optional) gets
+// {workgroups, resident workgroups, threads per workgroup, rows per interior
+// segment and interior segments of the first rect, VGPRs per lane}.
 template <int K, bool EXACT, bool EDGE>
 int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int64_t* dom, int mask, const double* u,
-              double* un, int64_t ld, int64_t nrows, hipStream_t s) {
+              double* un, int64_t ld, int64_t nrows, hipStream_t s, int64_t* info = nullptr) {
   constexpr int G = n_stages(K);
   constexpr int kMaxStrips = kMaxThreads / kWave / G;
   Args a{};
@@ -543,7 +585,8 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     per_cu = occ * cus;
     resident[a.nw].store(per_cu, std::memory_order_relaxed);
   }
-  const SegPlan sp = plan_segments<K>(a, o.seg_rows, lmax, per_cu);
+  const int sig_rects = o.signal_rects;  // non-empty rects (checked): the same indices after the compaction
+  const SegPlan sp = plan_segments<K>(a, o.seg_rows, lmax, per_cu, sig_rects);
   a.tstart[0] = 0;
   for (int k = 0; k < a.n; ++k) {
     a.e0[k] = sp.e0[k];
@@ -558,13 +601,23 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   }
   for (int k = a.n + 1; k <= kMaxRect; ++k) a.tstart[k] = a.tstart[a.n];
   const int64_t nb = a.tstart[a.n];
+  a.sig_wgs = a.tstart[sig_rects];
+  a.sig_count = o.signal_count;
+  a.signal = o.signal;
+  if (info) {
+    hipFuncAttributes fa{};
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE>));
+    const int64_t v[6] = {nb, per_cu, a.nw * G * kWave, a.lmid[0], a.nmid[0], fa.numRegs};
+    for (int j = 0; j < 6; ++j) info[j] = v[j];
+    return 0;
+  }
   jacobi5tb_kernel<K, EXACT, EDGE><<<grid_1d(nb), a.nw * G * kWave, smem, s>>>(a, u, un, nb);
   return static_cast<int>(hipGetLastError());
 }
 
 template <int K>
 int dispatch_k(const gmt_tb_opts& o, bool exact, int n_rect, const int64_t* rects, const int64_t* dom, int mask,
-               const double* u, double* un, int64_t ld, int64_t nrows, hipStream_t s) {
+               const double* u, double* un, int64_t ld, int64_t nrows, hipStream_t s, int64_t* info) {
   // a rect narrower than a strip whose width is 1 mod 3 ends inside a lane:
   // that lane stores its first column alone (wider rects end on a lane
   // boundary: their last strip is shifted to end at the rect's edge)
@@ -573,10 +626,10 @@ int dispatch_k(const gmt_tb_opts& o, bool exact, int n_rect, const int64_t* rect
     if (rects[4 * k + 1] > 0 && rects[4 * k + 3] > 0 && rects[4 * k + 1] < strip_out(K) && rects[4 * k + 1] % 3 == 1)
       edge = true;
   if (edge)
-    return exact ? launch_tb<K, true, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s)
-                 : launch_tb<K, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s);
-  return exact ? launch_tb<K, true, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s)
-               : launch_tb<K, false, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s);
+    return exact ? launch_tb<K, true, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
+                 : launch_tb<K, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
+  return exact ? launch_tb<K, true, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
+               : launch_tb<K, false, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
 }
 
 }  // namespace
@@ -585,21 +638,26 @@ extern "C" int gmt_jacobi5tb_supported(int sweeps) {
   return (sweeps >= 1 && sweeps <= kMaxK1) || (sweeps > kMaxK1 && sweeps <= GMT_TB_MAX_SWEEPS && sweeps % 2 == 0);
 }
 
-extern "C" int gmt_jacobi5tb(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, const int64_t* dom,
-                             int halo_mask, const double* u, double* un, int64_t ld, int64_t nrows, void* stream) {
+namespace {
+int jacobi5tb_run(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
+                  const double* u, double* un, int64_t ld, int64_t nrows, void* stream, int64_t* info) {
   gmt_tb_opts o{};
   if (opts) o = *opts;
   const int K = o.sweeps;
   if (!gmt_jacobi5tb_supported(K)) return static_cast<int>(hipErrorInvalidValue);
   if (n_rect < 0 || n_rect > kMaxRect) return static_cast<int>(hipErrorInvalidValue);
-  if (o.wg_waves < 0 || o.wg_waves > kMaxThreads / kWave || o.seg_rows < 0)
+  if (o.wg_waves < 0 || o.wg_waves > kMaxThreads / kWave || o.seg_rows < 0 || o.signal_rects < 0 ||
+      o.signal_rects > n_rect || (o.signal_rects > 0 && (!o.signal_count || !o.signal)))
     return static_cast<int>(hipErrorInvalidValue);
   if ((reinterpret_cast<uintptr_t>(u) & 7u) || (reinterpret_cast<uintptr_t>(un) & 7u) || ld <= 0)
     return static_cast<int>(hipErrorInvalidValue);
   if (static_cast<uint64_t>(ld) * 8u > 0xffffffffull) return static_cast<int>(hipErrorInvalidValue);
   for (int k = 0; k < n_rect; ++k) {
     const int64_t* r = rects + 4 * k;
-    if (r[1] <= 0 || r[3] <= 0) continue;
+    if (r[1] <= 0 || r[3] <= 0) {
+      if (k < o.signal_rects) return static_cast<int>(hipErrorInvalidValue);  // a signalling rect is never empty
+      continue;
+    }
     // the K-wide ring around the rect exists
     if (r[0] < K || r[2] < K || r[0] + r[1] + K > ld || r[2] + r[3] + K > nrows)
       return static_cast<int>(hipErrorInvalidValue);
@@ -609,7 +667,7 @@ extern "C" int gmt_jacobi5tb(const gmt_tb_opts* opts, int n_rect, const int64_t*
   switch (K) {
 #define GMT_TB_CASE(KK) \
   case KK:              \
-    return dispatch_k<KK>(o, exact, n_rect, rects, dom, halo_mask, u, un, ld, nrows, s);
+    return dispatch_k<KK>(o, exact, n_rect, rects, dom, halo_mask, u, un, ld, nrows, s, info);
     GMT_TB_CASE(1)
     GMT_TB_CASE(2)
     GMT_TB_CASE(3)
@@ -631,4 +689,25 @@ extern "C" int gmt_jacobi5tb(const gmt_tb_opts* opts, int n_rect, const int64_t*
     default:
       return static_cast<int>(hipErrorInvalidValue);
   }
+}
+}  // namespace
+
+extern "C" int gmt_jacobi5tb(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, const int64_t* dom,
+                             int halo_mask, const double* u, double* un, int64_t ld, int64_t nrows, void* stream) {
+  return jacobi5tb_run(opts, n_rect, rects, dom, halo_mask, u, un, ld, nrows, stream, nullptr);
+}
+
+extern "C" int64_t gmt_jacobi5tb_group_cols(int sweeps, int wg_waves) {
+  if (!gmt_jacobi5tb_supported(sweeps)) return 0;
+  const int G = n_stages(sweeps), cap = kMaxThreads / kWave / G;
+  const int nw = std::min(wg_waves > 0 ? wg_waves : (G == 1 ? 4 : 2), cap);
+  return static_cast<int64_t>(nw) * strip_out(sweeps);
+}
+
+extern "C" int gmt_jacobi5tb_plan(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, const int64_t* dom,
+                                  int halo_mask, int64_t ld, int64_t nrows, int64_t info[6]) {
+  if (!info) return static_cast<int>(hipErrorInvalidValue);
+  // u/un only pass the alignment check: nothing is launched or dereferenced
+  const double* p = reinterpret_cast<const double*>(alignof(double));
+  return jacobi5tb_run(opts, n_rect, rects, dom, halo_mask, p, const_cast<double*>(p), ld, nrows, nullptr, info);
 }

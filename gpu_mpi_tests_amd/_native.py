@@ -50,6 +50,9 @@ class TbOpts(ctypes.Structure):
         ("wg_waves", c_int),
         ("seg_rows", c_int),
         ("exact", c_int),
+        ("signal_rects", c_int),
+        ("signal_count", c_vp),
+        ("signal", c_vp),
     ]
 
 _SIGS = {
@@ -73,6 +76,9 @@ _SIGS = {
     ),
     "gmt_jacobi5tb_supported": (c_int, [c_int]),
     "gmt_jacobi5tb": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_vp]),
+    "gmt_jacobi5tb_plan": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_i64, c_i64, c_vp]),
+    "gmt_jacobi5tb_group_cols": (c_i64, [c_int, c_int]),
+    "gmt_signal_wait": (c_int, [c_vp, c_vp, c_vp, c_vp]),
     "gmt_error_string": (ctypes.c_char_p, [c_int]),
     "gmt_device_synchronize": (c_int, []),
     "gmt_build_info": (ctypes.c_char_p, []),

@@ -84,12 +84,21 @@ def load(device: str = "cuda") -> ctypes.CDLL:
     lib.gmt_engine_backend.restype = ctypes.c_char_p
     lib.gmt_engine_deriv_bench.argtypes = [i64, i64, c_int, c_int, c_int, c_int, c_int, vp, vp]
     lib.gmt_engine_deriv_bench.restype = c_int
+    # from libgmt (a dependency of the engine library: found through its handle)
+    lib.gmt_jacobi5tb_group_cols.argtypes = [c_int, c_int]
+    lib.gmt_jacobi5tb_group_cols.restype = i64
     got = lib.gmt_engine_backend().decode()
     if got != kind:
         raise EngineError(f"{path} bound to the {got} runtime, expected {kind} "
                           "(another libgmt.so is already loaded in this process)")
     _libs[kind] = lib
     return lib
+
+
+def group_cols(sweeps: int, wg_waves: int = 0, device: str = "cpu") -> int:
+    """Output columns one workgroup of the fused K-sweep kernel covers: the
+    width of the W/E bands of a band-first (overlapped) pass."""
+    return int(load(device).gmt_jacobi5tb_group_cols(int(sweeps), int(wg_waves)))
 
 
 class _StdoutToStderr:
@@ -177,10 +186,13 @@ class NativeJacobi:
                                                        cid, ctypes.byref(opts))
         if not self.h:
             raise EngineError("gmt_engine_jacobi_create failed")
-        info = (ctypes.c_int64 * 14)()
+        info = (ctypes.c_int64 * 15)()
         self.lib.gmt_engine_jacobi_info(self.h, info)
         (self.nx, self.ny, self.off_x, self.off_y, self.halo_bytes, self.halo_msgs,
-         graph_on, overlap_on, _, _, tb, t_ov, t_ser, exact_on) = list(info)
+         graph_on, overlap_on, _, _, tb, t_ov, t_ser, exact_on, band_on) = list(info)
+        # overlapped fused passes run band-first (boundary bands signal, the
+        # output halo travels under the interior)
+        self.band_first = bool(band_on)
         self.exact = bool(exact_on)
         # overlap="auto": measured seconds per fused pass {overlap, serial} (mean over ranks)
         self.tuned = {"overlap_s": t_ov / 1e9, "serial_s": t_ser / 1e9} if auto and t_ov else None

@@ -5,7 +5,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 export TMPDIR=/tmp
-OUT=gpurun_out/shares
+OUT=${OUT:-gpurun_out/shares}
 mkdir -p $OUT
 M=/opt/conda/bin/mpirun
 K=${K:-20}

@@ -53,6 +53,31 @@ def test_engine_periodic_matches_serial(env, ny, nx, steps, tblock, graph):
     assert float(np.abs(got - ref).max()) < 1e-13
 
 
+@pytest.mark.parametrize("ny,nx,steps,tblock,wg", [(260, 1100, 13, 4, 1), (300, 1100, 45, 12, 0),
+                                                  (400, 1300, 47, 20, 0), (333, 1501, 61, 24, 0)])
+@pytest.mark.parametrize("graph", [False, True])
+def test_engine_band_first_matches_serial(env, ny, nx, steps, tblock, wg, graph):
+    """Overlapped fused passes run band-first (csrc/engine/jacobi.cpp
+    enqueue_block): the boundary bands' workgroups raise a completion signal
+    inside the launch, the comm stream waits for it with gmt_signal_wait and
+    exchanges the pass's output halo under the interior.  Remainder passes
+    (K < tsteps) and graph replays of both parities included; bitwise."""
+    from gpu_mpi_tests_amd import engine
+
+    e = engine.NativeJacobi(ny, nx, env, periodic=True, overlap=True, graph=graph, tblock=tblock, wg_waves=wg)
+    try:
+        assert e.band_first and e.graph == graph
+        e.run(steps)
+        e.synchronize()
+        e.run(tblock + 1)
+        e.synchronize()
+        got = e.interior()
+    finally:
+        e.close()
+    ref = engine.serial_jacobi(ny, nx, steps + tblock + 1, True)
+    assert float(np.abs(got - ref).max()) == 0.0
+
+
 @pytest.mark.parametrize("tblock", [0, 12, 14])
 def test_engine_dirichlet_repeated_runs(env, tblock):
     """run() called several times (graph replays of both parities) == one serial run."""
@@ -106,6 +131,19 @@ def test_app_jacobi_ipc_graph_matches_serial(np_):
     out = _app(["mpi_jacobi2d", "301", "23", "--check", "--tblock", "--tsteps=4", "--warmup=3", "--graph",
                 "--transport=ipc"], np_=np_)
     assert re.search(r"transport = ipc overlap=\d graph=1", out), out
+    m = re.search(r"check\s*: max\|diff\| vs serial = ([0-9.eE+-]+) OK", out)
+    assert m and float(m.group(1)) == 0.0, out
+
+
+@pytest.mark.parametrize("np_,transport,extra", [(1, "rccl", ["--periodic"]), (2, "ipc", ["--graph"]),
+                                                 (3, "ipc", ["--dims=1x3"]), (2, "mpi-host", [])])
+def test_app_jacobi_band_first(np_, transport, extra):
+    """Band-first overlapped passes across processes sharing the GPU (the
+    exchange kernels run beside the pass's interior workgroups); bitwise."""
+    nx = 1200 * (3 if "--dims=1x3" in extra else 1)
+    out = _app(["mpi_jacobi2d", f"--ny=400", f"--nx={nx}", "0", "45", "--check", "--tblock", "--tsteps=20",
+                "--warmup=20", f"--transport={transport}", *extra], np_=np_)
+    assert "overlap=1 (band-first)" in out, out
     m = re.search(r"check\s*: max\|diff\| vs serial = ([0-9.eE+-]+) OK", out)
     assert m and float(m.group(1)) == 0.0, out
 
