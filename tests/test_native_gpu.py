@@ -199,6 +199,20 @@ def test_engine_deriv_bench_single_rank(env):
     assert r["allreduce_max_rel_err"] < 1e-12
 
 
+def test_engine_rccl_beside_torch_process_group():
+    """Every rank of a multi-GPU bench.py run holds torch's RCCL process group
+    and the engine's own RCCL communicator at once: both live in one process
+    (tests/rccl_coexist_worker.py), bitwise result."""
+    import sys
+
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", "29561",
+                        os.path.join(ROOT, "tests", "rccl_coexist_worker.py")],
+                       capture_output=True, text=True, timeout=110, cwd="/tmp", env=env)
+    assert p.returncode == 0 and "COEXIST OK 0.0" in p.stdout, f"{p.stdout[-2000:]}\n{p.stderr[-3000:]}"
+
+
 def test_engine_overlap_autotune_periodic(env):
     """overlap="auto" (bench.py default): both modes timed on the real field,
     then the initial field restored — the result still equals the serial run."""
