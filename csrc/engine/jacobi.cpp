@@ -314,9 +314,11 @@ void JacobiSolver::step_block() {
 
 // Measured cost of one fused pass of K sweeps (ms; gmt_kernel_bench
 // --only=tb --sustained=1: back-to-back launches with the default launch
-// shape and segment plan, Dirichlet sides, MI355X, profiles/r02_tb6/) on two
-// domain sizes.  One-wave strips (K <= 10) run at ~3.9-4.4 ms at 32768^2;
-// two-stage strips (K >= 12) are VALU bound from K ~ 16.  K = 1 is the single-sweep kernel;
+// shape and segment plan, Dirichlet sides, MI355X, profiles/r02_tb4c.md, the
+// 4-column kernel) on two domain sizes.  One-wave strips (K <= 8) run at
+// ~3.7-4.1 ms at 32768^2 (K = 9, 10 sit at 253-255 VGPRs); two-stage strips
+// (K >= 12) are VALU bound from K ~ 16; K = 22, 24 exceed the register file
+// at 2 waves per SIMD and spill (twice the time: the planner avoids them).
 // 0 = no kernel for that K (odd K > 10).
 namespace {
 struct PassCosts {
@@ -324,12 +326,12 @@ struct PassCosts {
   double ms[GMT_TB_MAX_SWEEPS + 1];
 };
 constexpr PassCosts kCostLarge = {32768.0 * 32768.0,
-                                  {0,    3.05, 4.27, 4.26, 4.15, 4.17, 4.19, 4.17, 4.23, 4.02, 3.53, 0,    3.62,
-                                   0,    3.91, 0,    4.44, 0,    4.91, 0,    4.87, 0,    5.39, 0,    5.78}};
+                                  {0,    3.98, 4.13, 3.79, 3.86, 3.85, 3.68, 3.85, 3.91, 4.58, 4.57, 0,    3.63,
+                                   0,    3.76, 0,    3.89, 0,    4.30, 0,    4.68, 0,    8.98, 0,    9.78}};
 constexpr PassCosts kCostSmall = {8192.0 * 8192.0,
-                                  {0,     0.20,  0.279, 0.286, 0.277, 0.277, 0.281, 0.290, 0.312,
-                                   0.316, 0.290, 0,     0.261, 0,     0.289, 0,     0.299, 0,
-                                   0.318, 0,     0.351, 0,     0.417, 0,     0.486}};
+                                  {0,     0.311, 0.300, 0.294, 0.292, 0.292, 0.302, 0.287, 0.289,
+                                   0.317, 0.322, 0,     0.264, 0,     0.284, 0,     0.289, 0,
+                                   0.319, 0,     0.349, 0,     0.676, 0,     0.714}};
 constexpr double kLaunchMs = 0.015;    // host launch + dispatch per pass
 constexpr double kExchangeMs = 0.035;  // a halo exchange not hidden by the overlap
 }  // namespace

@@ -208,10 +208,10 @@ int gmt_jacobi5tb(const gmt_tb_opts* o, int n_rect, const int64_t* rects, const 
 
 int64_t gmt_jacobi5tb_group_cols(int sweeps, int wg_waves) {
   if (!gmt_jacobi5tb_supported(sweeps)) return 0;
-  // the GPU kernel's strip geometry: 192 - 2 * ceil3(K) columns per strip
+  // the GPU kernel's strip geometry: 256 - 2 * ceil4(K) columns per strip
   const int G = sweeps <= 10 ? 1 : 2, cap = 8 / G;
   const int nw = std::min(wg_waves > 0 ? wg_waves : (G == 1 ? 4 : 2), cap);
-  return static_cast<int64_t>(nw) * (192 - 2 * ((sweeps + 2) / 3 * 3));
+  return static_cast<int64_t>(nw) * (256 - 2 * ((sweeps + 3) / 4 * 4));
 }
 
 // in-order CPU streams: the signal was raised before this call runs

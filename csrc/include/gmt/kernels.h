@@ -110,7 +110,7 @@ int gmt_jacobi5_rects(int n_rect, const int64_t* rects, const double* u, double*
 #define GMT_TB_MAX_SWEEPS 24
 typedef struct gmt_tb_opts {
   int sweeps;   /* K, see gmt_jacobi5tb_supported */
-  int wg_waves; /* 192-column strips per workgroup, 1..8 (0 = default; at
+  int wg_waves; /* 256-column strips per workgroup, 1..8 (0 = default; at
                    most 4 when K > 10) */
   int seg_rows; /* output rows per strip segment (0 = default: short edge
                    segments where a rect touches a Dirichlet row, interior

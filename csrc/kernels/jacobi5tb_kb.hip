@@ -1,0 +1,11 @@
+// Instantiations of the temporal-blocking kernel (jacobi5tb.hpp) for K = 8, 9.
+#include "jacobi5tb.hpp"
+
+namespace gmt {
+namespace tb {
+template int dispatch_k<8>(const gmt_tb_opts&, bool, int, const int64_t*, const int64_t*, int, const double*,
+                               double*, int64_t, int64_t, hipStream_t, int64_t*);
+template int dispatch_k<9>(const gmt_tb_opts&, bool, int, const int64_t*, const int64_t*, int, const double*,
+                               double*, int64_t, int64_t, hipStream_t, int64_t*);
+}  // namespace tb
+}  // namespace gmt

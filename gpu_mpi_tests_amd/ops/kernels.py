@@ -287,7 +287,7 @@ def jacobi5tb(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[i
     coordinates, each with its k-wide ring inside the array); the rest of ``un``
     is never written.  ``dom`` is the interior; bits of ``halo_mask`` (1 W, 2 E,
     4 S, 8 N) mark ghost sides owned by a neighbour (the others are fixed
-    Dirichlet rings).  ``k``: see :func:`tb_supported`.  ``wg_waves``: 192-column
+    Dirichlet rings).  ``k``: see :func:`tb_supported`.  ``wg_waves``: 256-column
     strips per workgroup (0 = default), ``seg_rows``: output rows per strip (0 =
     default), ``exact``: 1/4 multiply per level instead of power-of-two scaled
     levels."""

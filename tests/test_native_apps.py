@@ -283,14 +283,14 @@ def test_mpi_stencil2d_sycl_oo_strong_scaling_and_debug():
     (["100", "26", "--tblock", "--tsteps=12", "--dims=1x2"], 2),
     # band-first overlapped passes (ranks wide enough for boundary bands and
     # an interior): the pass's output halo is exchanged under its interior
-    (["--ny=200", "--nx=1200", "0", "13", "--tblock", "--tsteps=4", "--wg-strips=1", "--dims=2x2", "--periodic",
+    (["--ny=200", "--nx=1600", "0", "13", "--tblock", "--tsteps=4", "--wg-strips=1", "--dims=2x2", "--periodic",
       "--transport=ipc"], 4),
-    (["--ny=240", "--nx=1100", "0", "27", "--tblock", "--tsteps=12", "--wg-strips=1", "--dims=2x2"], 4),
-    (["--ny=150", "--nx=1800", "0", "15", "--tblock", "--tsteps=6", "--wg-strips=1", "--dims=1x3",
+    (["--ny=240", "--nx=1500", "0", "27", "--tblock", "--tsteps=12", "--wg-strips=1", "--dims=2x2"], 4),
+    (["--ny=150", "--nx=2400", "0", "15", "--tblock", "--tsteps=6", "--wg-strips=1", "--dims=1x3",
       "--transport=rccl"], 3),
     (["--ny=400", "--nx=300", "0", "17", "--tblock", "--tsteps=8", "--wg-strips=1", "--dims=2x1",
       "--transport=mpi-host"], 2),
-    (["--ny=130", "--nx=700", "0", "11", "--tblock", "--tsteps=5", "--wg-strips=1", "--periodic"], 1),
+    (["--ny=130", "--nx=800", "0", "11", "--tblock", "--tsteps=5", "--wg-strips=1", "--periodic"], 1),
 ])
 def test_mpi_jacobi2d_matches_serial(args, np_):
     out = run_app("mpi_jacobi2d", *args, "--check", "--warmup=2", "--halo-iters=3", np=np_).stdout

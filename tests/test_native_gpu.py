@@ -53,7 +53,7 @@ def test_engine_periodic_matches_serial(env, ny, nx, steps, tblock, graph):
     assert float(np.abs(got - ref).max()) < 1e-13
 
 
-@pytest.mark.parametrize("ny,nx,steps,tblock,wg", [(260, 1100, 13, 4, 1), (300, 1100, 45, 12, 0),
+@pytest.mark.parametrize("ny,nx,steps,tblock,wg", [(260, 1100, 13, 4, 1), (300, 1500, 45, 12, 0),
                                                   (400, 1300, 47, 20, 0), (333, 1501, 61, 24, 0)])
 @pytest.mark.parametrize("graph", [False, True])
 def test_engine_band_first_matches_serial(env, ny, nx, steps, tblock, wg, graph):
@@ -140,7 +140,7 @@ def test_app_jacobi_ipc_graph_matches_serial(np_):
 def test_app_jacobi_band_first(np_, transport, extra):
     """Band-first overlapped passes across processes sharing the GPU (the
     exchange kernels run beside the pass's interior workgroups); bitwise."""
-    nx = 1200 * (3 if "--dims=1x3" in extra else 1)
+    nx = 3000 * (3 if "--dims=1x3" in extra else 1)  # 3 x 432-column W/E bands per rank at K = 20
     out = _app(["mpi_jacobi2d", f"--ny=400", f"--nx={nx}", "0", "45", "--check", "--tblock", "--tsteps=20",
                 "--warmup=20", f"--transport={transport}", *extra], np_=np_)
     assert "overlap=1 (band-first)" in out, out
