@@ -210,7 +210,7 @@ int64_t gmt_jacobi5tb_group_cols(int sweeps, int wg_waves) {
   if (!gmt_jacobi5tb_supported(sweeps)) return 0;
   // the GPU kernel's strip geometry: 256 - 2 * ceil4(K) columns per strip
   const int G = sweeps <= 10 ? 1 : 2, cap = 8 / G;
-  const int nw = std::min(wg_waves > 0 ? wg_waves : (G == 1 ? 4 : 2), cap);
+  const int nw = std::min(wg_waves > 0 ? wg_waves : (G == 1 ? 4 : 1), cap);
   return static_cast<int64_t>(nw) * (256 - 2 * ((sweeps + 3) / 4 * 4));
 }
 

@@ -513,7 +513,7 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   constexpr int G = n_stages(K);
   constexpr int kMaxStrips = kMaxThreads / kWave / G;
   Args a{};
-  a.nw = std::min(o.wg_waves > 0 ? o.wg_waves : (G == 1 ? 4 : 2), kMaxStrips);
+  a.nw = std::min(o.wg_waves > 0 ? o.wg_waves : (G == 1 ? 4 : 1), kMaxStrips);  // two-stage: one strip (profiles/r02_tb4/launch_shapes.txt)
   a.ld = ld;
   a.last_row = nrows - 1;
   a.mask = mask;
