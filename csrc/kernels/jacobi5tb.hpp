@@ -22,7 +22,7 @@ constexpr int kCols = kNC * kWave;            // 256 columns per strip
 constexpr uint32_t kRowBytes = kCols * 8;     // one row of a strip: 2 KB
 constexpr uint32_t kSlotBytes = kRowBytes;    // DMA ring slot: two full-wave 16-B DMAs
 constexpr uint32_t kDrop = 0x80000000u;       // buffer offset past num_records: no-op access
-constexpr int kP = 4;                         // input rows in flight
+constexpr int kP = 6;                         // input rows in flight
 constexpr int kRS = kP + 2;                   // DMA ring: rows s-2..s in use, s+1..s+P-1 in flight
 constexpr int kHS = 6;                        // hand-off ring (2 stages): rows of steps s-4..s
 constexpr int kMaxK1 = 10;                    // largest single-wave K

@@ -1,0 +1,19 @@
+#!/bin/bash
+# A/B builds of the temporal-blocking kernel: copy csrc/kernels, apply a sed
+# expression to jacobi5tb.hpp, rebuild its translation units and link a
+# libgmt.so into build/var/NAME/ (run a binary against it with
+# LD_LIBRARY_PATH=build/var/NAME: the apps' RUNPATH yields to it).
+#   scripts/build_variant.sh p4 's/constexpr int kP = 6;/constexpr int kP = 4;/'
+set -e
+cd "$(dirname "$0")/.."
+name=$1; expr=$2
+D=build/var/$name
+rm -rf $D && mkdir -p $D/src $D/obj
+cp csrc/kernels/*.hpp csrc/kernels/jacobi5tb*.hip $D/src/
+sed -i "$expr" $D/src/jacobi5tb.hpp
+cmp -s csrc/kernels/jacobi5tb.hpp $D/src/jacobi5tb.hpp && { echo "sed changed nothing"; exit 1; }
+ls $D/src/jacobi5tb*.hip | xargs -P 8 -I{} sh -c '/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Icsrc/include -munsafe-fp-atomics -c {} -o '$D'/obj/$(basename {} .hip).o'
+others=$(ls build/obj/kernels/*.o | grep -v jacobi5tb)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/libgmt.so $D/obj/*.o $others build/obj/runtime/rt_hip.o \
+  -Wl,-soname,libgmt.so -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lamdhip64 -lrocprofiler-sdk-roctx -ldl
+echo "built $D/libgmt.so"
