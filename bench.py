@@ -76,8 +76,10 @@ def _timed(env, fn_run, fn_sync, steps, warmup):
     fn_run(steps)
     fn_sync()
     _sync(env)
-    gdist.barrier(env)
+    # this rank's finish, read before the closing barrier (whose own cost is
+    # not part of the K steps); the job's time is the max over ranks
     dt = time.perf_counter() - t0
+    gdist.barrier(env)
     return gdist.allreduce_max(dt, env)
 
 
