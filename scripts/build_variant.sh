@@ -4,13 +4,17 @@
 # libgmt.so into build/var/NAME/ (run a binary against it with
 # LD_LIBRARY_PATH=build/var/NAME: the apps' RUNPATH yields to it).
 #   scripts/build_variant.sh p4 's/constexpr int kP = 6;/constexpr int kP = 4;/'
+#   scripts/build_variant.sh head git:HEAD     (jacobi5tb.hpp as committed at HEAD)
 set -e
 cd "$(dirname "$0")/.."
 name=$1; expr=$2
 D=build/var/$name
 rm -rf $D && mkdir -p $D/src $D/obj
 cp csrc/kernels/*.hpp csrc/kernels/jacobi5tb*.hip $D/src/
-sed -i "$expr" $D/src/jacobi5tb.hpp
+case "$expr" in
+  git:*) git show "${expr#git:}:csrc/kernels/jacobi5tb.hpp" > $D/src/jacobi5tb.hpp ;;
+  *) sed -i "$expr" $D/src/jacobi5tb.hpp ;;
+esac
 cmp -s csrc/kernels/jacobi5tb.hpp $D/src/jacobi5tb.hpp && { echo "sed changed nothing"; exit 1; }
 ls $D/src/jacobi5tb*.hip | xargs -P 8 -I{} sh -c '/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Icsrc/include -munsafe-fp-atomics -c {} -o '$D'/obj/$(basename {} .hip).o'
 others=$(ls build/obj/kernels/*.o | grep -v jacobi5tb)
