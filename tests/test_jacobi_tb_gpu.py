@@ -1,7 +1,7 @@
 """Temporal-blocking Jacobi kernel (csrc/kernels/jacobi5tb.hip)
 vs the plain fp64 PyTorch reference of k single sweeps (ops/reference.py
 jacobi5xk): bitwise, every ghost-side pattern, partial strips / segments,
-right edges inside a lane (widths 0/1/2 mod 3), one- and two-stage strips
+right edges inside a lane (widths 0-3 mod 4), one- and two-stage strips
 (k <= 10 / k >= 12: levels split over two waves with an LDS hand-off),
 1..8 strips per workgroup, exact and scaled arithmetic, frame-rect launches
 as the engine issues them, and nothing written outside the rects."""
