@@ -46,6 +46,13 @@ __global__ __launch_bounds__(kBlock) void copy2d_batched_kernel(Copy2dBatch b) {
   if (w == 1) {
     row = i;
     col = 0;
+  } else if (total <= 0xffffffffll) {
+    // every halo face fits 32 bits: a 32-bit division (a few VALU
+    // instructions) instead of the 64-bit software sequence
+    const uint32_t ii = static_cast<uint32_t>(i), ww = static_cast<uint32_t>(w);
+    const uint32_t r = ii / ww;
+    row = r;
+    col = ii - r * ww;
   } else {
     row = i / w;
     col = i - row * w;
