@@ -253,6 +253,7 @@ extern "C" const char* gmt_error_string(int err) {
 extern "C" int gmt_device_synchronize(void) { return static_cast<int>(hipDeviceSynchronize()); }
 
 extern "C" const char* gmt_build_info(void) {
-  return "libgmt gfx950 (CDNA4) kernels: daxpy, stencil5 1d/2d, jacobi5 (reg/lds/scalar), "
+  return "libgmt gfx950 (CDNA4) kernels: daxpy, stencil5 1d/2d (dim 1: LDS-DMA pipeline), jacobi5, "
+         "jacobi5tb (1-24 fused sweeps, 4 columns per lane), ipc_exchange, signal_wait, "
          "copy2d_batched, sum_axis, diff_sq, fill_poly; built " __DATE__ " " __TIME__;
 }
