@@ -65,6 +65,7 @@ struct Args {
   int64_t sig_wgs;
   unsigned* sig_count;
   uint64_t* signal;
+  int prio;                      // single-round launch: stage-0 waves at raised priority
 };
 
 struct d4 {
@@ -381,6 +382,10 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   } else {
     constexpr int KA = stage0_levels(K);
     if (stage == 0) {
+      // a launch of one round has no later workgroups to fill the SIMDs
+      // while a strip's stage 1 waits on its stage 0: favour the producer
+      // (profiles/r02_tb.md 9.4)
+      if (a.prio) __builtin_amdgcn_s_setprio(2);
       if (rule)
         run_stage<K, 1, KA, EXACT, EDGE, true, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
       else
@@ -576,6 +581,7 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   for (int k = a.n + 1; k <= kMaxRect; ++k) a.tstart[k] = a.tstart[a.n];
   const int64_t nb = a.tstart[a.n];
   a.sig_wgs = a.tstart[sig_rects];
+  a.prio = nb <= per_cu ? 1 : 0;
   a.sig_count = o.signal_count;
   a.signal = o.signal;
   if (info) {
