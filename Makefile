@@ -45,9 +45,10 @@ RT_OBJ      := $(OBJ)/runtime/rt_hip.o
 CCL_OBJ     := $(OBJ)/runtime/ccl_rccl.o
 HOST_OBJS   := $(OBJ)/host/kernels_host.o $(OBJ)/host/rt_host.o
 HOSTCCL_OBJ := $(OBJ)/host/ccl_host.o
-COMM_OBJS   := $(OBJ)/comm/transport_mpi.o $(OBJ)/comm/transport_core.o $(OBJ)/engine/jacobi.o
-ENG_OBJS    := $(OBJ)/comm/transport_core.o $(OBJ)/engine/jacobi.o $(OBJ)/engine/engine_capi.o \
-               $(OBJ)/engine/deriv_bench.o
+COMM_OBJS   := $(OBJ)/comm/transport_mpi.o $(OBJ)/comm/transport_core.o $(OBJ)/comm/transport_ipc.o \
+               $(OBJ)/comm/control_socket.o $(OBJ)/engine/jacobi.o
+ENG_OBJS    := $(OBJ)/comm/transport_core.o $(OBJ)/comm/transport_ipc.o $(OBJ)/comm/control_socket.o \
+               $(OBJ)/engine/jacobi.o $(OBJ)/engine/engine_capi.o $(OBJ)/engine/deriv_bench.o
 APP_HDRS    := $(wildcard csrc/include/gmt/*.hpp csrc/include/gmt/*.h csrc/apps/*.hpp)
 
 # reference binary names (Makefile:2, CMakeLists.txt:22-82) + MI355X additions

@@ -149,7 +149,8 @@ def check_engine(env, dims, tsteps, graph):
 
 def peer_status(env, dims):
     """Which process-grid neighbours' GPUs this rank's GPU can reach directly
-    (xGMI peer access), gathered on rank 0: {"peer_access": bool, "rccl": version}."""
+    (xGMI peer access), gathered on rank 0: {"peer_access": bool, "rccl": version,
+    "ranks_per_gpu": n}.  Neighbours on the same GPU (oversubscription) need none."""
     if not env.is_gpu or env.world_size == 1:
         return {}
     py, px = dims
@@ -158,13 +159,15 @@ def peer_status(env, dims):
             if 0 <= cy + dy < py and 0 <= cx + dx < px]
     ok = True
     for r in nbrs:
-        dev = r % max(1, env.n_devices)  # one rank per GPU: rank r runs on device r (single node)
+        # single node, block mapping (parallel/dist.py select_device): rank r on r // ranks_per_device
+        dev = (r // max(1, env.ranks_per_device)) % max(1, env.n_devices)
         if dev != env.device.index:
             ok = ok and bool(torch.cuda.can_device_access_peer(env.device.index, dev))
     flags = [None] * env.world_size
     torch.distributed.all_gather_object(flags, ok, group=env.host_group)
     ver = torch.cuda.nccl.version() if hasattr(torch.cuda, "nccl") else None
-    return {"peer_access": all(flags), "rccl_version": ".".join(map(str, ver)) if isinstance(ver, tuple) else ver}
+    return {"peer_access": all(flags), "rccl_version": ".".join(map(str, ver)) if isinstance(ver, tuple) else ver,
+            "ranks_per_gpu": env.ranks_per_device}
 
 
 def halo_latency(env, eng, iters):
@@ -199,12 +202,13 @@ def ref_halo(env, n_local, n_other, iters):
     test_sum: 2-deep ghost faces of n_other doubles — 8 MiB at the defaults —
     exchanged between 1-D slab neighbours, dim 0 packed, dim 1 in place, the
     derivative kernel after each exchange; then the 1024-double all-reduce),
-    over RCCL on this job's GPUs.  Per-exchange median, max over ranks."""
+    over this job's transport (RCCL; IPC when ranks share a GPU).  Per-exchange
+    median, max over ranks."""
     from gpu_mpi_tests_amd.engine import deriv_bench
 
     r = deriv_bench(n_local, n_other, n_iter=iters, n_warmup=5, env=env)
     out = {"ref_halo_config": f"mpi_stencil2d_gt {n_local}x{n_other} per rank, 1-D slabs, "
-                              f"{iters} exchanges, rccl"}
+                              f"{iters} exchanges, {r['transport']}"}
     for d in (0, 1):
         out[f"ref_halo_dim{d}_us"] = round(gdist.allreduce_max(r[f"dim{d}"]["median_s"], env) * 1e6, 2)
         out[f"ref_halo_dim{d}_err_norm"] = gdist.allreduce_max(r[f"dim{d}"]["err_norm"], env)
@@ -214,7 +218,8 @@ def ref_halo(env, n_local, n_other, iters):
 
 
 def bench_daxpy(env, n, iters):
-    """Per-GPU DAXPY rate (each rank on its own GPU), reported as whole-job GB/s."""
+    """Per-GPU DAXPY rate (each rank on its own GPU, random-init x and y),
+    reported as whole-job GB/s."""
     dev = env.device
     x = torch.rand(n, dtype=torch.float64, device=dev)
     y = torch.rand(n, dtype=torch.float64, device=dev)
@@ -238,6 +243,54 @@ def bench_daxpy(env, n, iters):
     dt = gdist.allreduce_max(dt, env)
     del x, y
     return 24.0 * n / dt / 1e9 * env.world_size, dt
+
+
+def daxpy_allreduce(env, n, iters):
+    """BASELINE config "mpi_daxpy N ranks x 1 GPU, RCCL allreduce of partial
+    sums": the reference's distributed DAXPY check (mpi_daxpy_nvtx.cc:207-310)
+    with its closed form — x = (i+1)/n, y = -x, y <- 2x + y = x, so each rank's
+    SUM = (n+1)/2 and ALLSUM = world*(n+1)/2 — where the reference's host
+    sums and Allgather become a device partial sum (gfx950 reduce kernel) and
+    an in-place all-reduce of it over the native transport (RCCL over xGMI;
+    IPC when ranks share a GPU; a labelled 1-rank self all-reduce at N = 1).
+    Returns the keys for the JSON line; rel_err > 1e-9 fails the run."""
+    from gpu_mpi_tests_amd.engine import Comm
+
+    dev = env.device
+    x = torch.empty(n, dtype=torch.float64, device=dev)
+    ops.fill_poly(x, 3, 1.0 / n, 1.0 / n, 0.0, 0.0)  # x[i] = (i+1)/n
+    y = -x
+    ops.daxpy(2.0, x, y)
+    comm = Comm(env)
+    part = torch.empty(1, dtype=torch.float64, device=dev)
+    t_sum, t_red = [], []
+    try:
+        for i in range(iters + 3):
+            _sync(env)
+            t0 = time.perf_counter()
+            ops.sum_axis(y.view(1, n), 1, out=part)  # this rank's SUM, on the device
+            _sync(env)
+            t1 = time.perf_counter()
+            allsum = part.clone()
+            _sync(env)
+            t2 = time.perf_counter()
+            comm.allreduce_sum_(allsum)
+            t3 = time.perf_counter()
+            if i >= 3:
+                t_sum.append(t1 - t0)
+                t_red.append(t3 - t2)
+        local, total = float(part.item()), float(allsum.item())
+    finally:
+        comm.close()
+    exact_local = (n + 1) / 2.0
+    exact = env.world_size * exact_local
+    rel = max(abs(total - exact) / exact, gdist.allreduce_max(abs(local - exact_local) / exact_local, env))
+    kind = comm.name if env.world_size > 1 else f"1-rank self all-reduce ({comm.name})"
+    del x, y
+    return {"daxpy_allsum": total, "daxpy_allsum_exact": exact, "daxpy_allsum_rel_err": rel,
+            "daxpy_partial_sum_us": round(gdist.allreduce_max(float(np.median(t_sum)), env) * 1e6, 2),
+            "daxpy_allreduce_us": round(gdist.allreduce_max(float(np.median(t_red)), env) * 1e6, 2),
+            "daxpy_allreduce_kind": kind}
 
 
 def main(argv=None):
@@ -341,6 +394,14 @@ def main(argv=None):
         extras["daxpy_GBps_per_gpu"] = round(gbps / env.world_size, 1)
         extras["daxpy_n"] = args.daxpy_n
         extras["daxpy_ms"] = round(ddt * 1e3, 4)
+        extras.update(daxpy_allreduce(env, args.daxpy_n, iters=20))
+        if not extras["daxpy_allsum_rel_err"] <= 1e-9:
+            if env.rank == 0:
+                print(f"bench.py: DAXPY ALLSUM {extras['daxpy_allsum']} differs from the closed form "
+                      f"{extras['daxpy_allsum_exact']} (rel err {extras['daxpy_allsum_rel_err']:.3e})",
+                      file=sys.stderr)
+            gdist.shutdown()
+            sys.exit(4)
     else:
         solver.close()
     py, px = info["dims"] if info.get("dims") else gdims

@@ -12,6 +12,7 @@
 
 #include "gmt/buffer.hpp"
 #include "gmt/comm.hpp"
+#include "gmt/control.hpp"
 #include "gmt/mpi.hpp"
 
 namespace gmt {
@@ -57,31 +58,43 @@ void waitall(std::vector<MPI_Request>& reqs, const char* what) {
   reqs.clear();
 }
 
-// Host-staged collectives shared by the mpi-host and ipc transports.
-void staged_allreduce(MPI_Comm c, double* buf, size_t n, gmt_stream_t s) {
-  Buffer<double> h(n, GMT_SPACE_PINNED);
-  GMT_CHECK("allreduce D2H", gmt_rt_memcpy_async(h.data(), buf, n * sizeof(double), s));
+// Host-staged collectives of the mpi-host transport, through one persistent
+// pinned buffer (grown on demand; allocating pinned memory per call costs a
+// hipHostMalloc/hipHostFree pair, far more than an 8 KiB all-reduce).
+class Staging {
+ public:
+  char* get(size_t bytes) {
+    if (buf_.bytes() < bytes) buf_ = Buffer<char>(bytes, GMT_SPACE_PINNED);
+    return buf_.data();
+  }
+
+ private:
+  Buffer<char> buf_;
+};
+
+void staged_allreduce(Staging& st, MPI_Comm c, double* buf, size_t n, gmt_stream_t s) {
+  double* h = reinterpret_cast<double*>(st.get(n * sizeof(double)));
+  GMT_CHECK("allreduce D2H", gmt_rt_memcpy_async(h, buf, n * sizeof(double), s));
   GMT_CHECK("allreduce sync", gmt_rt_stream_synchronize(s));
-  GMT_MPI_CHECK(MPI_Allreduce(MPI_IN_PLACE, h.data(), static_cast<int>(n), MPI_DOUBLE, MPI_SUM, c));
-  GMT_CHECK("allreduce H2D", gmt_rt_memcpy_async(buf, h.data(), n * sizeof(double), s));
-  GMT_CHECK("allreduce sync", gmt_rt_stream_synchronize(s));
+  GMT_MPI_CHECK(MPI_Allreduce(MPI_IN_PLACE, h, static_cast<int>(n), MPI_DOUBLE, MPI_SUM, c));
+  GMT_CHECK("allreduce H2D", gmt_rt_memcpy_async(buf, h, n * sizeof(double), s));
+  GMT_CHECK("allreduce sync", gmt_rt_stream_synchronize(s));  // the staging is reused next call
 }
-void staged_allgather(MPI_Comm c, int rank, int size, const void* send, void* recv, size_t bpr,
+void staged_allgather(Staging& st, MPI_Comm c, int rank, int size, const void* send, void* recv, size_t bpr,
                       gmt_stream_t s) {
-  Buffer<char> h(bpr * size, GMT_SPACE_PINNED);
-  GMT_CHECK("allgather D2H", gmt_rt_memcpy_async(h.data() + rank * bpr, send, bpr, s));
+  char* h = st.get(bpr * size);
+  GMT_CHECK("allgather D2H", gmt_rt_memcpy_async(h + rank * bpr, send, bpr, s));
   GMT_CHECK("allgather sync", gmt_rt_stream_synchronize(s));
   MPI_Datatype t;
   int n;
   mpi_count(bpr, &t, &n);
-  GMT_MPI_CHECK(MPI_Allgather(MPI_IN_PLACE, 0, t, h.data(), n, t, c));
-  GMT_CHECK("allgather H2D", gmt_rt_memcpy_async(recv, h.data(), bpr * size, s));
+  GMT_MPI_CHECK(MPI_Allgather(MPI_IN_PLACE, 0, t, h, n, t, c));
+  GMT_CHECK("allgather H2D", gmt_rt_memcpy_async(recv, h, bpr * size, s));
   GMT_CHECK("allgather sync", gmt_rt_stream_synchronize(s));
 }
 
 class MpiTransport : public Transport {
- protected:
-  explicit MpiTransport(MPI_Comm c) : Transport(rank_of(c), size_of(c)), comm_(c) {}
+ public:
   static int rank_of(MPI_Comm c) {
     int r = 0;
     MPI_Comm_rank(c, &r);
@@ -92,6 +105,9 @@ class MpiTransport : public Transport {
     MPI_Comm_size(c, &n);
     return n;
   }
+
+ protected:
+  explicit MpiTransport(MPI_Comm c) : Transport(rank_of(c), size_of(c)), comm_(c) {}
   MPI_Comm comm_;
 };
 
@@ -109,16 +125,18 @@ class MpiTransport : public Transport {
 // receives never wait for this one's H2D copies to drain.
 class MpiHostExchange : public Exchange {
  public:
-  // pipeline chunk: 1 MiB (GMT_HOST_CHUNK_KB overrides, for measurement)
+  // pipeline chunk: 1 MiB (GMT_HOST_CHUNK_KB overrides, for measurement);
+  // the transport agrees on one value across ranks (receives are posted per
+  // chunk, so the two sides of a message must cut it the same way)
   static size_t chunk_bytes() {
     const char* e = std::getenv("GMT_HOST_CHUNK_KB");
     const long kb = e ? std::atol(e) : 0;
     return kb > 0 ? static_cast<size_t>(kb) << 10 : size_t(1) << 20;
   }
 
-  MpiHostExchange(MPI_Comm c, std::vector<Msg> r, std::vector<Msg> s)
+  MpiHostExchange(MPI_Comm c, size_t chunk, std::vector<Msg> r, std::vector<Msg> s)
       : c_(c), recvs_(std::move(r)), sends_(std::move(s)) {
-    const size_t kChunk = chunk_bytes();
+    const size_t kChunk = chunk;
     for (int set = 0; set < 2; ++set)
       for (auto& m : recvs_) rstage_[set].emplace_back(m.bytes, GMT_SPACE_PINNED);
     for (auto& m : sends_) sstage_.emplace_back(m.bytes, GMT_SPACE_PINNED);
@@ -227,18 +245,31 @@ class MpiHostExchange : public Exchange {
 
 class MpiHostTransport : public MpiTransport {
  public:
-  explicit MpiHostTransport(MPI_Comm c) : MpiTransport(c) {}
+  explicit MpiHostTransport(MPI_Comm c) : MpiTransport(c) {
+    const unsigned long long mine = MpiHostExchange::chunk_bytes();
+    unsigned long long lo = mine, hi = mine;
+    GMT_MPI_CHECK(MPI_Allreduce(MPI_IN_PLACE, &lo, 1, MPI_UNSIGNED_LONG_LONG, MPI_MIN, c));
+    GMT_MPI_CHECK(MPI_Allreduce(MPI_IN_PLACE, &hi, 1, MPI_UNSIGNED_LONG_LONG, MPI_MAX, c));
+    if (lo != hi && rank_ == 0)
+      std::printf("# mpi-host: GMT_HOST_CHUNK_KB differs between ranks (%llu..%llu KiB); using %llu KiB\n",
+                  lo >> 10, hi >> 10, hi >> 10);
+    chunk_ = static_cast<size_t>(hi);
+  }
   Kind kind() const override { return Kind::MpiHost; }
   const char* name() const override { return "mpi-host"; }
   std::unique_ptr<Exchange> plan(const std::vector<Msg>& r, const std::vector<Msg>& s) override {
-    return std::make_unique<MpiHostExchange>(comm_, r, s);
+    return std::make_unique<MpiHostExchange>(comm_, chunk_, r, s);
   }
   void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override {
-    staged_allreduce(comm_, buf, n, s);
+    staged_allreduce(staging_, comm_, buf, n, s);
   }
   void allgather(const void* send, void* recv, size_t bpr, gmt_stream_t s) override {
-    staged_allgather(comm_, rank_, size_, send, recv, bpr, s);
+    staged_allgather(staging_, comm_, rank_, size_, send, recv, bpr, s);
   }
+
+ private:
+  Staging staging_;
+  size_t chunk_ = size_t(1) << 20;
 };
 
 // ---------------------------------------------------------------- mpi-direct
@@ -311,227 +342,43 @@ class MpiDirectTransport : public MpiTransport {
   }
 };
 
-// ----------------------------------------------------------------------- ipc
-// handle-exchange tags: one offset per wire kind, so a pair of ranks that
-// exchange messages with the same tag in both directions cannot mismatch them
-constexpr int kStageTag = 10000, kFlagTag = 20000, kReadyTag = 30000;
-
-struct IpcWire {
-  gmt_ipc_handle h;
-  uint64_t offset;
-};
-
-// hipIpcOpenMemHandle maps an allocation once per process: cache by handle.
-class IpcCache {
+// ------------------------------------------------------- MPI control plane
+// gmt/control.hpp over MPI: the ipc transport's handle exchange and
+// host-staged collectives in the native apps.
+class MpiControl : public Control {
  public:
-  void* open(const gmt_ipc_handle& h) {
-    std::string k(reinterpret_cast<const char*>(h.bytes), sizeof(h.bytes));
-    auto it = map_.find(k);
-    if (it != map_.end()) {
-      ++it->second.refs;
-      return it->second.base;
-    }
-    void* base = nullptr;
-    GMT_CHECK("ipc open", gmt_rt_ipc_open(&base, &h));
-    map_[k] = {base, 1};
-    return base;
-  }
-  void close(void* base) {
-    for (auto it = map_.begin(); it != map_.end(); ++it)
-      if (it->second.base == base && --it->second.refs == 0) {
-        GMT_WARN("ipc close", gmt_rt_ipc_close(base));
-        map_.erase(it);
-        return;
-      }
-  }
-
- private:
-  struct E {
-    void* base;
-    int refs;
-  };
-  std::map<std::string, E> map_;
-};
-
-// Stream-ordered exchange over IPC-mapped memory (csrc/kernels/ipc.hip has
-// the protocol).  Every send message gets two staging slots in the sender's
-// memory; the receiver pulls the current slot once the sender's "ready" flag
-// (in the receiver's flag memory) reaches the exchange's epoch, then marks the
-// slot consumed (in the sender's flag memory).  start() and wait() are one
-// kernel launch each on the caller's stream: no host synchronisation, no MPI
-// traffic after construction, so the exchange can be captured into a graph.
-// Several ranks may share a GPU (the IPC mappings are then same-device).
-class IpcExchange : public Exchange {
- public:
-  IpcExchange(MPI_Comm c, int rank, IpcCache* cache, std::vector<Msg> r, std::vector<Msg> s)
-      : c_(c), rank_(rank), cache_(cache), recvs_(std::move(r)), sends_(std::move(s)) {
-    const size_t nr = recvs_.size(), ns = sends_.size();
-    // flags: ready[j] per receive (written by its sender), consumed[i] per send
-    // (written by its receiver); control: epoch, 2 launch counters, error word
-    flags_ = Buffer<uint64_t>(nr + ns + 1, GMT_SPACE_FLAGS);
-    ctl_ = Buffer<uint64_t>(4, GMT_SPACE_DEVICE);  // epoch | 3 x u32 counters + u32 error
-    GMT_CHECK("ipc ctl", gmt_rt_memset_async(ctl_.data(), 0, ctl_.bytes(), nullptr));
-    GMT_CHECK("ipc ctl", gmt_rt_stream_synchronize(nullptr));
-    for (auto& m : sends_) stage_.emplace_back(2 * (m.bytes ? m.bytes : 1), GMT_SPACE_DEVICE);
-
-    // wiring: the receiver of send i learns {its staging, its consumed flag};
-    // the sender of receive j learns {its ready flag}
-    auto wire = [](void* p) {
-      IpcWire w;
-      size_t off = 0;
-      GMT_CHECK("ipc get handle", gmt_rt_ipc_get_handle(&w.h, &off, p));
-      w.offset = off;
-      return w;
-    };
-    std::vector<IpcWire> out_stage(ns), out_cflag(ns), out_rflag(nr), in_stage(nr), in_cflag(nr), in_rflag(ns);
+  explicit MpiControl(MPI_Comm c) : Control(MpiTransport::rank_of(c), MpiTransport::size_of(c)), c_(c) {}
+  const char* name() const override { return "mpi"; }
+  void exchange(const std::vector<HostMsg>& recvs, const std::vector<HostMsg>& sends) override {
     std::vector<MPI_Request> reqs;
-    for (size_t j = 0; j < nr; ++j) {
-      if (recvs_[j].peer == rank_) continue;
+    reqs.reserve(recvs.size() + sends.size());
+    for (auto& m : recvs) {
       reqs.emplace_back();
-      GMT_MPI_CHECK(MPI_Irecv(&in_stage[j], sizeof(IpcWire), MPI_BYTE, recvs_[j].peer, recvs_[j].tag + kStageTag,
-                              c_, &reqs.back()));
-      reqs.emplace_back();
-      GMT_MPI_CHECK(MPI_Irecv(&in_cflag[j], sizeof(IpcWire), MPI_BYTE, recvs_[j].peer, recvs_[j].tag + kFlagTag,
-                              c_, &reqs.back()));
-      out_rflag[j] = wire(flags_.data() + j);
-      reqs.emplace_back();
-      GMT_MPI_CHECK(MPI_Isend(&out_rflag[j], sizeof(IpcWire), MPI_BYTE, recvs_[j].peer, recvs_[j].tag + kReadyTag,
-                              c_, &reqs.back()));
+      irecv(m.buf, m.bytes, m.peer, m.tag, c_, &reqs.back());
     }
-    for (size_t i = 0; i < ns; ++i) {
-      if (sends_[i].peer == rank_) continue;
+    for (auto& m : sends) {
       reqs.emplace_back();
-      GMT_MPI_CHECK(MPI_Irecv(&in_rflag[i], sizeof(IpcWire), MPI_BYTE, sends_[i].peer, sends_[i].tag + kReadyTag,
-                              c_, &reqs.back()));
-      out_stage[i] = wire(stage_[i].data());
-      out_cflag[i] = wire(flags_.data() + nr + i);
-      reqs.emplace_back();
-      GMT_MPI_CHECK(MPI_Isend(&out_stage[i], sizeof(IpcWire), MPI_BYTE, sends_[i].peer, sends_[i].tag + kStageTag,
-                              c_, &reqs.back()));
-      reqs.emplace_back();
-      GMT_MPI_CHECK(MPI_Isend(&out_cflag[i], sizeof(IpcWire), MPI_BYTE, sends_[i].peer, sends_[i].tag + kFlagTag,
-                              c_, &reqs.back()));
+      isend(m.buf, m.bytes, m.peer, m.tag, c_, &reqs.back());
     }
-    waitall(reqs, "ipc handle exchange");
-    auto open = [&](const IpcWire& w) {
-      void* base = cache_->open(w.h);
-      opened_.push_back(base);
-      return static_cast<char*>(base) + w.offset;
-    };
-    // self messages (periodic single rank): the matching local buffers
-    auto self_send = [&](int tag) -> int {
-      for (size_t i = 0; i < ns; ++i)
-        if (sends_[i].peer == rank_ && sends_[i].tag == tag) return static_cast<int>(i);
-      std::printf("ipc: no self-send for tag %d\n", tag);
-      abort_job(2);
-    };
-    auto self_recv = [&](int tag) -> int {
-      for (size_t j = 0; j < nr; ++j)
-        if (recvs_[j].peer == rank_ && recvs_[j].tag == tag) return static_cast<int>(j);
-      std::printf("ipc: no self-receive for tag %d\n", tag);
-      abort_job(2);
-    };
-    for (size_t i = 0; i < ns; ++i) {
-      const Msg& m = sends_[i];
-      gmt_ipc_chan ch{};
-      ch.src = m.buf;
-      ch.dst = stage_[i].data();
-      ch.bytes = static_cast<int64_t>(m.bytes);
-      ch.dst_stride = static_cast<int64_t>(m.bytes ? m.bytes : 1);
-      ch.wait = flags_.data() + nr + i;  // the receiver has consumed slot e & 1 (exchange e - 2)
-      ch.signal = m.peer == rank_ ? flags_.data() + self_recv(m.tag)
-                                  : reinterpret_cast<uint64_t*>(open(in_rflag[i]));
-      send_.push_back(ch);
-    }
-    for (size_t j = 0; j < nr; ++j) {
-      const Msg& m = recvs_[j];
-      gmt_ipc_chan ch{};
-      if (m.peer == rank_) {
-        const int i = self_send(m.tag);
-        ch.src = stage_[i].data();
-        ch.signal = flags_.data() + nr + i;
-      } else {
-        ch.src = open(in_stage[j]);
-        ch.signal = reinterpret_cast<uint64_t*>(open(in_cflag[j]));
-      }
-      ch.src_stride = static_cast<int64_t>(m.bytes ? m.bytes : 1);
-      ch.dst = m.buf;
-      ch.bytes = static_cast<int64_t>(m.bytes);
-      ch.wait = flags_.data() + j;  // the sender's slot for this exchange is ready
-      recv_.push_back(ch);
-    }
-    if (send_.size() > GMT_IPC_MAX_CHAN || recv_.size() > GMT_IPC_MAX_CHAN) {
-      std::printf("ipc: %zu sends / %zu receives exceed %d channels per launch\n", send_.size(), recv_.size(),
-                  GMT_IPC_MAX_CHAN);
-      abort_job(2);
-    }
+    waitall(reqs, "control exchange");
   }
-  ~IpcExchange() override {
-    for (void* b : opened_) cache_->close(b);
+  void allreduce_sum(double* buf, size_t n) override {
+    GMT_MPI_CHECK(MPI_Allreduce(MPI_IN_PLACE, buf, static_cast<int>(n), MPI_DOUBLE, MPI_SUM, c_));
   }
-  // one launch per exchange (send and receive channels in the same grid)
-  void start(gmt_stream_t s) override {
-    if (send_.empty() && recv_.empty()) return;
-    GMT_CHECK("ipc exchange", gmt_ipc_exchange(static_cast<int>(send_.size()), send_.data(),
-                                               static_cast<int>(recv_.size()), recv_.data(), epoch(), counters(),
-                                               err(), s));
+  void allreduce_max(double* buf, size_t n) override {
+    GMT_MPI_CHECK(MPI_Allreduce(MPI_IN_PLACE, buf, static_cast<int>(n), MPI_DOUBLE, MPI_MAX, c_));
   }
-  void wait(gmt_stream_t) override {}  // stream order: the launch in start() completes first
-  bool graph_capturable() const override { return true; }
+  void allgather(const void* send, void* recv, size_t bpr) override {
+    MPI_Datatype t;
+    int n;
+    mpi_count(bpr, &t, &n);
+    const bool inplace = send == static_cast<const char*>(recv) + rank_ * bpr;
+    GMT_MPI_CHECK(MPI_Allgather(inplace ? MPI_IN_PLACE : send, inplace ? 0 : n, t, recv, n, t, c_));
+  }
+  void barrier() override { GMT_MPI_CHECK(MPI_Barrier(c_)); }
 
  private:
-  uint64_t* epoch() { return ctl_.data(); }
-  unsigned* counters() { return reinterpret_cast<unsigned*>(ctl_.data() + 1); }  // 3 words
-  unsigned* err() { return reinterpret_cast<unsigned*>(ctl_.data() + 3); }
-
   MPI_Comm c_;
-  int rank_;
-  IpcCache* cache_;
-  std::vector<Msg> recvs_, sends_;
-  Buffer<uint64_t> flags_, ctl_;
-  std::vector<Buffer<char>> stage_;
-  std::vector<gmt_ipc_chan> send_, recv_;
-  std::vector<void*> opened_;
-};
-
-class IpcTransport : public MpiTransport {
- public:
-  explicit IpcTransport(MPI_Comm c) : MpiTransport(c) {}
-  ~IpcTransport() override { gathers_.clear(); }
-  Kind kind() const override { return Kind::Ipc; }
-  const char* name() const override { return "ipc"; }
-  std::unique_ptr<Exchange> plan(const std::vector<Msg>& r, const std::vector<Msg>& s) override {
-    return std::make_unique<IpcExchange>(comm_, rank_, &cache_, r, s);
-  }
-  void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override {
-    staged_allreduce(comm_, buf, n, s);
-  }
-  // All-gather as one persistent IPC exchange: every rank writes its block
-  // straight into every peer's receive buffer.  Plans are cached per
-  // (send, recv, size) so the handle exchange happens once per buffer set.
-  void allgather(const void* send, void* recv, size_t bpr, gmt_stream_t s) override {
-    char* r = static_cast<char*>(recv);
-    if (send != r + rank_ * bpr)
-      GMT_CHECK("gather self", gmt_rt_memcpy_async(r + rank_ * bpr, send, bpr, s));
-    if (size_ == 1) return;
-    const auto key = std::make_tuple(send, recv, bpr);
-    auto it = gathers_.find(key);
-    if (it == gathers_.end()) {
-      std::vector<Msg> recvs, sends;
-      for (int p = 0; p < size_; ++p) {
-        if (p == rank_) continue;
-        recvs.push_back({r + p * bpr, bpr, p, kGatherTag});
-        sends.push_back({const_cast<void*>(send), bpr, p, kGatherTag});
-      }
-      it = gathers_.emplace(key, plan(recvs, sends)).first;
-    }
-    it->second->run(s);
-  }
-
- private:
-  static constexpr int kGatherTag = 777;
-  IpcCache cache_;
-  std::map<std::tuple<const void*, void*, size_t>, std::unique_ptr<Exchange>> gathers_;
 };
 
 }  // namespace
@@ -611,7 +458,7 @@ std::unique_ptr<Transport> make_transport(Kind k, MPI_Comm comm, const RankBindi
       GMT_MPI_CHECK(MPI_Bcast(&id, sizeof(id), MPI_BYTE, 0, comm));
       return make_rccl_transport(rank, size, id);
     }
-    case Kind::Ipc: return std::make_unique<IpcTransport>(comm);
+    case Kind::Ipc: return make_ipc_transport(std::make_unique<MpiControl>(comm));
     case Kind::Local: return make_local_transport();
     default: break;
   }

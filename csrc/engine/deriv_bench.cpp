@@ -1,7 +1,7 @@
 // The reference's main benchmark (mpi_stencil2d_gt test_deriv / test_sum,
 // SURVEY.md §3.1) behind the MPI-free engine ABI (gmt/engine.h), so
 // bench.py can time the reference-shaped halo exchange over RCCL/xGMI on
-// every rank of a torch.distributed job: 8 MiB ghost faces per neighbour
+// every rank of a torch.distributed job (IPC when ranks share a GPU): 8 MiB ghost faces per neighbour
 // (2 x 524288 doubles), dim 0 packed by the gfx950 copy kernel, dim 1
 // zero-copy, the derivative kernel after every exchange, err_norm against
 // the analytic derivative, then the 1024-double in-place all-reduce.
@@ -11,18 +11,15 @@
 #include "gmt/deriv.hpp"
 #include "gmt/engine.h"
 
+namespace gmt {
+std::unique_ptr<comm::Transport> engine_transport(int rank, int world, int transport, const void* id);
+}
+
 extern "C" int gmt_engine_deriv_bench(int64_t n_local, int64_t n_other, int n_iter, int n_warmup,
                                       int rank, int world, int transport, const void* ccl_id,
                                       double* out) {
-  std::unique_ptr<gmt::comm::Transport> t;
-  if (transport == GMT_ENGINE_RCCL) {
-    gmt_ccl_id id;
-    std::memcpy(&id, ccl_id, sizeof(id));
-    t = gmt::comm::make_rccl_transport(rank, world, id);
-  } else {
-    if (world != 1) return 1;
-    t = gmt::comm::make_local_transport();
-  }
+  std::unique_ptr<gmt::comm::Transport> t = gmt::engine_transport(rank, world, transport, ccl_id);
+  if (!t) return 1;
   for (int dim = 0; dim < 2; ++dim) {
     gmt::apps::DerivConfig c;
     c.dim = dim;

@@ -1,8 +1,12 @@
 // C ABI of the native Jacobi engine (gmt/engine.h) for the Python package.
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <string>
 #include <memory>
 #include <vector>
 
+#include "gmt/control.hpp"
 #include "gmt/engine.h"
 #include "gmt/jacobi.hpp"
 #include "gmt/kernels.h"
@@ -13,7 +17,27 @@ struct Handle {
   std::unique_ptr<gmt::JacobiSolver> s;
   int py = 1, px = 1;
 };
+
 }  // namespace
+
+namespace gmt {
+// Transport of an engine handle (also used by deriv_bench.cpp); nullptr when
+// the request is invalid.
+std::unique_ptr<comm::Transport> engine_transport(int rank, int world, int transport, const void* id) {
+  if (world < 1 || rank < 0 || rank >= world) return nullptr;
+  if (transport == GMT_ENGINE_RCCL) {
+    gmt_ccl_id cid;
+    std::memcpy(&cid, id, sizeof(cid));
+    return comm::make_rccl_transport(rank, world, cid);
+  }
+  if (transport == GMT_ENGINE_IPC) {
+    if (!id) return nullptr;
+    return comm::make_ipc_transport(comm::make_socket_control(rank, world, static_cast<const char*>(id)));
+  }
+  if (world != 1) return nullptr;
+  return comm::make_local_transport();
+}
+}  // namespace gmt
 
 extern "C" {
 
@@ -25,6 +49,30 @@ int gmt_engine_unique_id(void* out128) {
   return e;
 }
 
+int gmt_engine_control_id(void* out128) {
+  gmt::comm::make_socket_control_id(static_cast<char*>(out128));
+  return 0;
+}
+
+void* gmt_engine_comm_create(int rank, int world, int transport, const void* id) {
+  return gmt::engine_transport(rank, world, transport, id).release();
+}
+int gmt_engine_comm_allreduce_sum(void* h, double* buf, int64_t n, void* stream) {
+  auto* t = static_cast<gmt::comm::Transport*>(h);
+  if (!t || n < 0) return 1;
+  const auto s = static_cast<gmt_stream_t>(stream);
+  t->allreduce_sum(buf, static_cast<size_t>(n), s);
+  GMT_CHECK("allreduce sync", gmt_rt_stream_synchronize(s));
+  std::string why;
+  if (!t->ok(&why)) {
+    std::printf("gmt_engine_comm_allreduce_sum: %s\n", why.c_str());
+    gmt::abort_job(EXIT_FAILURE);
+  }
+  return 0;
+}
+const char* gmt_engine_comm_name(void* h) { return static_cast<gmt::comm::Transport*>(h)->name(); }
+void gmt_engine_comm_destroy(void* h) { delete static_cast<gmt::comm::Transport*>(h); }
+
 void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank, int world,
                                int transport, const void* ccl_id, const gmt_engine_opts* opts) {
   gmt_engine_opts o{};
@@ -33,16 +81,10 @@ void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank,
       o.wg_waves > 8 || o.seg_rows < 0 || o.exact < -1 || o.exact > 1)
     return nullptr;
   auto* h = new Handle();
-  if (transport == GMT_ENGINE_RCCL) {
-    gmt_ccl_id id;
-    std::memcpy(&id, ccl_id, sizeof(id));
-    h->t = gmt::comm::make_rccl_transport(rank, world, id);
-  } else {
-    if (world != 1) {
-      delete h;
-      return nullptr;
-    }
-    h->t = gmt::comm::make_local_transport();
+  h->t = gmt::engine_transport(rank, world, transport, ccl_id);
+  if (!h->t) {
+    delete h;
+    return nullptr;
   }
   gmt::JacobiConfig c;
   c.ny_global = ny;

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 namespace gmt {
@@ -457,6 +458,14 @@ void JacobiSolver::synchronize() {
   if (err != 0) {
     std::printf("JacobiSolver: a band-first pass timed out waiting for its boundary bands (error %llu)\n",
                 static_cast<unsigned long long>(err));
+    abort_job(EXIT_FAILURE);
+  }
+  // a halo exchange that timed out (IPC) left stale ghost cells: fail loudly
+  for (auto& h : halo_)
+    if (h) h->check();
+  std::string why;
+  if (!t_.ok(&why)) {
+    std::printf("JacobiSolver: %s\n", why.c_str());
     abort_job(EXIT_FAILURE);
   }
   watchdog_kick("jacobi synchronize");

@@ -9,6 +9,8 @@
 // purpose: several MPI ranks share the CPU in the tests, and a rank-local
 // thread pool would only oversubscribe it.
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <sched.h>
 
@@ -237,34 +239,63 @@ int gmt_jacobi5tb_plan(const gmt_tb_opts* o, int n_rect, const int64_t* rects, c
 
 // CPU backend of csrc/kernels/ipc.hip: the same protocol on memfd-shared
 // memory between processes (flags through __atomic builtins): sends first,
-// their "ready" signals, then the receives.
-int gmt_ipc_exchange(int n_send, const gmt_ipc_chan* sends, int n_recv, const gmt_ipc_chan* recvs, uint64_t* epoch,
-                     unsigned* counters, unsigned* err, void*) {
-  if (n_send < 0 || n_recv < 0 || n_send > GMT_IPC_MAX_CHAN || n_recv > GMT_IPC_MAX_CHAN || n_send + n_recv < 1 ||
-      !epoch || !counters || !err)
+// their "ready" signals, then the receives.  Waits are bounded by
+// GMT_WAIT_TIMEOUT_MS (default 10 s) of wall clock, like the GPU kernel's.
+int64_t gmt_ipc_table_bytes(int n_chan) {
+  if (n_chan < 0) return 0;
+  return static_cast<int64_t>(n_chan) * static_cast<int64_t>(sizeof(gmt_ipc_chan)) +
+         (static_cast<int64_t>(n_chan) + 1) * static_cast<int64_t>(sizeof(int64_t));
+}
+
+int gmt_ipc_plan_init(gmt_ipc_plan* p, int n_send, const gmt_ipc_chan* sends, int n_recv, const gmt_ipc_chan* recvs) {
+  if (!p || !p->table || n_send < 0 || n_recv < 0 || n_send + n_recv < 1) return 1;
+  auto* c = static_cast<gmt_ipc_chan*>(p->table);
+  for (int k = 0; k < n_send + n_recv; ++k) {
+    c[k] = k < n_send ? sends[k] : recvs[k - n_send];
+    if (c[k].bytes < 0) return 1;
+  }
+  p->n_send = n_send;
+  p->n_recv = n_recv;
+  p->send_chunks = n_send;
+  p->recv_chunks = n_recv;
+  return 0;
+}
+
+int gmt_ipc_exchange(const gmt_ipc_plan* p, void*) {
+  if (!p || !p->table || !p->epoch || !p->counters || !p->err || p->n_send < 0 || p->n_recv < 0 ||
+      p->n_send + p->n_recv < 1)
     return 1;
-  const uint64_t e = __atomic_load_n(epoch, __ATOMIC_ACQUIRE) + 1;
-  auto run = [&](int n, const gmt_ipc_chan* cs, uint64_t lag) {
-    for (int k = 0; k < n; ++k) {
-      const gmt_ipc_chan& c = cs[k];
-      if (c.wait && e > lag) {
+  static const double limit_s = [] {
+    const char* e = std::getenv("GMT_WAIT_TIMEOUT_MS");
+    const long ms = e && std::atol(e) > 0 ? std::atol(e) : 10000;
+    return ms * 1e-3;
+  }();
+  const auto* chan = static_cast<const gmt_ipc_chan*>(p->table);
+  const uint64_t e = __atomic_load_n(p->epoch, __ATOMIC_ACQUIRE) + 1;
+  auto run = [&](int k0, int n, uint64_t lag) {
+    for (int k = k0; k < k0 + n; ++k) {
+      const gmt_ipc_chan& c = chan[k];
+      if (c.wait && e > lag && __atomic_load_n(p->err, __ATOMIC_RELAXED) == 0) {
+        const auto t0 = std::chrono::steady_clock::now();
         for (long it = 0; __atomic_load_n(c.wait, __ATOMIC_ACQUIRE) < e - lag; ++it) {
-          if (it > 20000000) {  // tens of seconds of polling: give up like the GPU kernel
-            __atomic_fetch_or(err, 1u, __ATOMIC_RELAXED);
-            break;
+          if (it > 1000) {
+            sched_yield();
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s) {
+              __atomic_store_n(p->err, static_cast<unsigned>(k + 1), __ATOMIC_RELAXED);
+              break;
+            }
           }
-          if (it > 1000) sched_yield();
         }
       }
       std::memcpy(static_cast<char*>(c.dst) + (e & 1) * c.dst_stride,
                   static_cast<const char*>(c.src) + (e & 1) * c.src_stride, static_cast<size_t>(c.bytes));
     }
-    for (int k = 0; k < n; ++k)
-      if (cs[k].signal) __atomic_store_n(cs[k].signal, e, __ATOMIC_RELEASE);
+    for (int k = k0; k < k0 + n; ++k)
+      if (chan[k].signal) __atomic_store_n(chan[k].signal, e, __ATOMIC_RELEASE);
   };
-  run(n_send, sends, 2);
-  run(n_recv, recvs, 0);
-  __atomic_store_n(epoch, e, __ATOMIC_RELEASE);
+  run(0, p->n_send, 2);
+  run(p->n_send, p->n_recv, 0);
+  __atomic_store_n(p->epoch, e, __ATOMIC_RELEASE);
   return 0;
 }
 

@@ -3,8 +3,14 @@
  *
  * The Python package drives the flagship benchmark through this ABI
  * (gpu_mpi_tests_amd/engine.py): torch.distributed does the rendezvous and
- * broadcasts the RCCL unique id, then every step runs in C++ (hipGraph
- * replay of halo exchange + sweeps) with no Python on the critical path.
+ * broadcasts a 128-byte id, then every step runs in C++ (hipGraph replay of
+ * halo exchange + sweeps) with no Python on the critical path.  Transports:
+ *   RCCL  one rank per GPU, xGMI; the id is an RCCL unique id;
+ *   IPC   several ranks per GPU allowed (GPU oversubscription, the
+ *         reference's mpi_daxpy.cc:43-54 mode) or one per GPU; HIP IPC
+ *         mappings traded once over a Unix-socket mesh of the node named by
+ *         the id (gmt_engine_control_id), one kernel launch per exchange;
+ *   LOCAL one rank, no id.
  * No MPI in this library.
  */
 #ifndef GMT_ENGINE_H
@@ -16,22 +22,25 @@
 extern "C" {
 #endif
 
-enum gmt_engine_transport { GMT_ENGINE_LOCAL = 0, GMT_ENGINE_RCCL = 1 };
+enum gmt_engine_transport { GMT_ENGINE_LOCAL = 0, GMT_ENGINE_RCCL = 1, GMT_ENGINE_IPC = 2 };
 
 /* fills 128 bytes (an RCCL unique id); returns 0 or an error code */
 int gmt_engine_unique_id(void* out128);
+/* fills 128 bytes: the name of a socket control plane (GMT_ENGINE_IPC) */
+int gmt_engine_control_id(void* out128);
 /* Engine options (explicit fields; 0 = default everywhere). */
 typedef struct gmt_engine_opts {
   int periodic; /* 1: periodic process grid, else Dirichlet (fixed ghost ring) */
   int overlap;  /* 0 off, 1 halo exchange overlapped with the core pass, 2 auto (time both once) */
   int graph;    /* 1: capture the per-parity passes into hipGraphs */
-  int tsteps;   /* sweeps per fused pass and per halo exchange: 1 (or 0) = single sweeps, 2..16 */
+  int tsteps;   /* sweeps per fused pass and per halo exchange: 0 or 1 = single sweeps, else
+                   2..GMT_TB_MAX_SWEEPS (odd values above 10 are rounded down to even) */
   int wg_waves; /* temporal-blocking kernel: waves per workgroup (0 = auto) */
   int seg_rows; /* temporal-blocking kernel: output rows per workgroup (0 = auto) */
   int exact;    /* -1 / 0: power-of-two scaled levels when the field bound allows (auto),
                    1: always the exact 1/4-per-level form */
 } gmt_engine_opts;
-/* ccl_id: 128 bytes (RCCL) or NULL (local); NULL on invalid options */
+/* id: 128 bytes (RCCL unique id / control id) or NULL (local); NULL on invalid options */
 void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank, int world,
                                int transport, const void* ccl_id, const gmt_engine_opts* opts);
 void gmt_engine_jacobi_destroy(void* h);
@@ -51,9 +60,18 @@ int gmt_engine_jacobi_prepare(void* h, int steps);
 int gmt_engine_jacobi_copy_interior(void* h, double* host);
 const char* gmt_engine_backend(void);
 
+/* A bare communicator on the same transports, for device collectives outside
+ * the engine (bench.py's DAXPY partial-sum all-reduce, BASELINE config 3).
+ * allreduce: in-place sum of n doubles in device memory, ordered on `stream`,
+ * complete on return. */
+void* gmt_engine_comm_create(int rank, int world, int transport, const void* id);
+int gmt_engine_comm_allreduce_sum(void* h, double* buf, int64_t n, void* stream);
+const char* gmt_engine_comm_name(void* h);
+void gmt_engine_comm_destroy(void* h);
+
 /* The reference's halo-exchange benchmark (mpi_stencil2d_gt test_deriv for
  * dim 0 and dim 1, then test_sum), n_local x n_other per rank, 2 ghosts,
- * non-periodic 1-D slabs, on the RCCL transport (or local for world == 1).
+ * non-periodic 1-D slabs, on the RCCL or IPC transport (local for world == 1).
  * out[14]: per dim d (6 values at 6*d): exchange seconds median, mean, min,
  * max, bytes sent per exchange, this rank's err_norm; out[12] = all-reduce
  * (1024 doubles in place) median seconds, out[13] = its max relative error. */

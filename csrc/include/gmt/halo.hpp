@@ -18,7 +18,9 @@
 // to the lower neighbour uses 456, to the upper 123; y faces add 1000.
 #pragma once
 
+#include <cstdio>
 #include <memory>
+#include <string>
 #include <vector>
 
 #include "gmt/buffer.hpp"
@@ -186,6 +188,19 @@ class Halo2D {
     start(s);
     finish(s);
     GMT_CHECK("halo sync", gmt_rt_stream_synchronize(s));
+    check();
+  }
+  // After a synchronisation: true unless an exchange failed without the host
+  // noticing (an IPC wait that timed out, gmt/transport.hpp Exchange::ok).
+  bool ok(std::string* why = nullptr) const {
+    return (!ex_ || ex_->ok(why)) && (!ex_x_ || ex_x_->ok(why));
+  }
+  // ok() or abort the job with the reason: stale ghost cells never pass
+  void check() const {
+    std::string why;
+    if (ok(&why)) return;
+    std::printf("halo exchange failed: %s\n", why.c_str());
+    abort_job(EXIT_FAILURE);
   }
 
  private:

@@ -142,22 +142,24 @@ int gmt_jacobi5tb_plan(const gmt_tb_opts* opts, int n_rect, const int64_t* rects
 
 /* One-workgroup kernel on `stream`: waits until *signal > *seen (a
  * gmt_tb_opts completion signal), then advances *seen by one — a stream
- * ordered wait that replays correctly in a hipGraph.  Gives up after about a
- * second and sets *err.  All three in GMT_SPACE_FLAGS memory. */
+ * ordered wait that replays correctly in a hipGraph.  Gives up after
+ * GMT_WAIT_TIMEOUT_MS of device wall clock (default 10 s) and sets bit 2 of
+ * *err.  All three in GMT_SPACE_FLAGS memory. */
 int gmt_signal_wait(const uint64_t* signal, uint64_t* seen, unsigned* err, void* stream);
 
-/* ---- Stream-ordered IPC exchange (csrc/kernels/ipc.hip), one launch:
- *      e = *epoch + 1.  Send channel: wait until *wait >= e - 2 (receiver done
- *      with the slot), copy src -> dst + (e & 1) * dst_stride.  Receive
- *      channel: wait until *wait >= e (sender's slot ready), copy
- *      src + (e & 1) * src_stride -> dst.  When all send (receive) channels
- *      are copied, e is stored into each of their non-NULL *signal flags
- *      (system-scope release); when everything is done, *epoch = e.
- *      counters: 3 device words, zero between launches; a wait that times
- *      out (~0.5 s) sets *err and gives up.  Flags: GMT_SPACE_FLAGS memory;
- *      wait flags local, signal flags may be IPC-mapped memory of another
- *      process or device. */
-#define GMT_IPC_MAX_CHAN 16
+/* ---- Stream-ordered IPC exchange (csrc/kernels/ipc.hip), one launch per
+ *      exchange of a persistent plan: e = *epoch + 1.  Send channel: wait
+ *      until *wait >= e - 2 (receiver done with the slot), copy src -> dst +
+ *      (e & 1) * dst_stride.  Receive channel: wait until *wait >= e
+ *      (sender's slot ready), copy src + (e & 1) * src_stride -> dst.  When
+ *      all send (receive) channels are copied, e is stored into each of their
+ *      non-NULL *signal flags (system-scope release); when everything is
+ *      done, *epoch = e.  Flags: GMT_SPACE_FLAGS memory; wait flags local,
+ *      signal flags may be IPC-mapped memory of another process or device.
+ *      Each wait is bounded by GMT_WAIT_TIMEOUT_MS of device wall clock
+ *      (default 10 s); one that expires stores 1 + its channel index (sends
+ *      first, then receives) into *err and gives up — the host must read
+ *      *err after synchronising and treat non-zero as a failed exchange. */
 typedef struct gmt_ipc_chan {
   const void* src;
   void* dst;
@@ -167,8 +169,20 @@ typedef struct gmt_ipc_chan {
   const uint64_t* wait;
   uint64_t* signal;
 } gmt_ipc_chan;
-int gmt_ipc_exchange(int n_send, const gmt_ipc_chan* sends, int n_recv, const gmt_ipc_chan* recvs,
-                     uint64_t* epoch, unsigned* counters, unsigned* err, void* stream);
+typedef struct gmt_ipc_plan {
+  void* table;         /* device memory of gmt_ipc_table_bytes(n_send + n_recv) bytes */
+  uint64_t* epoch;     /* device word, zero before the first exchange */
+  unsigned* counters;  /* 3 device words, zero before the first exchange */
+  unsigned* err;       /* host-visible (pinned) word, zero = no timeout */
+  int n_send, n_recv;          /* filled by gmt_ipc_plan_init */
+  int64_t send_chunks, recv_chunks;
+} gmt_ipc_plan;
+int64_t gmt_ipc_table_bytes(int n_chan);
+/* Writes the channel table (synchronous copy) and the chunk counts; any
+ * number of channels.  table/epoch/counters/err must be set by the caller. */
+int gmt_ipc_plan_init(gmt_ipc_plan* plan, int n_send, const gmt_ipc_chan* sends, int n_recv,
+                      const gmt_ipc_chan* recvs);
+int gmt_ipc_exchange(const gmt_ipc_plan* plan, void* stream);
 
 /* One kernel per entry point: the variants the defaults were chosen against
  * are measured by csrc/bench/variant_bench.hip, not shipped in this ABI. */

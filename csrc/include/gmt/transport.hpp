@@ -14,11 +14,13 @@
 //   rccl       ncclSend/ncclRecv grouped per exchange on the caller's stream,
 //              ncclAllReduce / ncclAllGather for collectives: xGMI links,
 //              stream-ordered, one rank per GPU
-//   ipc        HIP IPC: each rank opens its neighbours' receive buffers once
-//              and writes its halo straight into them (xGMI peer write, or a
-//              same-device copy when ranks share one GPU); MPI carries only
-//              zero-byte ready/done tokens.  The one device-direct path that
-//              works with several ranks per GPU.
+//   ipc        HIP IPC: each rank maps its peers' staging slots and flags
+//              once (handles traded over the host control plane,
+//              gmt/control.hpp: MPI in the apps, a socket mesh in the engine)
+//              and every exchange is one stream-ordered kernel that pulls the
+//              peers' slots (xGMI peer read, or a same-device copy when ranks
+//              share one GPU).  The one device-direct path that works with
+//              several ranks per GPU.
 //   local      single process: messages to self become device copies
 //              (periodic boundaries on one GPU; the Python engine's CPU tests)
 //
@@ -37,6 +39,8 @@
 namespace gmt {
 namespace comm {
 
+class Control;
+
 struct Msg {
   void* buf;     // device (or managed/host) memory
   size_t bytes;
@@ -54,6 +58,14 @@ class Exchange {
   // Fully stream-ordered (no host blocking in start/wait): may be captured
   // into a hipGraph.
   virtual bool graph_capturable() const { return false; }
+  // After the stream has been synchronised: false (and a reason) when an
+  // earlier exchange failed without the host noticing — an IPC wait that
+  // timed out and left stale data.  Transports that block on the host
+  // report failures at once and are always ok().
+  virtual bool ok(std::string* why = nullptr) const {
+    (void)why;
+    return true;
+  }
   void run(gmt_stream_t s) {
     start(s);
     wait(s);
@@ -74,6 +86,13 @@ class Transport {
   // recv = concat over ranks of `bytes_per_rank` from each rank's send;
   // in place when send == recv + rank*bytes_per_rank
   virtual void allgather(const void* send, void* recv, size_t bytes_per_rank, gmt_stream_t s) = 0;
+  // Exchange::ok for the transport's own cached plans (collectives)
+  virtual bool ok(std::string* why = nullptr) const {
+    (void)why;
+    return true;
+  }
+  // the host control plane under the transport, when it has one
+  virtual Control* control() { return nullptr; }
   int rank() const { return rank_; }
   int size() const { return size_; }
 
@@ -91,6 +110,10 @@ std::unique_ptr<Transport> make_rccl_transport(int rank, int size, const gmt_ccl
 // Single-process transport: every message must be addressed to rank 0
 // (periodic self-exchange); a device-to-device copy per message.
 std::unique_ptr<Transport> make_local_transport();
+// HIP IPC over a host control plane (csrc/comm/transport_ipc.cpp): owning,
+// or borrowing one that outlives the transport.  Same node only.
+std::unique_ptr<Transport> make_ipc_transport(std::unique_ptr<Control> ctl);
+std::unique_ptr<Transport> make_ipc_transport(Control& ctl);
 
 }  // namespace comm
 }  // namespace gmt

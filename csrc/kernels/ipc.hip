@@ -1,8 +1,8 @@
 // Stream-ordered IPC exchange (gmt_ipc_exchange, gmt/kernels.h), gfx950.
 //
-// The halo transport "ipc" (csrc/comm/transport_mpi.cpp) runs every
+// The halo transport "ipc" (csrc/comm/transport_ipc.cpp) runs every
 // exchange as ONE launch on the caller's stream — no host synchronisation,
-// no MPI token rounds, so the exchange can be captured into a hipGraph.
+// no control-plane rounds, so the exchange can be captured into a hipGraph.
 // Send channels and receive channels are workgroups of the same grid (at
 // most 128 per role, looping over 16 KB chunks, so spinning workgroups never
 // occupy the GPU that the peer processes' kernels need):
@@ -21,12 +21,20 @@
 // gmt_signal_wait (below) is the same kind of stream-ordered wait for a
 // completion signal raised inside another stream's kernel (gmt_tb_opts).
 //
-// The epoch lives in device memory (read at the start, advanced by the last
-// workgroup of the recv step), so replayed graphs stay in step.
+// The channel table lives in device memory (gmt_ipc_plan_init), so a plan
+// has any number of channels (an all-gather over 63 peers is 126) and the
+// launch arguments stay a few words — the same bytes in a replayed graph.
+// The epoch lives in device memory too (read at the start, advanced by the
+// last workgroup), so replayed graphs stay in step.
 //
 // Flags are GMT_SPACE_FLAGS memory (uncached); loads and stores of them are
-// vector atomics at system scope.  Every wait gives up after ~2^22 sleeps
-// (about a second) and sets *err, so a lost peer cannot hang the GPU.
+// vector atomics at system scope.  Every wait is bounded by the device wall
+// clock (GMT_WAIT_TIMEOUT_MS, default 10 s): a wait that expires stores
+// 1 + its channel index into the plan's error word (host-visible pinned
+// memory, read by the host after each synchronisation) and gives up, so a
+// lost peer can neither hang the GPU nor pass unnoticed.
+#include <cstdlib>
+
 #include "common.hpp"
 #include "gmt/kernels.h"
 
@@ -35,16 +43,16 @@ namespace ipc {
 
 constexpr int64_t kBlockBytes = 16 * 1024;  // bytes per chunk: 4 x 16 B per lane
 constexpr int64_t kMaxRoleBlocks = 128;     // workgroups per role: spinning groups never fill the GPU
-constexpr unsigned kSpinLimit = 1u << 22;
 
 struct Args {
-  gmt_ipc_chan c[2 * GMT_IPC_MAX_CHAN];     // sends, then receives
-  int64_t cstart[2 * GMT_IPC_MAX_CHAN + 1];  // prefix sum of chunks per channel (sends, then receives)
+  const gmt_ipc_chan* chan;  // sends, then receives (device memory)
+  const int64_t* cstart;     // prefix sum of chunks per channel, n_send + n_recv + 1 entries
   int ns, nr;
   int64_t sb, rb;  // workgroups of the send role, then of the receive role
   uint64_t* epoch;
   unsigned* counter;  // [0] send role, [1] receive role, [2] all
   unsigned* err;
+  uint64_t timeout_ticks;  // device wall-clock ticks per wait
 };
 
 __device__ __forceinline__ uint64_t load_sys(const uint64_t* p) {
@@ -56,6 +64,23 @@ __device__ __forceinline__ bool last_arrival(unsigned* c, unsigned total) {
   if (__hip_atomic_fetch_add(c, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) != total - 1) return false;
   __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
+}
+
+// Poll *flag until it reaches `want` or the wall clock runs out; on timeout
+// record `code` in *err (a plain system-scope store: any non-zero is an error).
+// Once an exchange of the plan has failed, later ones do not wait again (the
+// host aborts at its next synchronisation; queued exchanges drain quickly).
+__device__ __forceinline__ void bounded_wait(const uint64_t* flag, uint64_t want, uint64_t ticks, unsigned* err,
+                                             unsigned code) {
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
+  const uint64_t t0 = wall_clock64();
+  while (load_sys(flag) < want) {
+    __builtin_amdgcn_s_sleep(4);
+    if (wall_clock64() - t0 > ticks) {
+      __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void ipc_exchange_kernel(Args a) {
@@ -71,17 +96,9 @@ __global__ __launch_bounds__(kBlock) void ipc_exchange_kernel(Args a) {
   int k = k0;
   for (int64_t c = c0 + rb; c < c1; c += nrb) {
     while (k + 1 < k1 && c >= a.cstart[k + 1]) ++k;
-    const gmt_ipc_chan& ch = a.c[k];
-    if (threadIdx.x == 0 && ch.wait != nullptr && e > lag) {
-      unsigned it = 0;
-      while (load_sys(ch.wait) < e - lag) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++it == kSpinLimit) {
-          __hip_atomic_fetch_or(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-      }
-    }
+    const gmt_ipc_chan ch = a.chan[k];
+    if (threadIdx.x == 0 && ch.wait != nullptr && e > lag)
+      bounded_wait(ch.wait, e - lag, a.timeout_ticks, a.err, static_cast<unsigned>(k + 1));
     __syncthreads();
     const char* src = static_cast<const char*>(ch.src) + (e & 1) * ch.src_stride;
     char* dst = static_cast<char*>(ch.dst) + (e & 1) * ch.dst_stride;
@@ -109,8 +126,10 @@ __global__ __launch_bounds__(kBlock) void ipc_exchange_kernel(Args a) {
     // each role signals on its own: a rank's "ready" must not wait for its
     // own receives (those wait for the peers' "ready")
     if (last_arrival(a.counter + (send ? 0 : 1), static_cast<unsigned>(nrb))) {
-      for (int j = k0; j < k1; ++j)
-        if (a.c[j].signal) __hip_atomic_store(a.c[j].signal, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      for (int j = k0; j < k1; ++j) {
+        uint64_t* sig = a.chan[j].signal;
+        if (sig) __hip_atomic_store(sig, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
     if (last_arrival(a.counter + 2, static_cast<unsigned>(a.sb + a.rb)))
       __hip_atomic_store(a.epoch, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -118,18 +137,37 @@ __global__ __launch_bounds__(kBlock) void ipc_exchange_kernel(Args a) {
 }
 
 // gmt_signal_wait: thread 0 polls the signal (uncached memory) with sleeps
-__global__ __launch_bounds__(kWave) void signal_wait_kernel(const uint64_t* signal, uint64_t* seen, unsigned* err) {
+__global__ __launch_bounds__(kWave) void signal_wait_kernel(const uint64_t* signal, uint64_t* seen, unsigned* err,
+                                                           uint64_t ticks) {
   if (threadIdx.x != 0) return;
   const uint64_t want = __hip_atomic_load(seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  unsigned it = 0;
+  const uint64_t t0 = wall_clock64();
   while (__hip_atomic_load(const_cast<uint64_t*>(signal), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < want) {
-    __builtin_amdgcn_s_sleep(2);
-    if (++it == kSpinLimit) {
+    __builtin_amdgcn_s_sleep(4);
+    if (wall_clock64() - t0 > ticks) {
       __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
   }
   __hip_atomic_store(seen, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// per-wait bound in device wall-clock ticks (GMT_WAIT_TIMEOUT_MS, default 10 s)
+uint64_t timeout_ticks() {
+  static int dev_cached = -1;
+  static uint64_t ticks = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (dev != dev_cached) {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+      khz = 100000;  // 100 MHz, the CDNA constant clock
+    const char* e = std::getenv("GMT_WAIT_TIMEOUT_MS");
+    const long ms = e && std::atol(e) > 0 ? std::atol(e) : 10000;
+    ticks = static_cast<uint64_t>(ms) * static_cast<uint64_t>(khz);
+    dev_cached = dev;
+  }
+  return ticks;
 }
 
 }  // namespace ipc
@@ -138,33 +176,63 @@ __global__ __launch_bounds__(kWave) void signal_wait_kernel(const uint64_t* sign
 extern "C" int gmt_signal_wait(const uint64_t* signal, uint64_t* seen, unsigned* err, void* stream) {
   using namespace gmt;
   if (!signal || !seen || !err) return static_cast<int>(hipErrorInvalidValue);
-  ipc::signal_wait_kernel<<<1, kWave, 0, static_cast<hipStream_t>(stream)>>>(signal, seen, err);
+  ipc::signal_wait_kernel<<<1, kWave, 0, static_cast<hipStream_t>(stream)>>>(signal, seen, err,
+                                                                           ipc::timeout_ticks());
   GMT_RET_LAUNCH();
 }
 
-extern "C" int gmt_ipc_exchange(int n_send, const gmt_ipc_chan* sends, int n_recv, const gmt_ipc_chan* recvs,
-                                uint64_t* epoch, unsigned* counters, unsigned* err, void* stream) {
+extern "C" int64_t gmt_ipc_table_bytes(int n_chan) {
+  if (n_chan < 0) return 0;
+  return static_cast<int64_t>(n_chan) * static_cast<int64_t>(sizeof(gmt_ipc_chan)) +
+         (static_cast<int64_t>(n_chan) + 1) * static_cast<int64_t>(sizeof(int64_t));
+}
+
+extern "C" int gmt_ipc_plan_init(gmt_ipc_plan* p, int n_send, const gmt_ipc_chan* sends, int n_recv,
+                                 const gmt_ipc_chan* recvs) {
   using namespace gmt;
-  if (n_send < 0 || n_recv < 0 || n_send > GMT_IPC_MAX_CHAN || n_recv > GMT_IPC_MAX_CHAN || n_send + n_recv < 1 ||
-      !epoch || !counters || !err)
-    return static_cast<int>(hipErrorInvalidValue);
-  ipc::Args a{};
-  a.ns = n_send;
-  a.nr = n_recv;
-  a.epoch = epoch;
-  a.counter = counters;
-  a.err = err;
-  a.cstart[0] = 0;
-  for (int k = 0; k < n_send + n_recv; ++k) {
-    const gmt_ipc_chan& c = k < n_send ? sends[k] : recvs[k - n_send];
-    if (c.bytes < 0) return static_cast<int>(hipErrorInvalidValue);
-    a.c[k] = c;
+  if (!p || !p->table || n_send < 0 || n_recv < 0 || n_send + n_recv < 1) return static_cast<int>(hipErrorInvalidValue);
+  const int n = n_send + n_recv;
+  char* host = static_cast<char*>(std::malloc(static_cast<size_t>(gmt_ipc_table_bytes(n))));
+  if (!host) return static_cast<int>(hipErrorOutOfMemory);
+  auto* c = reinterpret_cast<gmt_ipc_chan*>(host);
+  auto* cs = reinterpret_cast<int64_t*>(host + static_cast<size_t>(n) * sizeof(gmt_ipc_chan));
+  cs[0] = 0;
+  for (int k = 0; k < n; ++k) {
+    c[k] = k < n_send ? sends[k] : recvs[k - n_send];
+    if (c[k].bytes < 0) {
+      std::free(host);
+      return static_cast<int>(hipErrorInvalidValue);
+    }
     // a zero-byte channel still takes one chunk: its wait and signal
-    a.cstart[k + 1] = a.cstart[k] + (c.bytes > 0 ? (c.bytes + ipc::kBlockBytes - 1) / ipc::kBlockBytes : 1);
+    cs[k + 1] = cs[k] + (c[k].bytes > 0 ? (c[k].bytes + ipc::kBlockBytes - 1) / ipc::kBlockBytes : 1);
   }
-  const int64_t sc = a.cstart[n_send], rc = a.cstart[n_send + n_recv] - sc;
-  a.sb = sc < ipc::kMaxRoleBlocks ? sc : ipc::kMaxRoleBlocks;
-  a.rb = rc < ipc::kMaxRoleBlocks ? rc : ipc::kMaxRoleBlocks;
+  p->n_send = n_send;
+  p->n_recv = n_recv;
+  p->send_chunks = cs[n_send];
+  p->recv_chunks = cs[n] - cs[n_send];
+  const hipError_t e = hipMemcpy(p->table, host, static_cast<size_t>(gmt_ipc_table_bytes(n)), hipMemcpyHostToDevice);
+  std::free(host);
+  return static_cast<int>(e);
+}
+
+extern "C" int gmt_ipc_exchange(const gmt_ipc_plan* p, void* stream) {
+  using namespace gmt;
+  if (!p || !p->table || !p->epoch || !p->counters || !p->err || p->n_send < 0 || p->n_recv < 0 ||
+      p->n_send + p->n_recv < 1)
+    return static_cast<int>(hipErrorInvalidValue);
+  const int n = p->n_send + p->n_recv;
+  ipc::Args a{};
+  a.chan = static_cast<const gmt_ipc_chan*>(p->table);
+  a.cstart = reinterpret_cast<const int64_t*>(static_cast<const char*>(p->table) + static_cast<size_t>(n) * sizeof(gmt_ipc_chan));
+  a.ns = p->n_send;
+  a.nr = p->n_recv;
+  a.epoch = p->epoch;
+  a.counter = p->counters;
+  a.err = p->err;
+  a.timeout_ticks = ipc::timeout_ticks();
+  a.sb = p->send_chunks < ipc::kMaxRoleBlocks ? p->send_chunks : ipc::kMaxRoleBlocks;
+  a.rb = p->recv_chunks < ipc::kMaxRoleBlocks ? p->recv_chunks : ipc::kMaxRoleBlocks;
+  if (a.sb + a.rb < 1) return static_cast<int>(hipErrorInvalidValue);
   ipc::ipc_exchange_kernel<<<grid_1d(a.sb + a.rb), kBlock, 0, static_cast<hipStream_t>(stream)>>>(a);
   GMT_RET_LAUNCH();
 }

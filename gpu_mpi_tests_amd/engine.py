@@ -1,12 +1,20 @@
 """Python front end of the native Jacobi engine (``libgmt_engine.so``).
 
 The flagship benchmark's step loop runs in C++ (``csrc/engine/jacobi.cpp``):
-halo exchange over RCCL on a high-priority stream overlapped with the
+halo exchange over RCCL (one rank per GPU) or HIP IPC (several ranks per
+GPU, or any same-node job) on a high-priority stream overlapped with the
 interior sweep, both step parities captured into hipGraphs.  Python only does
-the rendezvous: ``torch.distributed`` (one process per GPU) broadcasts the
-RCCL unique id, then each ``run(k)`` is a single ctypes call that enqueues k
-graph replays — no Python on the per-step critical path, which is what keeps
-small per-GPU domains (strong scaling to 8 GPUs) from going launch-bound.
+the rendezvous: ``torch.distributed`` broadcasts a 128-byte id (the RCCL
+unique id, or the name of the IPC transport's socket control plane), then
+each ``run(k)`` is a single ctypes call that enqueues k graph replays — no
+Python on the per-step critical path, which is what keeps small per-GPU
+domains (strong scaling to 8 GPUs) from going launch-bound.
+
+Transport choice (``transport="auto"``, or GMT_TRANSPORT in the environment):
+RCCL when every rank has its own GPU, IPC when ranks share one (RCCL refuses
+two ranks on one device; the reference's oversubscription mode,
+mpi_daxpy.cc:43-54); on the CPU backend the socket emulation of RCCL, with
+"ipc" selecting the memfd emulation of the IPC path.
 
 Library selection: device ``cuda`` loads ``gpu_mpi_tests_amd/_lib`` (HIP,
 gfx950); device ``cpu`` loads ``build/lib-host`` (the CPU backend, same ABI)
@@ -29,7 +37,8 @@ _ROOT = os.path.dirname(_HERE)
 HIP_ENGINE = os.path.join(_HERE, "_lib", "libgmt_engine.so")
 HOST_ENGINE = os.path.join(_ROOT, "build", "lib-host", "libgmt_engine.so")
 
-LOCAL, RCCL = 0, 1
+LOCAL, RCCL, IPC = 0, 1, 2
+_KINDS = {"local": LOCAL, "rccl": RCCL, "ipc": IPC}
 MAX_TSTEPS = 24  # GMT_TB_MAX_SWEEPS (csrc/include/gmt/kernels.h)
 _libs: dict[str, ctypes.CDLL] = {}
 
@@ -62,6 +71,16 @@ def load(device: str = "cuda") -> ctypes.CDLL:
     vp, i64, c_int = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
     lib.gmt_engine_unique_id.argtypes = [vp]
     lib.gmt_engine_unique_id.restype = c_int
+    lib.gmt_engine_control_id.argtypes = [vp]
+    lib.gmt_engine_control_id.restype = c_int
+    lib.gmt_engine_comm_create.argtypes = [c_int, c_int, c_int, vp]
+    lib.gmt_engine_comm_create.restype = vp
+    lib.gmt_engine_comm_allreduce_sum.argtypes = [vp, vp, i64, vp]
+    lib.gmt_engine_comm_allreduce_sum.restype = c_int
+    lib.gmt_engine_comm_name.argtypes = [vp]
+    lib.gmt_engine_comm_name.restype = ctypes.c_char_p
+    lib.gmt_engine_comm_destroy.argtypes = [vp]
+    lib.gmt_engine_comm_destroy.restype = None
     lib.gmt_engine_jacobi_create.argtypes = [i64, i64, c_int, c_int, c_int, c_int, c_int, vp, vp]
     lib.gmt_engine_jacobi_create.restype = vp
     lib.gmt_engine_jacobi_destroy.argtypes = [vp]
@@ -124,19 +143,93 @@ class _StdoutToStderr:
         return False
 
 
-def _broadcast_unique_id(lib, env) -> bytes:
+def _broadcast_id(lib, env, kind: int) -> bytes:
+    """Rank 0 creates the transport's 128-byte id, every rank gets it."""
     buf = ctypes.create_string_buffer(128)
     if env.rank == 0:
-        err = lib.gmt_engine_unique_id(buf)
+        err = (lib.gmt_engine_unique_id if kind == RCCL else lib.gmt_engine_control_id)(buf)
         if err:
-            raise EngineError(f"RCCL unique id failed: {err}")
+            raise EngineError(f"transport id failed: {err}")
     obj = [bytes(buf.raw) if env.rank == 0 else None]
-    torch.distributed.broadcast_object_list(obj, src=0, group=env.host_group)
+    if env.world_size > 1:
+        torch.distributed.broadcast_object_list(obj, src=0, group=env.host_group)
     return obj[0]
 
 
+def resolve_transport(env, transport: str = "auto") -> str:
+    """auto -> rccl with one rank per GPU, ipc when ranks share a GPU; local
+    for one rank.  GMT_TRANSPORT overrides auto (rccl|ipc)."""
+    if transport not in ("auto", "local", "rccl", "ipc"):
+        raise ValueError(f"transport must be auto, local, rccl or ipc, got {transport!r}")
+    if transport == "auto":
+        transport = os.environ.get("GMT_TRANSPORT", "auto").strip().lower() or "auto"
+        if transport not in ("auto", "rccl", "ipc"):
+            raise ValueError(f"GMT_TRANSPORT must be rccl or ipc, got {transport!r}")
+    if transport == "auto":
+        if env.world_size == 1:
+            return "local"
+        return "ipc" if env.is_gpu and env.ranks_per_device > 1 else "rccl"
+    if transport == "local" and env.world_size != 1:
+        raise ValueError("transport 'local' needs world size 1")
+    if transport == "rccl" and env.is_gpu and env.ranks_per_device > 1:
+        raise ValueError(f"RCCL needs one rank per GPU ({env.ranks_per_device} ranks share one): use ipc")
+    return transport
+
+
+def transport_label(kind: str, env) -> str:
+    """Name in reports: the CPU backend's emulations carry a -host suffix."""
+    return kind if env.is_gpu or kind == "local" else f"{kind}-host"
+
+
+def _transport_args(lib, env, transport: str):
+    kind = _KINDS[resolve_transport(env, transport)]
+    if kind == LOCAL:
+        return kind, None
+    return kind, ctypes.create_string_buffer(_broadcast_id(lib, env, kind), 128)
+
+
+class Comm:
+    """A bare communicator on the engine's transports (device collectives
+    outside the solver: bench.py's DAXPY partial-sum all-reduce)."""
+
+    def __init__(self, env=None, transport: str = "auto"):
+        self.env = env or gdist.get()
+        self.lib = load("cuda" if self.env.is_gpu else "cpu")
+        self.kind = resolve_transport(self.env, transport)
+        k, cid = _transport_args(self.lib, self.env, self.kind)
+        with _StdoutToStderr():
+            self.h = self.lib.gmt_engine_comm_create(self.env.rank, self.env.world_size, k, cid)
+        if not self.h:
+            raise EngineError("gmt_engine_comm_create failed")
+        self.name = transport_label(self.lib.gmt_engine_comm_name(self.h).decode(), self.env)
+
+    def allreduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum over ranks of a contiguous float64 tensor on this rank's device."""
+        if t.dtype != torch.float64 or not t.is_contiguous():
+            raise ValueError("allreduce_sum_ needs a contiguous float64 tensor")
+        if (t.device.type == "cuda") != self.env.is_gpu:
+            raise ValueError(f"tensor on {t.device}, communicator on {self.env.device}")
+        stream = torch.cuda.current_stream(t.device).cuda_stream if t.is_cuda else None
+        err = self.lib.gmt_engine_comm_allreduce_sum(self.h, t.data_ptr(), t.numel(), stream)
+        if err:
+            raise EngineError(f"all-reduce failed: {err}")
+        return t
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.gmt_engine_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class NativeJacobi:
-    """Distributed 2-D Jacobi (fp64) on the native engine; one rank per GPU."""
+    """Distributed 2-D Jacobi (fp64) on the native engine: one rank per GPU
+    (RCCL) or several ranks per GPU (IPC)."""
 
     def __init__(self, ny: int, nx: int, env: "gdist.DistEnv | None" = None,
                  dims: tuple[int, int] | None = None, periodic: bool = False,
@@ -153,26 +246,19 @@ class NativeJacobi:
         if py * px != e.world_size:
             raise ValueError(f"process grid {py}x{px} != world size {e.world_size}")
         self.ny_g, self.nx_g, self.py, self.px = ny, nx, py, px
-        if transport not in ("auto", "local", "rccl"):
-            raise ValueError(f"transport must be auto, local or rccl, got {transport!r}")
-        if e.world_size == 1 and transport != "rccl":
-            transport, cid = LOCAL, None
-        elif e.world_size == 1:
-            # a 1-rank RCCL communicator: a periodic domain exchanges its halo
-            # with itself through ncclSend/ncclRecv (latency measurements)
-            transport = RCCL
-            buf = ctypes.create_string_buffer(128)
-            if self.lib.gmt_engine_unique_id(buf):
-                raise EngineError("RCCL unique id failed")
-            cid = ctypes.create_string_buffer(bytes(buf.raw), 128)
+        kind = resolve_transport(e, transport)
+        if e.world_size == 1 and kind in ("rccl", "ipc"):
+            # a 1-rank communicator: a periodic domain exchanges its halo with
+            # itself through the transport (latency measurements)
+            k = _KINDS[kind]
+            cid = ctypes.create_string_buffer(_broadcast_id(self.lib, e, k), 128)
+            transport = k
         else:
-            if transport == "local":
-                raise ValueError("transport 'local' needs world size 1")
-            # GPU: RCCL over xGMI.  CPU: the host backend's emulation of the same
-            # RCCL semantics over Unix sockets (csrc/host/ccl_host.cpp), so the
+            # GPU: RCCL over xGMI or HIP IPC.  CPU: the host backend's
+            # emulations of the same semantics (RCCL over Unix sockets,
+            # csrc/host/ccl_host.cpp; IPC over memfd-shared memory), so the
             # multi-rank engine path runs and is checked without GPUs.
-            transport = RCCL
-            cid = ctypes.create_string_buffer(_broadcast_unique_id(self.lib, e), 128)
+            transport, cid = _transport_args(self.lib, e, kind)
         ks = 1 if not tblock else (2 if tblock is True else int(tblock))
         if not 1 <= ks <= MAX_TSTEPS:
             raise ValueError(f"tblock: sweeps per fused pass must be 1..{MAX_TSTEPS}, got {ks}")
@@ -200,7 +286,7 @@ class NativeJacobi:
         self.tblock = self.tsteps > 1
         self.graph = bool(graph_on)
         self.overlap = bool(overlap_on)
-        self.transport = ("rccl" if e.is_gpu else "rccl-host") if transport == RCCL else "local"
+        self.transport = transport_label(kind, e)
 
     # ------------------------------------------------------------------
     def run(self, steps: int) -> None:
@@ -250,21 +336,18 @@ class NativeJacobi:
 
 
 def deriv_bench(n_local: int = 1024, n_other: int = 512 * 1024, n_iter: int = 100,
-                n_warmup: int = 5, env: "gdist.DistEnv | None" = None) -> dict:
+                n_warmup: int = 5, env: "gdist.DistEnv | None" = None, transport: str = "auto") -> dict:
     """The reference's main benchmark on the native engine (one rank per GPU,
     RCCL): ``mpi_stencil2d_gt``'s test_deriv for dim 0 and dim 1 (2-deep
     ghost faces of ``n_other`` values per neighbour — 8 MiB at the reference
     default — exchanged, then the derivative kernel, ``n_iter`` times) and
     test_sum (in-place all-reduce of 1024 doubles).  Returns this rank's
     per-exchange seconds (median/mean/min/max), bytes sent per exchange,
-    err_norm, and the all-reduce median seconds.  Collective: every rank calls it."""
+    err_norm, and the all-reduce median seconds.  Collective: every rank calls it.
+    Transport as NativeJacobi (RCCL, IPC when ranks share a GPU)."""
     e = env or gdist.get()
     lib = load("cuda" if e.is_gpu else "cpu")
-    if e.world_size > 1:
-        transport = RCCL
-        cid = ctypes.create_string_buffer(_broadcast_unique_id(lib, e), 128)
-    else:
-        transport, cid = LOCAL, None
+    transport, cid = _transport_args(lib, e, transport)
     out = (ctypes.c_double * 14)()
     with _StdoutToStderr():
         err = lib.gmt_engine_deriv_bench(int(n_local), int(n_other), int(n_iter), int(n_warmup), e.rank,
@@ -279,6 +362,7 @@ def deriv_bench(n_local: int = 1024, n_other: int = 512 * 1024, n_iter: int = 10
                               err_norm=o[5])
     res["allreduce_median_s"] = v[12]
     res["allreduce_max_rel_err"] = v[13]
+    res["transport"] = transport_label({LOCAL: "local", RCCL: "rccl", IPC: "ipc"}[transport], e)
     return res
 
 

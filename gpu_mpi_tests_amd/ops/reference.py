@@ -62,8 +62,12 @@ def poly(mode: int, nx: int, ny: int, x0: float, dx: float, y0: float, dy: float
         v = X * X * X + Y * Y
     elif mode == 1:
         v = 3 * X * X
-    else:
+    elif mode == 2:
         v = 2 * Y
+    elif mode == 3:
+        v = X.clone()  # linear ramp (DAXPY inputs), gmt_fill_poly mode 3
+    else:
+        raise ValueError(f"poly: mode {mode} (0-3 here; mode 4 is the engine's integer lattice)")
     return v.to(dtype)
 
 

@@ -6,6 +6,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 from conftest import free_port
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -13,8 +15,8 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
         "scaling", "vs_baseline", "dtype", "data", "config"}
 
 
-def _run(cmd, timeout=600):
-    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+def _run(cmd, timeout=600, **extra_env):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1", **extra_env)
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=env)
     assert p.returncode == 0, p.stdout + p.stderr
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -38,6 +40,11 @@ def _baseline_keys(rec, small):
     assert rec[f"stencil_{small}_MLUPS"] > 0 and "steps:" in rec[f"stencil_{small}_pass_plan"]
     assert rec["halo_exchange_us"] is not None and rec["halo_exchange_us"] > 0
     assert rec["halo_exchange_kind"]
+    # BASELINE config 3: DAXPY partial sums all-reduced, checked against the closed form
+    assert rec["daxpy_allsum_rel_err"] <= 1e-9
+    assert rec["daxpy_allsum_exact"] == rec["n_gpus"] * (rec["daxpy_n"] + 1) / 2
+    assert rec["daxpy_allreduce_us"] > 0 and rec["daxpy_partial_sum_us"] > 0
+    assert rec["daxpy_allreduce_kind"]
     plan = rec["config"]["pass_plan"]
     assert plan and sum(int(a) * int(b) for a, b in (p.split("x") for p in plan.split("+"))) == rec["steps"]
 
@@ -52,16 +59,22 @@ def test_bench_single_process_native_engine_cpu():
     assert "self-exchange" in rec["halo_exchange_kind"]
 
 
-def test_bench_two_ranks_torchrun_cpu():
+@pytest.mark.parametrize("transport", ["rccl", "ipc"])
+def test_bench_two_ranks_torchrun_cpu(transport):
+    """N = 2 under torchrun on the CPU backend; GMT_TRANSPORT=ipc runs the IPC
+    transport (socket control plane + memfd emulation of the IPC kernel) that
+    oversubscribed GPU ranks use."""
     port = str(free_port())
     rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
                 "--device", "cpu", "--size", "256", "--steps", "3", "--warmup", "1",
                 "--daxpy-n", "20000", "--ref-n-local", "32", "--ref-n-other", "300",
-                "--ref-iters", "4", "--small-size", "96"])
+                "--ref-iters", "4", "--small-size", "96"], GMT_TRANSPORT=transport)
     _check(rec, 2, 3, 1)
     _baseline_keys(rec, 96)
-    assert rec["config"]["engine"] == "native" and rec["config"]["transport"] == "rccl-host"
+    assert rec["config"]["engine"] == "native" and rec["config"]["transport"] == f"{transport}-host"
+    assert rec["ref_halo_config"].endswith(f"{transport}-host")
+    assert rec["daxpy_allreduce_kind"] == f"{transport}-host"
     assert rec["halo_exchange_us"] is not None and rec["halo_exchange_us"] > 0
     # the reference's own halo benchmark (test_deriv dim 0/1 + test_sum) on the same ranks
     assert rec["ref_halo_dim0_us"] > 0 and rec["ref_halo_dim1_us"] > 0
@@ -93,3 +106,21 @@ def test_bench_overlap_autotune_keeps_the_solution():
     tuned = two["config"]["overlap_tuning"]
     assert tuned and tuned["overlap_s"] > 0 and tuned["serial_s"] > 0
     assert abs(two["residual_l2"] - one["residual_l2"]) <= 1e-12 * max(1.0, one["residual_l2"])
+
+
+def test_bench_ipc_peer_hang_fails_the_job_cpu():
+    """Fault injection on the IPC transport (CPU backend): rank 1 stops at its
+    3rd halo exchange; rank 0's bounded wait gives up, the engine reads the
+    error word at synchronize() and aborts — the job exits non-zero with no
+    JSON number (the GPU version: tests/test_multirank_gpu.py)."""
+    port = str(free_port())
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
+               GMT_TRANSPORT="ipc", GMT_INJECT_HANG="1:2", GMT_WAIT_TIMEOUT_MS="500")
+    p = subprocess.run(["timeout", "-k", "5", "120", sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port", port, "bench.py",
+                        "--gpus", "2", "--device", "cpu", "--size", "128", "--steps", "6", "--warmup", "1",
+                        "--skip-extras"], capture_output=True, text=True, timeout=150, cwd=ROOT, env=env)
+    assert p.returncode != 0, p.stdout + p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")], p.stdout
+    assert "GMT FAULT INJECTION: rank 1" in p.stderr, p.stderr[-4000:]
+    assert "timed out waiting for the peer" in p.stdout + p.stderr, (p.stdout + p.stderr)[-4000:]

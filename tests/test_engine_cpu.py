@@ -74,6 +74,7 @@ def test_native_engine_k_sweeps(k):
     assert r["diff"] < 1e-13
 
 
+@pytest.mark.parametrize("transport", ["rccl", "ipc"])
 @pytest.mark.parametrize("np_,ny,nx,steps,periodic,overlap,tblock,dims", [
     (2, 40, 70, 7, False, True, 0, None),
     (2, 41, 66, 9, True, True, 2, "1x2"),
@@ -82,10 +83,11 @@ def test_native_engine_k_sweeps(k):
     (3, 50, 90, 11, True, False, 8, "1x3"),
     (6, 66, 70, 10, True, True, 6, "2x3"),
 ])
-def test_native_engine_multirank_rccl_semantics(np_, ny, nx, steps, periodic, overlap, tblock, dims):
+def test_native_engine_multirank(transport, np_, ny, nx, steps, periodic, overlap, tblock, dims):
     """The multi-GPU data plane of bench.py (native engine, RCCL grouped
-    send/recv, temporal-blocking halos with corners, residual all-reduce) at
-    np_ ranks on the CPU backend: the result equals the serial sweep."""
+    send/recv or the IPC transport over the socket control plane,
+    temporal-blocking halos with corners, residual all-reduce) at np_ ranks
+    on the CPU backend: the result equals the serial sweep."""
     ensure_host_build()
     port = str(free_port())
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(np_),
@@ -94,10 +96,10 @@ def test_native_engine_multirank_rccl_semantics(np_, ny, nx, steps, periodic, ov
            "1" if periodic else "0", "1" if overlap else "0", str(tblock)] + ([dims] if dims else [])
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
                        env=dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
-                                OMP_NUM_THREADS="1"))
+                                OMP_NUM_THREADS="1", GMT_TRANSPORT=transport))
     assert p.returncode == 0, p.stdout + p.stderr
     r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
-    assert r["transport"] == "rccl-host"
+    assert r["transport"] == f"{transport}-host"
     assert r["diff"] < 1e-13, r
     assert r["resid_same"]
     if dims:
