@@ -95,22 +95,26 @@ def plan_str(plan):
     return "+".join(out)
 
 
-def bench_native(env, shape, steps, warmup, overlap, dims, graph, tblock, wg_waves, seg_rows):
+def bench_native(env, shape, steps, warmup, overlap, dims, graph, tblock, wg_waves, seg_rows, init="random",
+                 seed=0, calibrate=True):
     from gpu_mpi_tests_amd.engine import NativeJacobi
 
     eng = NativeJacobi(shape[0], shape[1], env, dims=dims, overlap=overlap, graph=graph, tblock=tblock,
-                       wg_waves=wg_waves, seg_rows=seg_rows)
-    eng.prepare(steps)  # one launch of every pass type of the timed plan, initial field restored
+                       wg_waves=wg_waves, seg_rows=seg_rows, init=init, seed=seed, calibrate=calibrate)
+    # calibration (one timed pass of every pass size on this share, max over
+    # ranks) -> the plan; then one launch of every pass type of the timed
+    # plan; the initial field is restored
+    eng.prepare(steps)
     dt = _timed(env, eng.run, eng.synchronize, steps, warmup)
     info = {"engine": "native", "graph": eng.graph, "overlap": eng.overlap, "tblock": eng.tblock,
             "overlap_tuning": eng.tuned, "tsteps": eng.tsteps, "pass_plan": plan_str(eng.plan(steps)),
-            "exact": eng.exact,
+            "exact": eng.exact, "max_abs_u0": eng.max_abs_u0, "pass_cost_ms": eng.pass_cost_ms(),
             "transport": eng.transport if env.world_size > 1 else "none",
             "halo_bytes_per_rank": eng.halo_bytes, "dims": (eng.py, eng.px)}
     return eng, dt, info
 
 
-def check_engine(env, dims, tsteps, graph):
+def check_engine(env, dims, tsteps, graph, init="analytic", seed=0):
     """Distributed-correctness gate (reference: mpi_stencil2d_gt.cc:555-570
     err_norm): the engine with this job's process grid and sweeps per pass on
     a small Dirichlet domain, overlap on and off, vs the serial NumPy
@@ -126,10 +130,11 @@ def check_engine(env, dims, tsteps, graph):
     wb = group_cols(k, 0, "cuda" if env.is_gpu else "cpu") if k > 1 else 0
     ny, nx = py * (4 * k + 75) + 3, px * (3 * wb + 8 * k + 37) + 5
     steps = 2 * k + 3  # full passes, a remainder pass and (odd) single sweeps
-    ref = serial_jacobi(ny, nx, steps) if env.rank == 0 else None
+    ref = serial_jacobi(ny, nx, steps, init=init, seed=seed) if env.rank == 0 else None
     worst = 0.0
     for ov in (True, False):
-        e = NativeJacobi(ny, nx, env, dims=dims, overlap=ov, graph=graph, tblock=k if k > 1 else False)
+        e = NativeJacobi(ny, nx, env, dims=dims, overlap=ov, graph=graph, tblock=k if k > 1 else False,
+                         init=init, seed=seed)
         e.run(steps)
         e.synchronize()
         part = (e.off_y, e.off_x, e.interior())
@@ -212,6 +217,10 @@ def ref_halo(env, n_local, n_other, iters):
     for d in (0, 1):
         out[f"ref_halo_dim{d}_us"] = round(gdist.allreduce_max(r[f"dim{d}"]["median_s"], env) * 1e6, 2)
         out[f"ref_halo_dim{d}_err_norm"] = gdist.allreduce_max(r[f"dim{d}"]["err_norm"], env)
+        # scale-free: round-off of x^3 + y^2 at the reference's spacing grows
+        # with the extent; a missing or wrong ghost cell gives O(1) and more
+        out[f"ref_halo_dim{d}_rel_err"] = gdist.allreduce_max(
+            r[f"dim{d}"]["err_norm"] / max(r[f"dim{d}"]["exact_norm"], 1e-300), env)
     out["ref_halo_bytes_per_rank"] = int(gdist.allreduce_max(float(r["dim0"]["bytes"]), env))
     out["ref_allreduce_1024_us"] = round(gdist.allreduce_max(r["allreduce_median_s"], env) * 1e6, 2)
     return out
@@ -318,6 +327,13 @@ def main(argv=None):
                     help="temporal-blocking kernel: 128-column waves per workgroup (0 = auto)")
     ap.add_argument("--seg-rows", type=int, default=0, help="temporal-blocking kernel: rows per workgroup (0 = auto)")
     ap.add_argument("--dims", type=str, default=None, help="process grid PYxPX, e.g. 4x2")
+    ap.add_argument("--init", choices=("random", "analytic"), default="random",
+                    help="initial field: random (default: uniform [0,1), a hash of the global lattice "
+                         "point and --seed, the same for every process grid) or analytic x^3+y^2")
+    ap.add_argument("--seed", type=int, default=20261017, help="random-init seed")
+    ap.add_argument("--no-calibrate", action="store_true",
+                    help="plan passes from the built-in cost table instead of timing each pass size "
+                         "on the real share at start-up")
     ap.add_argument("--daxpy-n", type=int, default=1 << 28)
     ap.add_argument("--small-size", type=int, default=8192,
                     help="second stencil domain (BASELINE single-GPU config 8192^2; 0 = skip)")
@@ -347,7 +363,7 @@ def main(argv=None):
     tsteps = (args.tsteps or DEFAULT_TSTEPS) if args.tblock == "on" else 1
     extras = {}
     if not args.skip_check:
-        diff = check_engine(env, dims or gdims, tsteps, graph)
+        diff = check_engine(env, dims or gdims, tsteps, graph, args.init, args.seed)
         extras["check_max_diff"] = diff
         extras.update(peer_status(env, dims or gdims))
         if diff != 0.0:
@@ -357,7 +373,8 @@ def main(argv=None):
             gdist.shutdown()
             sys.exit(3)
     solver, dt, info = bench_native(env, shape, args.steps, args.warmup, overlap, dims, graph,
-                                    tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows)
+                                    tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows,
+                                    args.init, args.seed, not args.no_calibrate)
     points = shape[0] * shape[1]
     mlups = points * args.steps / dt / 1e6
     ms_per_step = dt / args.steps * 1e3
@@ -382,7 +399,8 @@ def main(argv=None):
             s2 = (args.small_size, args.small_size)
             steps2 = max(100, 4 * args.steps)
             eng2, dt2, info2 = bench_native(env, s2, steps2, max(args.warmup, 10), overlap, dims, graph,
-                                            tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows)
+                                            tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows,
+                                            args.init, args.seed, not args.no_calibrate)
             eng2.close()
             extras[f"stencil_{args.small_size}_MLUPS"] = round(s2[0] * s2[1] * steps2 / dt2 / 1e6, 1)
             extras[f"stencil_{args.small_size}_ms_per_step"] = round(dt2 / steps2 * 1e3, 5)
@@ -418,7 +436,9 @@ def main(argv=None):
             "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "fp64",
-            "data": "synthetic (analytic x^3+y^2 initial field, Dirichlet boundary)",
+            "data": (f"synthetic: random-init field, uniform [0,1) hashed from the global lattice point "
+                     f"(seed {args.seed}), Dirichlet boundary" if args.init == "random" else
+                     "synthetic: analytic x^3+y^2 initial field, Dirichlet boundary"),
             "config": {
                 "model": f"mpi_stencil2d jacobi5 {shape[0]}x{shape[1]} fp64",
                 "global_batch": points,
@@ -432,6 +452,9 @@ def main(argv=None):
                 "sweeps_per_pass": info.get("tsteps", 1),
                 "pass_plan": info.get("pass_plan"),
                 "exact_levels": info.get("exact"),
+                "init": args.init,
+                "max_abs_u0": info.get("max_abs_u0"),
+                "pass_cost_ms": info.get("pass_cost_ms"),
                 "transport": info["transport"],
                 "halo_bytes_per_rank": info["halo_bytes_per_rank"],
                 "device": str(env.device),

@@ -58,6 +58,9 @@ class RcclTransport : public Transport {
   void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override {
     GMT_CCL_CHECK("allreduce", gmt_ccl_allreduce_sum_f64(buf, buf, n, cc_, s));
   }
+  void allreduce_max(double* buf, size_t n, gmt_stream_t s) override {
+    GMT_CCL_CHECK("allreduce max", gmt_ccl_allreduce_max_f64(buf, buf, n, cc_, s));
+  }
   void allgather(const void* send, void* recv, size_t bpr, gmt_stream_t s) override {
     GMT_CCL_CHECK("allgather", gmt_ccl_allgather(send, recv, bpr, cc_, s));
   }
@@ -106,6 +109,7 @@ class LocalTransport : public Transport {
     return std::make_unique<LocalExchange>(r, s);
   }
   void allreduce_sum(double*, size_t, gmt_stream_t) override {}
+  void allreduce_max(double*, size_t, gmt_stream_t) override {}
   void allgather(const void* send, void* recv, size_t bpr, gmt_stream_t s) override {
     if (send != recv) GMT_CHECK("local gather", gmt_rt_memcpy_async(recv, send, bpr, s));
   }

@@ -226,12 +226,17 @@ class IpcTransport : public Transport {
   }
   // Host-staged through one persistent pinned buffer (grown on demand): a
   // device D2H, the control plane's rank-ordered sum, an H2D on the stream.
-  void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override {
+  void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override { staged(buf, n, s, false); }
+  void allreduce_max(double* buf, size_t n, gmt_stream_t s) override { staged(buf, n, s, true); }
+  void staged(double* buf, size_t n, gmt_stream_t s, bool max) {
     if (size_ == 1) return;
     double* h = stage(n * sizeof(double));
     GMT_CHECK("allreduce D2H", gmt_rt_memcpy_async(h, buf, n * sizeof(double), s));
     GMT_CHECK("allreduce sync", gmt_rt_stream_synchronize(s));
-    ctl_->allreduce_sum(h, n);
+    if (max)
+      ctl_->allreduce_max(h, n);
+    else
+      ctl_->allreduce_sum(h, n);
     GMT_CHECK("allreduce H2D", gmt_rt_memcpy_async(buf, h, n * sizeof(double), s));
     // the pinned buffer is reused by the next call: the copy must have read it
     GMT_CHECK("allreduce sync", gmt_rt_stream_synchronize(s));

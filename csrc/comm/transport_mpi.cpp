@@ -72,11 +72,11 @@ class Staging {
   Buffer<char> buf_;
 };
 
-void staged_allreduce(Staging& st, MPI_Comm c, double* buf, size_t n, gmt_stream_t s) {
+void staged_allreduce(Staging& st, MPI_Comm c, double* buf, size_t n, gmt_stream_t s, MPI_Op op = MPI_SUM) {
   double* h = reinterpret_cast<double*>(st.get(n * sizeof(double)));
   GMT_CHECK("allreduce D2H", gmt_rt_memcpy_async(h, buf, n * sizeof(double), s));
   GMT_CHECK("allreduce sync", gmt_rt_stream_synchronize(s));
-  GMT_MPI_CHECK(MPI_Allreduce(MPI_IN_PLACE, h, static_cast<int>(n), MPI_DOUBLE, MPI_SUM, c));
+  GMT_MPI_CHECK(MPI_Allreduce(MPI_IN_PLACE, h, static_cast<int>(n), MPI_DOUBLE, op, c));
   GMT_CHECK("allreduce H2D", gmt_rt_memcpy_async(buf, h, n * sizeof(double), s));
   GMT_CHECK("allreduce sync", gmt_rt_stream_synchronize(s));  // the staging is reused next call
 }
@@ -263,6 +263,9 @@ class MpiHostTransport : public MpiTransport {
   void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override {
     staged_allreduce(staging_, comm_, buf, n, s);
   }
+  void allreduce_max(double* buf, size_t n, gmt_stream_t s) override {
+    staged_allreduce(staging_, comm_, buf, n, s, MPI_MAX);
+  }
   void allgather(const void* send, void* recv, size_t bpr, gmt_stream_t s) override {
     staged_allgather(staging_, comm_, rank_, size_, send, recv, bpr, s);
   }
@@ -329,6 +332,11 @@ class MpiDirectTransport : public MpiTransport {
     require_mpi_readable(buf, "all-reduce buffer");
     GMT_CHECK("allreduce sync", gmt_rt_stream_synchronize(s));
     GMT_MPI_CHECK(MPI_Allreduce(MPI_IN_PLACE, buf, static_cast<int>(n), MPI_DOUBLE, MPI_SUM, comm_));
+  }
+  void allreduce_max(double* buf, size_t n, gmt_stream_t s) override {
+    require_mpi_readable(buf, "all-reduce buffer");
+    GMT_CHECK("allreduce sync", gmt_rt_stream_synchronize(s));
+    GMT_MPI_CHECK(MPI_Allreduce(MPI_IN_PLACE, buf, static_cast<int>(n), MPI_DOUBLE, MPI_MAX, comm_));
   }
   void allgather(const void* send, void* recv, size_t bpr, gmt_stream_t s) override {
     require_mpi_readable(send, "all-gather send buffer");

@@ -36,6 +36,7 @@ extern "C" int gmt_engine_deriv_bench(int64_t n_local, int64_t n_other, int n_it
     o[3] = r.iters.max();
     o[4] = static_cast<double>(r.bytes_per_exchange);
     o[5] = r.err_norm;
+    out[14 + dim] = r.exact_norm;
   }
   const gmt::apps::SumResult s = gmt::apps::run_sum_on(0, GMT_SPACE_DEVICE, static_cast<size_t>(n_local),
                                                        static_cast<size_t>(n_other), n_iter, n_warmup,

@@ -78,7 +78,8 @@ void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank,
   gmt_engine_opts o{};
   if (opts) o = *opts;
   if (o.tsteps < 0 || o.tsteps > GMT_TB_MAX_SWEEPS || o.overlap < 0 || o.overlap > 2 || o.wg_waves < 0 ||
-      o.wg_waves > 8 || o.seg_rows < 0 || o.exact < -1 || o.exact > 1)
+      o.wg_waves > 8 || o.seg_rows < 0 || o.exact < -1 || o.exact > 1 || o.init < 0 || o.init > 1 ||
+      o.calibrate < 0 || o.calibrate > 1 || o.seed < 0 || o.seed >= (int64_t(1) << 53))
     return nullptr;
   auto* h = new Handle();
   h->t = gmt::engine_transport(rank, world, transport, ccl_id);
@@ -100,6 +101,9 @@ void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank,
   c.wg_waves = o.wg_waves;
   c.seg_rows = o.seg_rows;
   c.exact = o.exact;
+  c.init = o.init;
+  c.seed = static_cast<uint64_t>(o.seed);
+  c.calibrate = o.calibrate != 0;
   h->py = py;
   h->px = px;
   h->s = std::make_unique<gmt::JacobiSolver>(*h->t, c);
@@ -159,6 +163,15 @@ int gmt_engine_jacobi_prepare(void* p, int steps) {
 int gmt_engine_jacobi_copy_interior(void* p, double* host) {
   static_cast<Handle*>(p)->s->copy_interior(host);
   return 0;
+}
+double gmt_engine_jacobi_stat(void* p, int what) {
+  const auto& s = *static_cast<Handle*>(p)->s;
+  switch (what) {
+    case 0: return s.max_abs_u0();
+    case 1: return s.measured_pass_ms(s.tsteps());
+    case 2: return s.table_pass_ms(s.tsteps());
+    default: return 0.0;
+  }
 }
 const char* gmt_engine_backend(void) { return gmt_rt_backend_name(); }
 

@@ -76,13 +76,10 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   ks_ = c.tsteps > 1 ? c.tsteps : (c.tblock ? 2 : 1);
   if (ks_ > GMT_TB_MAX_SWEEPS) ks_ = GMT_TB_MAX_SWEEPS;
   while (ks_ > 1 && !gmt_jacobi5tb_supported(ks_)) --ks_;  // odd counts above 10: the next even one
-  // Scaled levels (4^p u_p) are bitwise equal to the exact form while
-  // max|u| * 4^K stays finite (and no level value is subnormal).  The initial
-  // field x^3 + y^2 on [-gh, 1 + gh]^2 is bounded by 2 + 3gh, and every
-  // Jacobi sweep averages, so that bound holds for every later field.
-  const double hb = 1.0 / (static_cast<double>(c.ny_global > c.nx_global ? c.ny_global : c.nx_global) + 1);
-  const double umax = 2.0 + 3.0 * ks_ * hb;
-  exact_ = c.exact == 1 || !(umax * std::ldexp(1.0, 2 * ks_) < 1e300);
+  if (c.init != 0 && c.init != 1) {
+    std::printf("JacobiSolver: init must be 0 (analytic) or 1 (random), got %d\n", c.init);
+    abort_job(EXIT_FAILURE);
+  }
   g_ = ks_;
   yo_ = g_;
   xo_ = round_up(g_, 8);  // ghost columns fit left of the interior; 64-B aligned interior
@@ -99,6 +96,16 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   // ring: u(x, y) = x^3 + y^2 at global ghost-inclusive coordinates * h
   for (int b = 0; b < 2; ++b) buf_[b] = Buffer<double>(elems, GMT_SPACE_DEVICE);
   init_field();
+  // Scaled levels (4^p u_p) are bitwise equal to the exact form while
+  // max|u| * 4^K stays finite (and no level value is subnormal).  Every
+  // Jacobi sweep averages, so the initial field's max|u| — measured here on
+  // the device, max over ranks — bounds every later field.
+  umax_ = measure_max_abs();
+  exact_ = c.exact == 1 || !(umax_ * std::ldexp(1.0, 2 * ks_) < 1e300);
+  // exact passes stop at the largest K whose kernel fits the register file
+  // (the ghost ring keeps its width: wider than a pass needs is harmless)
+  if (ks_ > 1 && exact_)
+    while (ks_ > gmt_jacobi5tb_max_sweeps(1) || !gmt_jacobi5tb_supported(ks_)) --ks_;
   resid_ws_ = Buffer<double>(gmt_jacobi_resid_workspace(nx_, ny_) + 1, GMT_SPACE_DEVICE);
   // band-first passes: arrival counter, signal, waiter's count, error word
   sig_ = Buffer<uint64_t>(4, GMT_SPACE_FLAGS);
@@ -115,12 +122,72 @@ void JacobiSolver::init_field() {
   const double h = 1.0 / (static_cast<double>(c.ny_global > c.nx_global ? c.ny_global : c.nx_global) + 1);
   for (int b = 0; b < 2; ++b) {
     GMT_CHECK("memset", gmt_rt_memset_async(buf_[b].data(), 0, buf_[b].bytes(), s_));
-    GMT_CHECK("fill", gmt_fill_poly(4, nx_ + 2 * g_, ny_ + 2 * g_, static_cast<double>(ox_ - g_), h,
-                                    static_cast<double>(oy_ - g_), h, buf_[b].data() + (xo_ - g_), ld_, s_));
+    // global lattice index of the first ghost column / row: ox_ - g_, oy_ - g_
+    if (c.init == 1)
+      GMT_CHECK("fill", gmt_fill_poly(5, nx_ + 2 * g_, ny_ + 2 * g_, static_cast<double>(ox_ - g_),
+                                      static_cast<double>(c.seed), static_cast<double>(oy_ - g_), 0.0,
+                                      buf_[b].data() + (xo_ - g_), ld_, s_));
+    else
+      GMT_CHECK("fill", gmt_fill_poly(4, nx_ + 2 * g_, ny_ + 2 * g_, static_cast<double>(ox_ - g_), h,
+                                      static_cast<double>(oy_ - g_), h, buf_[b].data() + (xo_ - g_), ld_, s_));
   }
   GMT_CHECK("init sync", gmt_rt_stream_synchronize(s_));
   parity_ = 0;
   fresh_[0] = fresh_[1] = false;  // periodic / neighbour ghosts come from an exchange
+}
+
+double JacobiSolver::measure_max_abs() {
+  const int64_t w = nx_ + 2 * g_, hgt = ny_ + 2 * g_;
+  Buffer<double> ws(static_cast<size_t>(gmt_diff_sq_workspace(w, hgt)) + 1, GMT_SPACE_DEVICE);
+  GMT_CHECK("abs max", gmt_abs_max(w, hgt, buf_[parity_].data() + (xo_ - g_), ld_, ws.data(), ws.data() + 1, s_));
+  t_.allreduce_max(ws.data(), 1, s_);
+  double m = 0.0;
+  GMT_CHECK("abs max D2H", gmt_rt_memcpy_async(&m, ws.data(), sizeof(double), s_));
+  GMT_CHECK("abs max sync", gmt_rt_stream_synchronize(s_));
+  return m;
+}
+
+// One timed pass of every size the planner may use, on this rank's share
+// with its real neighbours (a serial pass includes its exchange), max over
+// ranks: the job's pass takes as long as its slowest rank.
+void JacobiSolver::calibrate_costs() {
+  if (ks_ < 2) return;
+  std::vector<int> ks;
+  for (int K = 1; K <= ks_; ++K)
+    if (K == 1 || gmt_jacobi5tb_supported(K)) ks.push_back(K);
+  Buffer<double> d(ks.size(), GMT_SPACE_DEVICE);
+  std::vector<double> host(ks.size(), 0.0);
+  constexpr int kPasses = 2;
+  for (size_t i = 0; i < ks.size(); ++i) {
+    const int K = ks[i];
+    auto one = [&] {
+      if (K == 1) {
+        step();
+      } else {
+        enqueue_block(parity_, K);
+        parity_ ^= 1;
+      }
+    };
+    one();  // first launch of this pass type (code object, occupancy query)
+    synchronize();
+    const double t0 = wtime();
+    for (int r = 0; r < kPasses; ++r) one();
+    synchronize();
+    host[i] = (wtime() - t0) / kPasses * 1e3;
+  }
+  GMT_CHECK("calib H2D", gmt_rt_memcpy(d.data(), host.data(), host.size() * sizeof(double)));
+  t_.allreduce_max(d.data(), host.size(), s_);
+  GMT_CHECK("calib D2H", gmt_rt_memcpy_async(host.data(), d.data(), host.size() * sizeof(double), s_));
+  GMT_CHECK("calib sync", gmt_rt_stream_synchronize(s_));
+  for (size_t i = 0; i < ks.size(); ++i) meas_ms_[ks[i]] = host[i];
+  calibrated_ = true;
+  // the built-in table was measured on one box for one kernel revision: say
+  // so when this share disagrees with it by more than 10 %
+  const double tab = table_pass_ms(ks_), got = meas_ms_[ks_];
+  if (t_.rank() == 0 && tab > 0 && std::fabs(got - tab) > 0.1 * tab)
+    std::fprintf(stderr, "# jacobi: measured %d-sweep pass %.3f ms vs the cost table's %.3f ms (%+.0f%%); "
+                         "planning with the measured costs\n", ks_, got, tab, 100.0 * (got - tab) / tab);
+  init_field();  // the timed passes advanced the solution: start over
 }
 
 void JacobiSolver::autotune_overlap() {
@@ -318,9 +385,9 @@ void JacobiSolver::step_block() {
 // shape and segment plan, Dirichlet sides, MI355X, profiles/r02_tb4c.md, the
 // 4-column kernel) on two domain sizes.  One-wave strips (K <= 8) run at
 // ~3.7-4.1 ms at 32768^2 (K = 9, 10 sit at 253-255 VGPRs); two-stage strips
-// (K >= 12) are VALU bound from K ~ 16; K = 22, 24 exceed the register file
-// at 2 waves per SIMD and spill (twice the time: the planner avoids them).
-// 0 = no kernel for that K (odd K > 10).
+// (K >= 12) are VALU bound from K ~ 16 (K = 22, 24 would exceed the register
+// file at 2 waves per SIMD and spill: not built).  0 = no kernel for that K
+// (odd K > 10).
 namespace {
 struct PassCosts {
   double points;  // lattice points of the measured domain
@@ -328,33 +395,42 @@ struct PassCosts {
 };
 constexpr PassCosts kCostLarge = {32768.0 * 32768.0,
                                   {0,    3.98, 4.13, 3.79, 3.86, 3.85, 3.68, 3.85, 3.91, 4.58, 4.57, 0,    3.63,
-                                   0,    3.76, 0,    3.89, 0,    4.30, 0,    4.68, 0,    8.98, 0,    9.78}};
+                                   0,    3.76, 0,    3.89, 0,    4.30, 0,    4.68}};
 constexpr PassCosts kCostSmall = {8192.0 * 8192.0,
                                   {0,     0.311, 0.300, 0.294, 0.292, 0.292, 0.302, 0.287, 0.289,
                                    0.317, 0.322, 0,     0.264, 0,     0.284, 0,     0.289, 0,
-                                   0.319, 0,     0.349, 0,     0.676, 0,     0.714}};
+                                   0.319, 0,     0.349}};
 constexpr double kLaunchMs = 0.015;    // host launch + dispatch per pass
 constexpr double kExchangeMs = 0.035;  // a halo exchange not hidden by the overlap
 }  // namespace
 
-std::vector<int> JacobiSolver::plan_passes(int k) const {
-  std::vector<int> plan;
-  if (k <= 0) return plan;
-  if (ks_ <= 1) return std::vector<int>(k, 1);
+double JacobiSolver::table_pass_ms(int K) const {
+  if (K < 1 || K > GMT_TB_MAX_SWEEPS) return 0.0;
   // the table measured on the closer domain size, scaled to this rank's
   const double pts = static_cast<double>(nx_) * static_cast<double>(ny_);
   const PassCosts& tab = std::fabs(std::log(pts / kCostLarge.points)) < std::fabs(std::log(pts / kCostSmall.points))
                              ? kCostLarge
                              : kCostSmall;
-  const double scale = pts / tab.points;
+  if (tab.ms[K] <= 0) return 0.0;
   const double over = kLaunchMs + (halo_[0] && halo_[0]->active() && !cfg_.overlap ? kExchangeMs : 0.0);
+  return tab.ms[K] * pts / tab.points + over;
+}
+
+std::vector<int> JacobiSolver::plan_passes(int k) const {
+  std::vector<int> plan;
+  if (k <= 0) return plan;
+  if (ks_ <= 1) return std::vector<int>(k, 1);
+  // pass costs: measured on this share (prepare with calibrate; launches and
+  // serial exchanges included), else the built-in table
+  std::vector<double> cost(ks_ + 1, 0.0);
+  for (int K = 1; K <= ks_; ++K) cost[K] = calibrated_ ? meas_ms_[K] : table_pass_ms(K);
   std::vector<double> best(k + 1, 1e300);
   std::vector<int> pick(k + 1, 0);
   best[0] = 0.0;
   for (int s = 1; s <= k; ++s)
     for (int K = 1; K <= ks_ && K <= s; ++K) {
-      if (tab.ms[K] <= 0) continue;
-      const double c = best[s - K] + tab.ms[K] * scale + over;
+      if (cost[K] <= 0) continue;
+      const double c = best[s - K] + cost[K];
       if (c < best[s]) {
         best[s] = c;
         pick[s] = K;
@@ -383,6 +459,7 @@ void JacobiSolver::run(int k) {
 }
 
 void JacobiSolver::prepare(int k) {
+  if (cfg_.calibrate && !calibrated_) calibrate_costs();
   std::vector<int> kinds;
   for (int K : plan_passes(k))
     if (std::find(kinds.begin(), kinds.end(), K) == kinds.end()) kinds.push_back(K);

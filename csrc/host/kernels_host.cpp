@@ -98,10 +98,34 @@ int gmt_diff_sq(int64_t nx, int64_t ny, const double* a, int64_t lda, const doub
   return 0;
 }
 
+int gmt_abs_max(int64_t nx, int64_t ny, const double* z, int64_t ld, double* out, double*, void*) {
+  double m = 0.0;
+  for (int64_t y = 0; y < ny; ++y)
+    for (int64_t x = 0; x < nx; ++x) m = std::max(m, std::fabs(z[y * ld + x]));
+  out[0] = m;
+  return 0;
+}
+
+// fill mode 5: the same counter-based hash as reduce.hip lattice_uniform
+static double lattice_uniform(int64_t gx, int64_t gy, uint64_t seed) {
+  uint64_t k = (static_cast<uint64_t>(gy + (int64_t(1) << 30)) << 32) ^ static_cast<uint64_t>(gx + (int64_t(1) << 30));
+  k ^= seed;
+  k += 0x9E3779B97F4A7C15ull;
+  k = (k ^ (k >> 30)) * 0xBF58476D1CE4E5B9ull;
+  k = (k ^ (k >> 27)) * 0x94D049BB133111EBull;
+  k ^= k >> 31;
+  return static_cast<double>(k >> 11) * 0x1.0p-53;
+}
+
 int gmt_fill_poly(int mode, int64_t nx, int64_t ny, double x0, double dx, double y0, double dy,
                   double* z, int64_t ld, void*) {
   for (int64_t j = 0; j < ny; ++j)
     for (int64_t i = 0; i < nx; ++i) {
+      if (mode == 5) {
+        z[j * ld + i] = lattice_uniform(static_cast<int64_t>(x0) + i, static_cast<int64_t>(y0) + j,
+                                        static_cast<uint64_t>(dx));
+        continue;
+      }
       if (mode == 4) {  // integer lattice, see reduce.hip (built with -ffp-contract=off)
         const double xl = (x0 + static_cast<double>(i)) * dx, yl = (y0 + static_cast<double>(j)) * dy;
         z[j * ld + i] = xl * xl * xl + yl * yl;
@@ -187,6 +211,7 @@ static int host_xk(int K, int n_rect, const int64_t* rects, const int64_t* dom, 
 }
 
 int gmt_jacobi5tb_supported(int K) { return (K >= 1 && K <= 10) || (K > 10 && K <= GMT_TB_MAX_SWEEPS && K % 2 == 0); }
+int gmt_jacobi5tb_max_sweeps(int exact) { return exact ? 18 : GMT_TB_MAX_SWEEPS; }  // as the gfx950 build
 
 // CPU backend of csrc/kernels/jacobi5tb.hip: same argument checks, reference loops
 int gmt_jacobi5tb(const gmt_tb_opts* o, int n_rect, const int64_t* rects, const int64_t* dom, int mask,

@@ -39,6 +39,11 @@ typedef struct gmt_engine_opts {
   int seg_rows; /* temporal-blocking kernel: output rows per workgroup (0 = auto) */
   int exact;    /* -1 / 0: power-of-two scaled levels when the field bound allows (auto),
                    1: always the exact 1/4-per-level form */
+  int init;     /* initial field: 0 = x^3 + y^2 on the global lattice, 1 = uniform [0, 1)
+                   random (a hash of the global lattice point and `seed`) */
+  int calibrate; /* 1: prepare() times every fused-pass size on the real share and the
+                    planner uses those costs instead of the built-in table */
+  int64_t seed;
 } gmt_engine_opts;
 /* id: 128 bytes (RCCL unique id / control id) or NULL (local); NULL on invalid options */
 void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank, int world,
@@ -58,6 +63,10 @@ int gmt_engine_jacobi_plan(void* h, int steps, int* out, int max);
  * initial field (first-launch costs stay out of a timed run). */
 int gmt_engine_jacobi_prepare(void* h, int steps);
 int gmt_engine_jacobi_copy_interior(void* h, double* host);
+/* what: 0 = max |u| of the initial field (all ranks; drives the exactness
+ * guard), 1 = measured ms of a full tsteps pass (0 before a calibrated
+ * prepare), 2 = the built-in cost table's ms for that pass on this share */
+double gmt_engine_jacobi_stat(void* h, int what);
 const char* gmt_engine_backend(void);
 
 /* A bare communicator on the same transports, for device collectives outside
@@ -72,9 +81,10 @@ void gmt_engine_comm_destroy(void* h);
 /* The reference's halo-exchange benchmark (mpi_stencil2d_gt test_deriv for
  * dim 0 and dim 1, then test_sum), n_local x n_other per rank, 2 ghosts,
  * non-periodic 1-D slabs, on the RCCL or IPC transport (local for world == 1).
- * out[14]: per dim d (6 values at 6*d): exchange seconds median, mean, min,
+ * out[16]: per dim d (6 values at 6*d): exchange seconds median, mean, min,
  * max, bytes sent per exchange, this rank's err_norm; out[12] = all-reduce
- * (1024 doubles in place) median seconds, out[13] = its max relative error. */
+ * (1024 doubles in place) median seconds, out[13] = its max relative error;
+ * out[14 + d] = norm of the analytic derivative over this rank's output. */
 int gmt_engine_deriv_bench(int64_t n_local, int64_t n_other, int n_iter, int n_warmup, int rank,
                            int world, int transport, const void* ccl_id, double* out);
 

@@ -61,8 +61,19 @@ struct JacobiConfig {
   int wg_waves = 0;                              // gmt_tb_opts.wg_waves: strips per workgroup (0 = auto)
   int seg_rows = 0;                              // gmt_tb_opts.seg_rows (0 = auto)
   // -1 / 0: power-of-two scaled levels when max|u| * 4^K stays finite (the
-  // initial field bounds every later one: Jacobi averages), 1: always exact
+  // initial field bounds every later one: Jacobi averages; max|u| is
+  // measured on the device at start-up), 1: always exact
   int exact = -1;
+  // initial field (interior and Dirichlet ring): 0 = x^3 + y^2 on the global
+  // lattice (gmt_fill_poly mode 4), 1 = uniform [0, 1) random values, a hash
+  // of the global lattice point and `seed` (mode 5) — both independent of the
+  // decomposition, so every process grid computes the same numbers
+  int init = 0;
+  uint64_t seed = 0;
+  // prepare() times one pass of every fused-pass size on this rank's real
+  // share (max over ranks) and plan_passes uses those costs instead of the
+  // built-in table (measured on one box for one kernel revision)
+  bool calibrate = false;
 };
 
 class JacobiSolver {
@@ -107,6 +118,11 @@ class JacobiSolver {
   // overlap_auto: seconds per pass measured {overlap, serial} (mean over ranks), 0 if not tuned
   double tuned_overlap_s() const { return tune_s_[0]; }
   double tuned_serial_s() const { return tune_s_[1]; }
+  // ms per fused pass of k sweeps: measured by prepare() with calibrate (0 if
+  // not), and the built-in table's estimate for this share
+  double measured_pass_ms(int k) const { return k >= 0 && k <= GMT_TB_MAX_SWEEPS ? meas_ms_[k] : 0.0; }
+  double table_pass_ms(int k) const;
+  double max_abs_u0() const { return umax_; }
   gmt_stream_t stream() const { return s_; }
 
  private:
@@ -122,6 +138,8 @@ class JacobiSolver {
   void capture_graphs();
   void init_field();
   void autotune_overlap();
+  void calibrate_costs();
+  double measure_max_abs();
   int halo_mask() const;
 
   comm::Transport& t_;
@@ -143,6 +161,9 @@ class JacobiSolver {
   gmt_graph_t graph2_[2] = {nullptr, nullptr};  // fused ks_-sweep block, per parity
   int parity_ = 0;  // buf_[parity_] holds the current u
   double tune_s_[2] = {0.0, 0.0};
+  double meas_ms_[GMT_TB_MAX_SWEEPS + 1] = {};
+  bool calibrated_ = false;
+  double umax_ = 0.0;  // max |u| of the initial field over every rank
 };
 
 // Balanced block split of n over p parts: offset and length of part i.

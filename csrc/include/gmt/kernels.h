@@ -72,12 +72,20 @@ int64_t gmt_diff_sq_workspace(int64_t nx, int64_t ny);
 int gmt_diff_sq(int64_t nx, int64_t ny, const double* a, int64_t lda, const double* b,
                 int64_t ldb, double* out, double* workspace, void* stream);
 
+/* ---- max over the nx x ny region of |z| -> out[0]; workspace of
+ *      gmt_diff_sq_workspace(nx, ny) doubles */
+int gmt_abs_max(int64_t nx, int64_t ny, const double* z, int64_t ld, double* out, double* workspace,
+                void* stream);
+
 /* ---- analytic fill z[y][x] = (x0+i*dx)^3 + (y0+j*dy)^2 over nx x ny (device
  *      side replacement of the reference's host init loops,
  *      mpi_stencil2d_gt.cc:439-497).  mode 0: x^3+y^2 (z), 1: 3x^2 (dz/dx),
  *      2: 2y (dz/dy), 3: x (linear ramp; DAXPY inputs), 4: x^3+y^2 on the
  *      integer lattice x = (x0 + i)*dx, y = (y0 + j)*dy with x0, y0 integer
- *      indices, no fma contraction (bitwise reproducible on the host). */
+ *      indices, no fma contraction (bitwise reproducible on the host),
+ *      5: uniform [0, 1) random field, a counter-based hash (splitmix64) of
+ *      the integer lattice point (x0 + i, y0 + j) with seed (uint64) dx —
+ *      decomposition-independent random init. */
 int gmt_fill_poly(int mode, int64_t nx, int64_t ny, double x0, double dx, double y0,
                   double dy, double* z, int64_t ld, void* stream);
 
@@ -105,9 +113,10 @@ int gmt_jacobi5_rects(int n_rect, const int64_t* rects, const double* u, double*
  *      cells belong to a neighbour (they get the intermediate updates); a
  *      clear bit means a fixed Dirichlet ghost.  Cells of `un` outside the
  *      rects are never written.  Sweep counts: 1..10 (one wave per strip)
- *      and even 12..GMT_TB_MAX_SWEEPS (two waves per strip, levels split);
+ *      and even 12..GMT_TB_MAX_SWEEPS (two waves per strip, levels split; K = 22
+ *      and 24 exceed the register file at 2 waves per SIMD and are not built);
  *      gmt_jacobi5tb_supported() says which. */
-#define GMT_TB_MAX_SWEEPS 24
+#define GMT_TB_MAX_SWEEPS 20
 typedef struct gmt_tb_opts {
   int sweeps;   /* K, see gmt_jacobi5tb_supported */
   int wg_waves; /* 256-column strips per workgroup, 1..8 (0 = default; at
@@ -129,6 +138,9 @@ typedef struct gmt_tb_opts {
   uint64_t* signal;
 } gmt_tb_opts;
 int gmt_jacobi5tb_supported(int sweeps);
+/* Largest sweep count whose kernel runs without scratch: GMT_TB_MAX_SWEEPS
+ * for the scaled form, 18 with exact = 1 (planners stay at or below it). */
+int gmt_jacobi5tb_max_sweeps(int exact);
 int gmt_jacobi5tb(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, const int64_t* dom,
                   int halo_mask, const double* u, double* un, int64_t ld, int64_t nrows, void* stream);
 /* The launch gmt_jacobi5tb would make, without launching: info = {workgroups,

@@ -83,6 +83,8 @@ class Transport {
                                          const std::vector<Msg>& sends) = 0;
   // in-place sum over all ranks of a device/managed vector, stream-ordered on s
   virtual void allreduce_sum(double* buf, size_t n, gmt_stream_t s) = 0;
+  // in-place max over all ranks (device/managed vector), stream-ordered on s
+  virtual void allreduce_max(double* buf, size_t n, gmt_stream_t s) = 0;
   // recv = concat over ranks of `bytes_per_rank` from each rank's send;
   // in place when send == recv + rank*bytes_per_rank
   virtual void allgather(const void* send, void* recv, size_t bytes_per_rank, gmt_stream_t s) = 0;

@@ -86,10 +86,6 @@ extern template int dispatch_k<18>(const gmt_tb_opts&, bool, int, const int64_t*
                                       const double*, double*, int64_t, int64_t, hipStream_t, int64_t*);
 extern template int dispatch_k<20>(const gmt_tb_opts&, bool, int, const int64_t*, const int64_t*, int,
                                       const double*, double*, int64_t, int64_t, hipStream_t, int64_t*);
-extern template int dispatch_k<22>(const gmt_tb_opts&, bool, int, const int64_t*, const int64_t*, int,
-                                      const double*, double*, int64_t, int64_t, hipStream_t, int64_t*);
-extern template int dispatch_k<24>(const gmt_tb_opts&, bool, int, const int64_t*, const int64_t*, int,
-                                      const double*, double*, int64_t, int64_t, hipStream_t, int64_t*);
 }  // namespace tb
 }  // namespace gmt
 
@@ -98,6 +94,11 @@ using namespace gmt::tb;
 extern "C" int gmt_jacobi5tb_supported(int sweeps) {
   return (sweeps >= 1 && sweeps <= kMaxK1) || (sweeps > kMaxK1 && sweeps <= GMT_TB_MAX_SWEEPS && sweeps % 2 == 0);
 }
+
+// The exact (1/4 per level) K = 20 kernel needs one VGPR more than the 256 of
+// 2 waves per SIMD and spills 8 B per lane (tests/test_kernel_resources.py):
+// it exists for the kernel-level API, but planners use at most 18 exact sweeps.
+extern "C" int gmt_jacobi5tb_max_sweeps(int exact) { return exact ? 18 : GMT_TB_MAX_SWEEPS; }
 
 namespace {
 int jacobi5tb_run(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, const int64_t* dom, int halo_mask,
@@ -144,8 +145,6 @@ int jacobi5tb_run(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, con
     GMT_TB_CASE(16)
     GMT_TB_CASE(18)
     GMT_TB_CASE(20)
-    GMT_TB_CASE(22)
-    GMT_TB_CASE(24)
 #undef GMT_TB_CASE
     default:
       return static_cast<int>(hipErrorInvalidValue);

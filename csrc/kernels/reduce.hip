@@ -143,6 +143,55 @@ __global__ __launch_bounds__(kBlock) void diffsq_pass1(int64_t nx, int64_t ny,
   if (threadIdx.x == 0) ws[blk] = acc;
 }
 
+// ---------------- max |z| over a 2-D region (the engine's exactness guard on
+// a measured field bound); same tiles and workspace as diff_sq
+__device__ __forceinline__ double block_max(double v) {
+  __shared__ double s_part[kBlock / kWave];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
+  if ((threadIdx.x & (kWave - 1)) == 0) s_part[threadIdx.x / kWave] = v;
+  __syncthreads();
+  double t = s_part[0];
+#pragma unroll
+  for (int i = 1; i < kBlock / kWave; ++i) t = fmax(t, s_part[i]);
+  __syncthreads();
+  return t;
+}
+
+__global__ __launch_bounds__(kBlock) void absmax_pass1(int64_t nx, int64_t ny, const double* __restrict__ z,
+                                                       int64_t ld, double* __restrict__ ws, int64_t nch) {
+  const int64_t blk = blockIdx.x;
+  const int64_t c = blk % nch, y = blk / nch;
+  const int64_t x0 = c * kDiffTile;
+  const int64_t x1 = (x0 + kDiffTile) < nx ? (x0 + kDiffTile) : nx;
+  const double* p = z + y * ld;
+  double m = 0.0;
+  for (int64_t x = x0 + threadIdx.x; x < x1; x += kBlock) m = fmax(m, fabs(p[x]));
+  m = block_max(m);
+  if (threadIdx.x == 0) ws[blk] = m;
+}
+
+__global__ __launch_bounds__(kBlock) void max_all(const double* __restrict__ ws, int64_t n,
+                                                  double* __restrict__ out) {
+  double m = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += kBlock) m = fmax(m, ws[i]);
+  m = block_max(m);
+  if (threadIdx.x == 0) out[0] = m;
+}
+
+// counter-based uniform [0, 1) of an integer lattice point (fill mode 5):
+// splitmix64 of the packed global coordinates — the same value whatever the
+// decomposition, and reproducible on the host (ops/reference.py)
+__device__ __forceinline__ double lattice_uniform(int64_t gx, int64_t gy, uint64_t seed) {
+  uint64_t k = (static_cast<uint64_t>(gy + (int64_t(1) << 30)) << 32) ^ static_cast<uint64_t>(gx + (int64_t(1) << 30));
+  k ^= seed;
+  k += 0x9E3779B97F4A7C15ull;
+  k = (k ^ (k >> 30)) * 0xBF58476D1CE4E5B9ull;
+  k = (k ^ (k >> 27)) * 0x94D049BB133111EBull;
+  k ^= k >> 31;
+  return static_cast<double>(k >> 11) * 0x1.0p-53;
+}
+
 __global__ __launch_bounds__(kBlock) void sum_all(const double* __restrict__ ws, int64_t n,
                                                   double* __restrict__ out) {
   double acc = 0.0;
@@ -161,6 +210,11 @@ __global__ __launch_bounds__(kBlock) void fill_poly_kernel(int mode, int64_t nx,
   if (i >= nx * ny) return;
   const int64_t ix = i % nx, iy = i / nx;
   double v;
+  if (mode == 5) {  // x0, y0: integer global lattice origin; dx: seed
+    z[iy * ld + ix] = lattice_uniform(static_cast<int64_t>(x0) + ix, static_cast<int64_t>(y0) + iy,
+                                      static_cast<uint64_t>(dx));
+    return;
+  }
   if (mode == 4) {
     // integer lattice: x = (x0 + ix) * dx with x0 an integer index (exact
     // sum, one rounding) and no fma contraction, so a NumPy reference
@@ -236,6 +290,17 @@ extern "C" int gmt_diff_sq(int64_t nx, int64_t ny, const double* a, int64_t lda,
   GMT_RET_LAUNCH();
 }
 
+extern "C" int gmt_abs_max(int64_t nx, int64_t ny, const double* z, int64_t ld, double* out, double* ws,
+                           void* stream) {
+  using namespace gmt;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (nx <= 0 || ny <= 0) return static_cast<int>(hipMemsetAsync(out, 0, sizeof(double), s));
+  const int64_t nch = (nx + kDiffTile - 1) / kDiffTile;
+  absmax_pass1<<<grid_1d(nch * ny), kBlock, 0, s>>>(nx, ny, z, ld, ws, nch);
+  max_all<<<1, kBlock, 0, s>>>(ws, nch * ny, out);
+  GMT_RET_LAUNCH();
+}
+
 extern "C" int gmt_fill_poly(int mode, int64_t nx, int64_t ny, double x0, double dx, double y0,
                              double dy, double* z, int64_t ld, void* stream) {
   using namespace gmt;
@@ -254,6 +319,6 @@ extern "C" int gmt_device_synchronize(void) { return static_cast<int>(hipDeviceS
 
 extern "C" const char* gmt_build_info(void) {
   return "libgmt gfx950 (CDNA4) kernels: daxpy, stencil5 1d/2d (dim 1: LDS-DMA pipeline), jacobi5, "
-         "jacobi5tb (1-24 fused sweeps, 4 columns per lane), ipc_exchange, signal_wait, "
-         "copy2d_batched, sum_axis, diff_sq, fill_poly; built " __DATE__ " " __TIME__;
+         "jacobi5tb (1-20 fused sweeps, 4 columns per lane), ipc_exchange, signal_wait, "
+         "copy2d_batched, sum_axis, diff_sq, abs_max, fill_poly; built " __DATE__ " " __TIME__;
 }

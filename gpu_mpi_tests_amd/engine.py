@@ -38,15 +38,17 @@ HIP_ENGINE = os.path.join(_HERE, "_lib", "libgmt_engine.so")
 HOST_ENGINE = os.path.join(_ROOT, "build", "lib-host", "libgmt_engine.so")
 
 LOCAL, RCCL, IPC = 0, 1, 2
+INITS = {"analytic": 0, "random": 1}  # JacobiConfig::init
 _KINDS = {"local": LOCAL, "rccl": RCCL, "ipc": IPC}
-MAX_TSTEPS = 24  # GMT_TB_MAX_SWEEPS (csrc/include/gmt/kernels.h)
+MAX_TSTEPS = 20  # GMT_TB_MAX_SWEEPS (csrc/include/gmt/kernels.h)
 _libs: dict[str, ctypes.CDLL] = {}
 
 
 class EngineOpts(ctypes.Structure):
     """gmt_engine_opts (csrc/include/gmt/engine.h)."""
     _fields_ = [(n, ctypes.c_int) for n in
-                ("periodic", "overlap", "graph", "tsteps", "wg_waves", "seg_rows", "exact")]
+                ("periodic", "overlap", "graph", "tsteps", "wg_waves", "seg_rows", "exact", "init",
+                 "calibrate")] + [("seed", ctypes.c_int64)]
 
 
 class EngineError(RuntimeError):
@@ -100,6 +102,8 @@ def load(device: str = "cuda") -> ctypes.CDLL:
     lib.gmt_engine_jacobi_prepare.restype = c_int
     lib.gmt_engine_jacobi_copy_interior.argtypes = [vp, vp]
     lib.gmt_engine_jacobi_copy_interior.restype = c_int
+    lib.gmt_engine_jacobi_stat.argtypes = [vp, c_int]
+    lib.gmt_engine_jacobi_stat.restype = ctypes.c_double
     lib.gmt_engine_backend.restype = ctypes.c_char_p
     lib.gmt_engine_deriv_bench.argtypes = [i64, i64, c_int, c_int, c_int, c_int, c_int, vp, vp]
     lib.gmt_engine_deriv_bench.restype = c_int
@@ -235,7 +239,7 @@ class NativeJacobi:
                  dims: tuple[int, int] | None = None, periodic: bool = False,
                  overlap: "bool | str" = True, graph: bool = True,
                  tblock: bool | int = False, wg_waves: int = 0, seg_rows: int = 0, exact: int = -1,
-                 transport: str = "auto"):
+                 transport: str = "auto", init: str = "analytic", seed: int = 0, calibrate: bool = False):
         from .parallel.decomp import choose_dims
 
         self.env = env or gdist.get()
@@ -264,9 +268,15 @@ class NativeJacobi:
             raise ValueError(f"tblock: sweeps per fused pass must be 1..{MAX_TSTEPS}, got {ks}")
         # overlap: True / False / "auto" (time both once, every rank keeps the faster)
         auto = overlap == "auto"
+        if init not in INITS:
+            raise ValueError(f"init must be one of {sorted(INITS)}, got {init!r}")
+        if not 0 <= int(seed) < 1 << 53:
+            raise ValueError("seed must be in [0, 2^53)")
+        self.init, self.seed = init, int(seed)
         opts = EngineOpts(periodic=int(bool(periodic)), overlap=2 if auto else int(bool(overlap)),
                           graph=int(bool(graph)), tsteps=ks, wg_waves=int(wg_waves),
-                          seg_rows=int(seg_rows), exact=int(exact))
+                          seg_rows=int(seg_rows), exact=int(exact), init=INITS[init],
+                          calibrate=int(bool(calibrate)), seed=int(seed))
         with _StdoutToStderr():
             self.h = self.lib.gmt_engine_jacobi_create(ny, nx, py, px, e.rank, e.world_size, transport,
                                                        cid, ctypes.byref(opts))
@@ -308,6 +318,18 @@ class NativeJacobi:
     def synchronize(self) -> None:
         self.lib.gmt_engine_jacobi_sync(self.h)
 
+    @property
+    def max_abs_u0(self) -> float:
+        """max |u| of the initial field over all ranks (measured on the device;
+        drives the scaled-level exactness guard)."""
+        return float(self.lib.gmt_engine_jacobi_stat(self.h, 0))
+
+    def pass_cost_ms(self) -> dict:
+        """A full tsteps pass: measured by a calibrated prepare() (0 before) and
+        the built-in table's estimate for this share."""
+        return {"measured": round(float(self.lib.gmt_engine_jacobi_stat(self.h, 1)), 4),
+                "table": round(float(self.lib.gmt_engine_jacobi_stat(self.h, 2)), 4)}
+
     def exchange(self) -> None:
         self.lib.gmt_engine_jacobi_exchange(self.h)
 
@@ -348,7 +370,7 @@ def deriv_bench(n_local: int = 1024, n_other: int = 512 * 1024, n_iter: int = 10
     e = env or gdist.get()
     lib = load("cuda" if e.is_gpu else "cpu")
     transport, cid = _transport_args(lib, e, transport)
-    out = (ctypes.c_double * 14)()
+    out = (ctypes.c_double * 16)()
     with _StdoutToStderr():
         err = lib.gmt_engine_deriv_bench(int(n_local), int(n_other), int(n_iter), int(n_warmup), e.rank,
                                          e.world_size, transport, cid, out)
@@ -359,21 +381,50 @@ def deriv_bench(n_local: int = 1024, n_other: int = 512 * 1024, n_iter: int = 10
     for d in (0, 1):
         o = v[6 * d:6 * d + 6]
         res[f"dim{d}"] = dict(median_s=o[0], mean_s=o[1], min_s=o[2], max_s=o[3], bytes=int(o[4]),
-                              err_norm=o[5])
+                              err_norm=o[5], exact_norm=v[14 + d])
     res["allreduce_median_s"] = v[12]
     res["allreduce_max_rel_err"] = v[13]
     res["transport"] = transport_label({LOCAL: "local", RCCL: "rccl", IPC: "ipc"}[transport], e)
     return res
 
 
-def serial_jacobi(ny: int, nx: int, steps: int, periodic: bool = False) -> np.ndarray:
-    """NumPy reference of exactly the engine's problem (init, boundary, update):
-    bitwise — the engine fills x^3 + y^2 on the same integer lattice with the
-    same operation order (gmt_fill_poly mode 4) and sweeps in the same order."""
+def lattice_uniform(gx: np.ndarray, gy: np.ndarray, seed: int) -> np.ndarray:
+    """uniform [0, 1) of integer lattice points: the same splitmix64 hash as
+    gmt_fill_poly mode 5 (csrc/kernels/reduce.hip lattice_uniform), bitwise."""
+    u64 = np.uint64
+    gx = np.asarray(gx, dtype=np.int64) + (1 << 30)
+    gy = np.asarray(gy, dtype=np.int64) + (1 << 30)
+    k = (gy.astype(u64) << u64(32)) ^ gx.astype(u64)
+    k = k ^ u64(seed)
+    k = k + u64(0x9E3779B97F4A7C15)
+    k = (k ^ (k >> u64(30))) * u64(0xBF58476D1CE4E5B9)
+    k = (k ^ (k >> u64(27))) * u64(0x94D049BB133111EB)
+    k = k ^ (k >> u64(31))
+    return (k >> u64(11)).astype(np.float64) * 2.0 ** -53
+
+
+def initial_field(ny: int, nx: int, init: str = "analytic", seed: int = 0) -> np.ndarray:
+    """The engine's initial field with its ghost ring, (ny+2) x (nx+2),
+    global lattice index -1..n (gmt_fill_poly mode 4 / 5)."""
+    if init == "random":
+        gx = np.arange(-1, nx + 1, dtype=np.int64)[None, :]
+        gy = np.arange(-1, ny + 1, dtype=np.int64)[:, None]
+        return lattice_uniform(np.broadcast_to(gx, (ny + 2, nx + 2)), np.broadcast_to(gy, (ny + 2, nx + 2)), seed)
+    if init != "analytic":
+        raise ValueError(f"init must be analytic or random, got {init!r}")
     h = 1.0 / (max(ny, nx) + 1)
     x = (np.arange(nx + 2, dtype=np.float64) - 1.0) * h
     y = (np.arange(ny + 2, dtype=np.float64) - 1.0) * h
-    u = (x[None, :] * x[None, :] * x[None, :]) + (y[:, None] * y[:, None])
+    return (x[None, :] * x[None, :] * x[None, :]) + (y[:, None] * y[:, None])
+
+
+def serial_jacobi(ny: int, nx: int, steps: int, periodic: bool = False, init: str = "analytic",
+                  seed: int = 0) -> np.ndarray:
+    """NumPy reference of exactly the engine's problem (init, boundary, update):
+    bitwise — the engine fills x^3 + y^2 on the same integer lattice with the
+    same operation order (gmt_fill_poly mode 4), or the same hashed random
+    field (mode 5), and sweeps in the same order."""
+    u = initial_field(ny, nx, init, seed)
     un = u.copy()
     for _ in range(steps):
         if periodic:

@@ -255,12 +255,12 @@ def jacobi5_rects(u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, 
                                       _stream(u)), "gmt_jacobi5_rects")
 
 
-TB_MAX_SWEEPS = 24  # GMT_TB_MAX_SWEEPS (csrc/include/gmt/kernels.h)
+TB_MAX_SWEEPS = 20  # GMT_TB_MAX_SWEEPS (csrc/include/gmt/kernels.h)
 
 
 def tb_supported(k: int) -> bool:
     """Sweep counts the temporal-blocking kernel is built for: 1..10 (one wave
-    per strip) and even 12..24 (two waves per strip, levels split)."""
+    per strip) and even 12..20 (two waves per strip, levels split)."""
     return 1 <= k <= 10 or (10 < k <= TB_MAX_SWEEPS and k % 2 == 0)
 
 

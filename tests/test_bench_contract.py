@@ -80,6 +80,7 @@ def test_bench_two_ranks_torchrun_cpu(transport):
     assert rec["ref_halo_dim0_us"] > 0 and rec["ref_halo_dim1_us"] > 0
     assert rec["ref_halo_bytes_per_rank"] == 2 * 2 * 300 * 8 // 2  # edge ranks: one neighbour
     assert rec["ref_halo_dim0_err_norm"] < 1e-6 and rec["ref_halo_dim1_err_norm"] < 1e-6
+    assert rec["ref_halo_dim0_rel_err"] < 1e-9 and rec["ref_halo_dim1_rel_err"] < 1e-9
     assert rec["ref_allreduce_1024_us"] > 0
 
 

@@ -104,3 +104,70 @@ def test_native_engine_multirank(transport, np_, ny, nx, steps, periodic, overla
     assert r["resid_same"]
     if dims:
         assert r["dims"] == [int(v) for v in dims.split("x")]
+
+
+CODE_INIT = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+import numpy as np
+from gpu_mpi_tests_amd import engine
+from gpu_mpi_tests_amd.parallel import dist as gd
+env = gd.init(device="cpu")
+e = engine.NativeJacobi({ny}, {nx}, env, periodic={periodic}, overlap=True, tblock={tblock}, init={init!r},
+                        seed={seed}, calibrate=True)
+e.prepare({steps})  # calibration: one timed pass of every size, then the plan
+plan = e.plan({steps})
+e.run({steps}); e.synchronize()
+ref = engine.serial_jacobi({ny}, {nx}, {steps}, {periodic}, init={init!r}, seed={seed})
+print(json.dumps(dict(diff=float(np.abs(e.interior() - ref).max()), umax=e.max_abs_u0, plan=plan,
+                      cost=e.pass_cost_ms(), exact=e.exact, tsteps=e.tsteps)))
+e.close()
+"""
+
+
+@pytest.mark.parametrize("init,seed", [("random", 0), ("random", 987654321), ("analytic", 0)])
+@pytest.mark.parametrize("periodic", [False, True])
+def test_native_engine_init_and_calibration(init, seed, periodic):
+    """Random init (gmt_fill_poly mode 5: a hash of the global lattice point)
+    is bitwise the NumPy reference's; the exactness guard runs on the
+    measured max|u|; a calibrated prepare() times every pass size and the
+    plan covers the steps."""
+    ensure_host_build()
+    code = CODE_INIT.format(root=ROOT, ny=45, nx=70, steps=23, periodic=periodic, tblock=8, init=init, seed=seed)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES=""))
+    assert p.returncode == 0, p.stdout + p.stderr
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["diff"] == 0.0, r
+    assert sum(r["plan"]) == 23 and max(r["plan"]) <= 8
+    assert r["cost"]["measured"] > 0 and r["cost"]["table"] > 0
+    if init == "random":
+        assert 0.9 < r["umax"] < 1.0  # uniform [0, 1) over ~3400 cells
+    else:
+        assert 1.0 < r["umax"] < 2.2  # x^3 + y^2 on the lattice, below 2 + 3h
+    assert r["exact"] is False  # max|u| * 4^8 is far from overflow
+
+
+def test_lattice_uniform_matches_fill_mode5():
+    """ops.fill_poly mode 5 on the host backend vs the NumPy hash (the engine's
+    random init): same bits, decomposition-independent."""
+    ensure_host_build()
+    code = r"""
+import sys, ctypes, json
+sys.path.insert(0, {root!r})
+import numpy as np
+from gpu_mpi_tests_amd import engine
+lib = engine.load("cpu")
+L = ctypes.CDLL(lib._name.replace("libgmt_engine.so", "libgmt.so"))
+L.gmt_fill_poly.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
+                            ctypes.c_double, ctypes.c_double, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+z = np.zeros((6, 9))
+L.gmt_fill_poly(5, 9, 6, -3.0, 12345.0, 7.0, 0.0, z.ctypes.data, 9, None)
+gx = np.arange(-3, 6)[None, :].repeat(6, 0); gy = np.arange(7, 13)[:, None].repeat(9, 1)
+print(json.dumps(dict(same=bool((z == engine.lattice_uniform(gx, gy, 12345)).all()), lo=float(z.min()), hi=float(z.max()))))
+""".format(root=ROOT)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES=""))
+    assert p.returncode == 0, p.stdout + p.stderr
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["same"] and 0.0 <= r["lo"] and r["hi"] < 1.0

@@ -61,7 +61,7 @@ def test_tb_bitwise(k, ny, nx, mask):
     _check(k, u, dom, mask)
 
 
-@pytest.mark.parametrize("k", [1, 5, 10, 12, 20, 24])
+@pytest.mark.parametrize("k", [1, 5, 10, 12, 18, 20])
 @pytest.mark.parametrize("nx", [140, 141, 142, 143, 300, 301, 302])
 @pytest.mark.parametrize("xo", [24, 25, 26])
 def test_tb_widths_and_offsets(k, nx, xo):
@@ -71,7 +71,7 @@ def test_tb_widths_and_offsets(k, nx, xo):
     _check(k, u, dom, 10)
 
 
-@pytest.mark.parametrize("k", [2, 7, 10, 14, 24])
+@pytest.mark.parametrize("k", [2, 7, 10, 14, 20])
 @pytest.mark.parametrize("wg", [1, 2, 3, 4, 8])
 def test_tb_workgroup_shapes(k, wg):
     """Strips per workgroup, including workgroups whose last strips are idle
@@ -88,14 +88,14 @@ def test_tb_segments(k, seg):
     _check(k, u, dom, 5, seg_rows=seg)
 
 
-@pytest.mark.parametrize("k", [2, 3, 8, 14, 24])
+@pytest.mark.parametrize("k", [2, 3, 8, 14, 20])
 @pytest.mark.parametrize("mask", [0, 15, 3, 12])
 def test_tb_exact(k, mask):
     u, dom = _field(k, 75, 333, seed=93)
     _check(k, u, dom, mask, exact=True)
 
 
-@pytest.mark.parametrize("k", [8, 16, 24])
+@pytest.mark.parametrize("k", [8, 16, 20])
 def test_tb_extreme_magnitudes(k):
     """Scaled levels (4^p u_p) stay bitwise for tiny normal magnitudes; the exact
     form covers magnitudes where 4^k |u| would overflow."""

@@ -67,7 +67,13 @@ def test_bench_oversubscribed_ipc(n, extra, name):
     assert rec["config"]["transport"] == "ipc", rec["config"]
     assert rec["ranks_per_gpu"] == n
     assert rec["check_max_diff"] == 0.0
-    assert rec["ref_halo_dim0_err_norm"] < 1e-6 and rec["ref_halo_dim1_err_norm"] < 1e-6
+    # err_norm of the reference's own benchmark at its default per-rank shape
+    # (1024 x 512Ki, x^3 + y^2 at spacing 8/n_global: |z| reaches ~4e6 in dim
+    # 0 and ~9e9 in dim 1): the 4th-order stencil is exact for cubics, so it
+    # is round-off summed over 5e8 points (measured 4.9e-4 / 0.77), tiny
+    # against the analytic derivative's norm; one missing ghost cell alone
+    # would add ~|z| / (12 h) >= 1e8 (mpi_stencil2d_gt.cc:555-570)
+    assert rec["ref_halo_dim0_rel_err"] < 1e-4 and rec["ref_halo_dim1_rel_err"] < 1e-4, rec
     assert rec["ref_halo_config"].endswith("ipc")
     assert rec["daxpy_allsum_rel_err"] <= 1e-9 and rec["daxpy_allreduce_kind"] == "ipc"
     assert rec["value"] > 0 and rec["halo_exchange_us"] > 0
