@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-kernel table from a scripts/gpu_r02_pmc.sh output directory.
+"""Per-kernel table from a scripts/experiments/gpu_r02_pmc.sh output directory.
 
 Joins the kernel trace (duration, VGPR/SGPR/scratch per dispatch) with every
 --pmc pass (counter means per dispatch, grouped by kernel name) and derives:
