@@ -15,7 +15,7 @@
 //   --no-overlap --graph --periodic --warmup=W
 //   --tblock                temporal blocking (gmt_jacobi5tb): K sweeps per memory pass
 //                           and per (K-wide) halo exchange
-//   --tsteps=K              sweeps per fused pass with --tblock (2-24; default 2; odd
+//   --tsteps=K              sweeps per fused pass with --tblock (2-20; default 2; odd
 //                           counts above 10 round down)
 //   --wg-strips=N --seg-rows=L   gmt_tb_opts launch shape (0 = default)
 //   --halo-iters=K          K blocking halo exchanges -> latency line

@@ -406,13 +406,20 @@ constexpr double kExchangeMs = 0.035;  // a halo exchange not hidden by the over
 
 double JacobiSolver::table_pass_ms(int K) const {
   if (K < 1 || K > GMT_TB_MAX_SWEEPS) return 0.0;
-  // the table measured on the closer domain size, scaled to this rank's
-  const double pts = static_cast<double>(nx_) * static_cast<double>(ny_);
+  // The table measured on the closer domain size, scaled to the LARGEST
+  // share of the job (ceil of the global extents over the grid): every rank
+  // must compute the same plan — ranks whose shares differ by a row would
+  // otherwise pick different pass sequences and exchange at different sweeps
+  // — and the job's pass takes as long as its largest share.
+  const JacobiConfig& c = cfg_;
+  const double pts = static_cast<double>((c.nx_global + c.px - 1) / c.px) *
+                     static_cast<double>((c.ny_global + c.py - 1) / c.py);
   const PassCosts& tab = std::fabs(std::log(pts / kCostLarge.points)) < std::fabs(std::log(pts / kCostSmall.points))
                              ? kCostLarge
                              : kCostSmall;
   if (tab.ms[K] <= 0) return 0.0;
-  const double over = kLaunchMs + (halo_[0] && halo_[0]->active() && !cfg_.overlap ? kExchangeMs : 0.0);
+  const bool exchanges = t_.size() > 1 || c.periodic;  // the same on every rank
+  const double over = kLaunchMs + (exchanges && !c.overlap ? kExchangeMs : 0.0);
   return tab.ms[K] * pts / tab.points + over;
 }
 
@@ -421,7 +428,8 @@ std::vector<int> JacobiSolver::plan_passes(int k) const {
   if (k <= 0) return plan;
   if (ks_ <= 1) return std::vector<int>(k, 1);
   // pass costs: measured on this share (prepare with calibrate; launches and
-  // serial exchanges included), else the built-in table
+  // serial exchanges included; max over ranks), else the built-in table for
+  // the job's largest share — the same costs, hence the same plan, on every rank
   std::vector<double> cost(ks_ + 1, 0.0);
   for (int K = 1; K <= ks_; ++K) cost[K] = calibrated_ ? meas_ms_[K] : table_pass_ms(K);
   std::vector<double> best(k + 1, 1e300);

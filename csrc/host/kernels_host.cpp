@@ -98,6 +98,14 @@ int gmt_diff_sq(int64_t nx, int64_t ny, const double* a, int64_t lda, const doub
   return 0;
 }
 
+int64_t gmt_sum_workspace(int64_t) { return 1; }
+int gmt_sum(int64_t n, const double* x, double* out, double*, void*) {
+  double s = 0.0;
+  for (int64_t i = 0; i < n; ++i) s += x[i];
+  out[0] = s;
+  return 0;
+}
+
 int gmt_abs_max(int64_t nx, int64_t ny, const double* z, int64_t ld, double* out, double*, void*) {
   double m = 0.0;
   for (int64_t y = 0; y < ny; ++y)

@@ -72,6 +72,12 @@ int64_t gmt_diff_sq_workspace(int64_t nx, int64_t ny);
 int gmt_diff_sq(int64_t nx, int64_t ny, const double* a, int64_t lda, const double* b,
                 int64_t ldb, double* out, double* workspace, void* stream);
 
+/* ---- out[0] = sum of x[0..n) (one HBM pass, deterministic order);
+ *      workspace of gmt_sum_workspace(n) doubles.  The DAXPY partial sums
+ *      (reference: host loops, mpi_daxpy_nvtx.cc:251-268) */
+int64_t gmt_sum_workspace(int64_t n);
+int gmt_sum(int64_t n, const double* x, double* out, double* workspace, void* stream);
+
 /* ---- max over the nx x ny region of |z| -> out[0]; workspace of
  *      gmt_diff_sq_workspace(nx, ny) doubles */
 int gmt_abs_max(int64_t nx, int64_t ny, const double* z, int64_t ld, double* out, double* workspace,

@@ -551,18 +551,22 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     if (e != hipSuccess) return static_cast<int>(e);
   }
   // resident workgroups on the device for this shape (registers, LDS);
-  // queried once per kernel and strips-per-workgroup (an idempotent cache)
-  static std::atomic<int> resident[kMaxThreads / kWave + 1] = {};
-  int per_cu = resident[a.nw].load(std::memory_order_relaxed);
+  // queried once per device, kernel and strips-per-workgroup (an idempotent
+  // cache: a process driving several devices keeps one entry per device)
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> resident[kMaxDev][kMaxThreads / kWave + 1] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::atomic<int>* slot = dev >= 0 && dev < kMaxDev ? &resident[dev][a.nw] : nullptr;
+  int per_cu = slot ? slot->load(std::memory_order_relaxed) : 0;
   if (per_cu <= 0) {
-    int occ = 0, dev = 0, cus = 256;
+    int occ = 0, cus = 256;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE>),
                                                      a.nw * G * kWave, smem) != hipSuccess || occ < 1)
       occ = 1;
-    (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     per_cu = occ * cus;
-    resident[a.nw].store(per_cu, std::memory_order_relaxed);
+    if (slot) slot->store(per_cu, std::memory_order_relaxed);
   }
   const int sig_rects = o.signal_rects;  // non-empty rects (checked): the same indices after the compaction
   const SegPlan sp = plan_segments<K>(a, o.seg_rows, lmax, per_cu, sig_rects);

@@ -143,6 +143,34 @@ __global__ __launch_bounds__(kBlock) void diffsq_pass1(int64_t nx, int64_t ny,
   if (threadIdx.x == 0) ws[blk] = acc;
 }
 
+// ---------------- sum of a contiguous vector (the DAXPY partial sums of
+// mpi_daxpy_nvtx.cc:251-268, on the device): a fixed grid streams the
+// vector with 16-B loads, one partial per workgroup, then one workgroup
+// adds the partials in order — deterministic, one pass over HBM
+constexpr int64_t kSumBlocks = 2048;  // 8 per CU: enough bytes in flight for HBM
+
+__global__ __launch_bounds__(kBlock) void sum1d_pass1(int64_t n, const double* __restrict__ x,
+                                                      double* __restrict__ ws, bool vec) {
+  const int64_t nb = gridDim.x, b = blockIdx.x;
+  double acc = 0.0;
+  if (vec) {
+    d2 a0 = {0.0, 0.0}, a1 = {0.0, 0.0};
+    const int64_t n2 = n / 2, stride = nb * kBlock;
+    int64_t i = b * kBlock + threadIdx.x;
+    for (; i + stride < n2; i += 2 * stride) {
+      a0 += ld2_nt(x + 2 * i);
+      a1 += ld2_nt(x + 2 * (i + stride));
+    }
+    if (i < n2) a0 += ld2_nt(x + 2 * i);
+    acc = (a0.x + a0.y) + (a1.x + a1.y);
+    if ((n & 1) && b == 0 && threadIdx.x == 0) acc += x[n - 1];
+  } else {
+    for (int64_t i = b * kBlock + threadIdx.x; i < n; i += nb * kBlock) acc += x[i];
+  }
+  acc = block_sum(acc);
+  if (threadIdx.x == 0) ws[b] = acc;
+}
+
 // ---------------- max |z| over a 2-D region (the engine's exactness guard on
 // a measured field bound); same tiles and workspace as diff_sq
 __device__ __forceinline__ double block_max(double v) {
@@ -290,6 +318,22 @@ extern "C" int gmt_diff_sq(int64_t nx, int64_t ny, const double* a, int64_t lda,
   GMT_RET_LAUNCH();
 }
 
+extern "C" int64_t gmt_sum_workspace(int64_t n) {
+  using namespace gmt;
+  const int64_t nb = (n + 2 * kBlock - 1) / (2 * kBlock);
+  return nb < 1 ? 1 : (nb < kSumBlocks ? nb : kSumBlocks);
+}
+
+extern "C" int gmt_sum(int64_t n, const double* x, double* out, double* ws, void* stream) {
+  using namespace gmt;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (n <= 0) return static_cast<int>(hipMemsetAsync(out, 0, sizeof(double), s));
+  const int64_t nb = gmt_sum_workspace(n);
+  sum1d_pass1<<<grid_1d(nb), kBlock, 0, s>>>(n, x, ws, aligned16(x));
+  sum_all<<<1, kBlock, 0, s>>>(ws, nb, out);
+  GMT_RET_LAUNCH();
+}
+
 extern "C" int gmt_abs_max(int64_t nx, int64_t ny, const double* z, int64_t ld, double* out, double* ws,
                            void* stream) {
   using namespace gmt;
@@ -320,5 +364,5 @@ extern "C" int gmt_device_synchronize(void) { return static_cast<int>(hipDeviceS
 extern "C" const char* gmt_build_info(void) {
   return "libgmt gfx950 (CDNA4) kernels: daxpy, stencil5 1d/2d (dim 1: LDS-DMA pipeline), jacobi5, "
          "jacobi5tb (1-20 fused sweeps, 4 columns per lane), ipc_exchange, signal_wait, "
-         "copy2d_batched, sum_axis, diff_sq, abs_max, fill_poly; built " __DATE__ " " __TIME__;
+         "copy2d_batched, sum_axis, sum, diff_sq, abs_max, fill_poly; built " __DATE__ " " __TIME__;
 }

@@ -63,6 +63,9 @@ _SIGS = {
     "gmt_sum_axis_workspace": (c_i64, [c_int, c_i64, c_i64]),
     "gmt_sum_axis": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "gmt_diff_sq_workspace": (c_i64, [c_i64, c_i64]),
+    "gmt_sum_workspace": (c_i64, [c_i64]),
+    "gmt_sum": (c_int, [c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "gmt_abs_max": (c_int, [c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "gmt_diff_sq": (c_int, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "gmt_fill_poly": (c_int, [c_int, c_i64, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_vp, c_i64, c_vp]),
     "gmt_jacobi_resid_workspace": (c_i64, [c_i64, c_i64]),

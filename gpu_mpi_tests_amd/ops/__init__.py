@@ -7,6 +7,7 @@ and the BASELINE 5-point Jacobi ``jacobi5`` / ``jacobi5_rects`` (single sweep)
 and ``jacobi5tb`` (K fused sweeps per memory pass).
 """
 from .kernels import (  # noqa: F401
+    abs_max,
     copy2d_batched,
     daxpy,
     diff_norm,
@@ -20,5 +21,6 @@ from .kernels import (  # noqa: F401
     stencil5_1d,
     stencil5_2d,
     sum_axis,
+    vsum,
 )
 from .reference import DERIV5  # noqa: F401

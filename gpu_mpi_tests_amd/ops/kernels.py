@@ -165,6 +165,39 @@ def sum_axis(z: torch.Tensor, keep_dim: int, out: torch.Tensor | None = None) ->
     return out
 
 
+def vsum(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Sum of a contiguous fp64 vector into a 1-element tensor (one HBM pass,
+    deterministic order): the DAXPY partial sums, mpi_daxpy_nvtx.cc:251-268."""
+    if x.dtype != torch.float64 or not x.is_contiguous():
+        raise ValueError("vsum: contiguous float64 vector required")
+    if out is None:
+        out = torch.empty(1, dtype=torch.float64, device=x.device)
+    if not _is_dev(x):
+        out.copy_(x.sum().reshape(1))
+        return out
+    L = _native.lib()
+    n = x.numel()
+    ws = torch.empty(max(1, L.gmt_sum_workspace(n)), dtype=torch.float64, device=x.device)
+    _native.check(L.gmt_sum(n, x.data_ptr(), out.data_ptr(), ws.data_ptr(), _stream(x)), "gmt_sum")
+    return out
+
+
+def abs_max(z: torch.Tensor) -> torch.Tensor:
+    """0-d tensor max |z| over a 2-D (or 1-D) fp64 tensor with unit x-stride."""
+    if z.dim() == 1:
+        z = z.view(1, -1)
+    _check2d(z, "abs_max.z")
+    if not _is_dev(z):
+        return z.abs().max()
+    ny, nx = z.shape
+    L = _native.lib()
+    ws = torch.empty(max(1, L.gmt_diff_sq_workspace(nx, ny)), dtype=torch.float64, device=z.device)
+    out = torch.empty((), dtype=torch.float64, device=z.device)
+    _native.check(L.gmt_abs_max(nx, ny, z.data_ptr(), z.stride(0), out.data_ptr(), ws.data_ptr(), _stream(z)),
+                  "gmt_abs_max")
+    return out
+
+
 def diff_sq(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """0-d tensor ``sum((a-b)^2)`` (un-rooted so it can be all-reduced).  K10/K12."""
     if a.dim() == 1:

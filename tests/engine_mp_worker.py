@@ -18,9 +18,9 @@ def main():
     ny, nx, steps, periodic, overlap, tblock = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]),
                                                 sys.argv[4] == "1", sys.argv[5] == "1", int(sys.argv[6]))
     dims = tuple(int(v) for v in sys.argv[7].split("x")) if len(sys.argv) > 7 else None
-    env = gd.init(device="cpu")
-    e = engine.NativeJacobi(ny, nx, env, dims=dims, periodic=periodic, overlap=overlap, graph=True,
-                            tblock=tblock)
+    env = gd.init(device=os.environ.get("GMT_TEST_DEVICE", "cpu"))
+    e = engine.NativeJacobi(ny, nx, env, dims=dims, periodic=periodic, overlap=overlap,
+                            graph=os.environ.get("GMT_TEST_GRAPH", "1") == "1", tblock=tblock)
     e.run(steps)
     e.synchronize()
     e.exchange()  # a blocking exchange on its own (bench.py's latency probe)
@@ -35,7 +35,9 @@ def main():
         for oy, ox, a in parts:
             full[oy:oy + a.shape[0], ox:ox + a.shape[1]] = a
         ref = engine.serial_jacobi(ny, nx, steps, periodic)
-        print(json.dumps(dict(diff=float(np.abs(full - ref).max()), transport=e.transport,
+        bad = np.argwhere(np.abs(full - ref) > 0)
+        print(json.dumps(dict(diff=float(np.abs(full - ref).max()), transport=e.transport, nbad=int(len(bad)),
+                              first_bad=bad[:4].tolist(), overlap=e.overlap, band_first=e.band_first,
                               dims=[e.py, e.px], tsteps=e.tsteps, halo=e.halo_bytes,
                               resid_same=len(set(resids)) == 1)), flush=True)
     e.close()

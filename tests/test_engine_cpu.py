@@ -82,6 +82,9 @@ def test_native_engine_k_sweeps(k):
     (4, 60, 64, 25, False, True, 12, "2x2"),
     (3, 50, 90, 11, True, False, 8, "1x3"),
     (6, 66, 70, 10, True, True, 6, "2x3"),
+    # uneven shares (156 / 157 rows): every rank must plan the same passes
+    # ([20, 16, 7] for 43 sweeps) — the plan once followed each rank's own share
+    (2, 313, 1695, 43, False, False, 20, "2x1"),
 ])
 def test_native_engine_multirank(transport, np_, ny, nx, steps, periodic, overlap, tblock, dims):
     """The multi-GPU data plane of bench.py (native engine, RCCL grouped

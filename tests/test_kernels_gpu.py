@@ -249,3 +249,22 @@ def test_stream_semantics():
         ops.daxpy(2.0, x, y)
     s.synchronize()
     assert torch.equal(y, exp)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 255, 512, 513, 4097, 1 << 20, (1 << 22) + 7])
+def test_vsum_matches_fp64_reference(n):
+    """gmt_sum (the DAXPY partial sums) vs a plain PyTorch fp64 sum."""
+    x = torch.rand(n, dtype=torch.float64, device=DEV) - 0.25
+    got = float(ops.vsum(x))
+    ref = float(x.double().cpu().sum())
+    assert abs(got - ref) <= 1e-12 * max(1.0, float(x.abs().sum()))
+    # unaligned start: the scalar path
+    if n > 1:
+        got2 = float(ops.vsum(x[1:]))
+        assert abs(got2 - float(x[1:].cpu().sum())) <= 1e-12 * max(1.0, float(x.abs().sum()))
+
+
+@pytest.mark.parametrize("ny,nx", [(1, 1), (3, 7), (257, 4099), (1000, 1024)])
+def test_abs_max_matches_reference(ny, nx):
+    z = torch.randn(ny, nx + 3, dtype=torch.float64, device=DEV)[:, 1:nx + 1]
+    assert float(ops.abs_max(z)) == float(z.abs().max())
