@@ -54,7 +54,7 @@ def test_engine_periodic_matches_serial(env, ny, nx, steps, tblock, graph):
 
 
 @pytest.mark.parametrize("ny,nx,steps,tblock,wg", [(260, 1100, 13, 4, 1), (300, 1500, 45, 12, 0),
-                                                  (400, 1300, 47, 20, 0), (333, 1501, 61, 24, 0)])
+                                                  (400, 1300, 47, 20, 0), (333, 1501, 61, 18, 0)])
 @pytest.mark.parametrize("graph", [False, True])
 def test_engine_band_first_matches_serial(env, ny, nx, steps, tblock, wg, graph):
     """Overlapped fused passes run band-first (csrc/engine/jacobi.cpp
