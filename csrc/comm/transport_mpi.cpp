@@ -123,6 +123,10 @@ class MpiTransport : public Transport {
 //          D2H, the wire and H2D of different chunks overlap.
 // Receive staging is double-buffered across exchanges: the next exchange's
 // receives never wait for this one's H2D copies to drain.
+// Device -> host leg (GMT_HOST_STAGE): "kernel" (default) — one gmt_stage_copy
+// launch writes every chunk into coherent pinned memory with the CUs and
+// raises a per-chunk host flag (csrc/kernels/stage.hip); "sdma" — one
+// hipMemcpyAsync and one event per chunk (round 2).
 class MpiHostExchange : public Exchange {
  public:
   // pipeline chunk: 1 MiB (GMT_HOST_CHUNK_KB overrides, for measurement);
@@ -134,12 +138,17 @@ class MpiHostExchange : public Exchange {
     return kb > 0 ? static_cast<size_t>(kb) << 10 : size_t(1) << 20;
   }
 
+  static bool kernel_staging() {
+    const char* e = std::getenv("GMT_HOST_STAGE");
+    return !(e && std::strcmp(e, "sdma") == 0);
+  }
+
   MpiHostExchange(MPI_Comm c, size_t chunk, std::vector<Msg> r, std::vector<Msg> s)
-      : c_(c), recvs_(std::move(r)), sends_(std::move(s)) {
+      : c_(c), recvs_(std::move(r)), sends_(std::move(s)), kernel_(kernel_staging()) {
     const size_t kChunk = chunk;
     for (int set = 0; set < 2; ++set)
       for (auto& m : recvs_) rstage_[set].emplace_back(m.bytes, GMT_SPACE_PINNED);
-    for (auto& m : sends_) sstage_.emplace_back(m.bytes, GMT_SPACE_PINNED);
+    for (auto& m : sends_) sstage_.emplace_back(m.bytes, kernel_ ? GMT_SPACE_PINNED_COHERENT : GMT_SPACE_PINNED);
     for (size_t i = 0; i < sends_.size(); ++i)
       for (size_t off = 0; off < sends_[i].bytes || off == 0; off += kChunk) {
         schunks_.push_back({i, off, std::min(kChunk, sends_[i].bytes - off)});
@@ -150,8 +159,25 @@ class MpiHostExchange : public Exchange {
         rchunks_.push_back({i, off, std::min(kChunk, recvs_[i].bytes - off)});
         if (recvs_[i].bytes == 0) break;
       }
-    events_.resize(schunks_.size(), nullptr);
-    for (auto& e : events_) GMT_CHECK("event", gmt_rt_event_create(&e, 0));
+    if (kernel_ && !schunks_.empty()) {
+      const size_t n = schunks_.size();
+      std::vector<gmt_stage_chunk> t(n);
+      for (size_t k = 0; k < n; ++k) {
+        const Chunk& ch = schunks_[k];
+        t[k] = {static_cast<const char*>(sends_[ch.msg].buf) + ch.off, sstage_[ch.msg].data() + ch.off,
+                static_cast<int64_t>(ch.len)};
+      }
+      table_ = Buffer<gmt_stage_chunk>(n, GMT_SPACE_DEVICE);
+      GMT_CHECK("stage table", gmt_rt_memcpy(table_.data(), t.data(), n * sizeof(gmt_stage_chunk)));
+      counters_ = Buffer<unsigned>(n, GMT_SPACE_DEVICE);
+      GMT_CHECK("stage counters", gmt_rt_memset_async(counters_.data(), 0, counters_.bytes(), nullptr));
+      GMT_CHECK("stage counters", gmt_rt_stream_synchronize(nullptr));
+      flags_ = Buffer<uint64_t>(n, GMT_SPACE_PINNED_COHERENT);
+      for (size_t k = 0; k < n; ++k) flags_.data()[k] = 0;
+    } else {
+      events_.resize(schunks_.size(), nullptr);
+      for (auto& e : events_) GMT_CHECK("event", gmt_rt_event_create(&e, 0));
+    }
     for (auto& e : h2d_done_) GMT_CHECK("event", gmt_rt_event_create(&e, 0));
   }
   ~MpiHostExchange() override {
@@ -167,6 +193,13 @@ class MpiHostExchange : public Exchange {
       const Chunk& ch = rchunks_[k];
       const Msg& m = recvs_[ch.msg];
       irecv(rstage_[cur_][ch.msg].data() + ch.off, ch.len, m.peer, m.tag, c_, &rreqs_[k]);
+    }
+    if (kernel_) {
+      // 1 MiB chunks: 32 workgroups each (2 x 16 B in flight per lane)
+      ++epoch_;
+      GMT_CHECK("stage D2H", gmt_stage_copy(static_cast<int>(schunks_.size()), table_.data(), counters_.data(),
+                                            flags_.data(), epoch_, kStageWgs, s));
+      return;
     }
     for (size_t k = 0; k < schunks_.size(); ++k) {
       const Chunk& ch = schunks_[k];
@@ -197,9 +230,14 @@ class MpiHostExchange : public Exchange {
       sreqs.emplace_back();
       isend(sstage_[ch.msg].data() + ch.off, ch.len, m.peer, m.tag, c_, &sreqs.back());
     };
+    // chunk k of the send staging is complete (kernel: its host flag; sdma: its event)
+    auto staged = [&](size_t k) {
+      return kernel_ ? __atomic_load_n(flags_.data() + k, __ATOMIC_ACQUIRE) >= epoch_
+                     : gmt_rt_event_query(events_[k]) == 0;
+    };
     while (next < schunks_.size() || pending > 0) {
       bool progress = false;
-      while (next < schunks_.size() && gmt_rt_event_query(events_[next]) == 0) {
+      while (next < schunks_.size() && staged(next)) {
         send(next++);
         progress = true;
       }
@@ -214,6 +252,7 @@ class MpiHostExchange : public Exchange {
       }
       if (progress) continue;
       if (next < schunks_.size()) {  // nothing landed: block on the next D2H chunk
+        if (kernel_) continue;      // poll its flag (and the receives) again
         GMT_CHECK("stage D2H wait", gmt_rt_event_synchronize(events_[next]));
         send(next++);
       } else {  // every chunk is sent: block on the receives
@@ -232,8 +271,14 @@ class MpiHostExchange : public Exchange {
   struct Chunk {
     size_t msg, off, len;
   };
+  static constexpr int kStageWgs = 32;
   MPI_Comm c_;
   std::vector<Msg> recvs_, sends_;
+  bool kernel_;
+  Buffer<gmt_stage_chunk> table_;
+  Buffer<unsigned> counters_;
+  Buffer<uint64_t> flags_;  // per send chunk: the exchange (epoch) whose data it holds
+  uint64_t epoch_ = 0;
   std::vector<Buffer<char>> rstage_[2], sstage_;
   std::vector<Chunk> schunks_, rchunks_;
   std::vector<gmt_event_t> events_;

@@ -332,6 +332,17 @@ int gmt_ipc_exchange(const gmt_ipc_plan* p, void*) {
   return 0;
 }
 
+// CPU backend of csrc/kernels/stage.hip: copy, then publish each chunk's flag
+int gmt_stage_copy(int n_chunks, const gmt_stage_chunk* chunks, unsigned*, uint64_t* flags, uint64_t value,
+                   int wgs_per_chunk, void*) {
+  if (n_chunks < 0 || wgs_per_chunk < 1 || (n_chunks > 0 && (!chunks || !flags))) return 1;
+  for (int k = 0; k < n_chunks; ++k) {
+    if (chunks[k].bytes > 0) std::memcpy(chunks[k].dst, chunks[k].src, static_cast<size_t>(chunks[k].bytes));
+    __atomic_store_n(flags + k, value, __ATOMIC_RELEASE);
+  }
+  return 0;
+}
+
 const char* gmt_error_string(int err) {
   switch (err) {
     case 0: return "success";

@@ -142,9 +142,10 @@ int gmt_rt_malloc(void** p, size_t bytes, int space) {
     *p = m;
     return kOk;
   }
-  if (space == GMT_SPACE_PINNED || space == GMT_SPACE_HOST) {
+  if (space == GMT_SPACE_PINNED || space == GMT_SPACE_PINNED_COHERENT || space == GMT_SPACE_HOST) {
     if (posix_memalign(p, 64, bytes) != 0) return kNoMem;
-    if (space == GMT_SPACE_PINNED) {
+    std::memset(*p, 0, bytes);
+    if (space != GMT_SPACE_HOST) {
       std::lock_guard<std::mutex> g(g_mu);
       g_allocs[reinterpret_cast<uintptr_t>(*p)] = Alloc{bytes, space, -1};
     }

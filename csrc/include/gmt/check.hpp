@@ -61,7 +61,8 @@ inline const char* space_name(int space) {
   switch (space) {
     case GMT_SPACE_DEVICE: return "Device";
     case GMT_SPACE_MANAGED: return "Managed";
-    case GMT_SPACE_PINNED: return "Host";
+    case GMT_SPACE_PINNED:
+    case GMT_SPACE_PINNED_COHERENT: return "Host";
     default: return "Unregistered";
   }
 }

@@ -202,6 +202,21 @@ int gmt_ipc_plan_init(gmt_ipc_plan* plan, int n_send, const gmt_ipc_chan* sends,
                       const gmt_ipc_chan* recvs);
 int gmt_ipc_exchange(const gmt_ipc_plan* plan, void* stream);
 
+/* ---- Kernel-driven host staging (csrc/kernels/stage.hip): one launch copies
+ *      every chunk src -> dst (device memory -> page-locked host memory the
+ *      GPU maps; or the reverse), G workgroups per chunk; once chunk k is
+ *      complete and visible system-wide, `value` is stored into flags[k]
+ *      (GMT_SPACE_PINNED_COHERENT memory) so the host can hand chunk k to MPI
+ *      while later chunks are still being copied.  The chunk table and the
+ *      per-chunk arrival counters (zero between launches) are device memory. */
+typedef struct gmt_stage_chunk {
+  const void* src;
+  void* dst;
+  int64_t bytes;
+} gmt_stage_chunk;
+int gmt_stage_copy(int n_chunks, const gmt_stage_chunk* chunks, unsigned* counters, uint64_t* flags,
+                   uint64_t value, int wgs_per_chunk, void* stream);
+
 /* One kernel per entry point: the variants the defaults were chosen against
  * are measured by csrc/bench/variant_bench.hip, not shipped in this ABI. */
 

@@ -41,6 +41,9 @@ enum gmt_space {
   GMT_SPACE_FLAGS = 4,   /* device memory for cross-process flags: uncached
                             (every access reaches memory), zeroed, exportable
                             by IPC (hipExtMallocWithFlags Uncached)       */
+  GMT_SPACE_PINNED_COHERENT = 5, /* page-locked host memory the GPU writes
+                            through (hipHostMallocCoherent): kernel-driven
+                            staging and GPU -> host completion flags      */
   GMT_SPACE_UNREGISTERED = -1
 };
 

@@ -82,6 +82,7 @@ int gmt_rt_malloc(void** p, size_t bytes, int space) {
   switch (space) {
     case GMT_SPACE_DEVICE: RT_RET(hipMalloc(p, bytes));
     case GMT_SPACE_PINNED: RT_RET(hipHostMalloc(p, bytes, hipHostMallocDefault));
+    case GMT_SPACE_PINNED_COHERENT: RT_RET(hipHostMalloc(p, bytes, hipHostMallocCoherent));
     case GMT_SPACE_MANAGED: RT_RET(hipMallocManaged(p, bytes, hipMemAttachGlobal));
     case GMT_SPACE_FLAGS: {
       hipError_t e = hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
@@ -103,7 +104,8 @@ int gmt_rt_free(void* p, int space) {
     case GMT_SPACE_DEVICE:
     case GMT_SPACE_FLAGS:
     case GMT_SPACE_MANAGED: RT_RET(hipFree(p));
-    case GMT_SPACE_PINNED: RT_RET(hipHostFree(p));
+    case GMT_SPACE_PINNED:
+    case GMT_SPACE_PINNED_COHERENT: RT_RET(hipHostFree(p));
     case GMT_SPACE_HOST: free(p); return 0;
     default: return static_cast<int>(hipErrorInvalidValue);
   }

@@ -323,11 +323,11 @@ def test_kernel_bench_host():
     GPU-only csrc/bench/variant_bench.hip); the K-sweep section runs every
     built sweep count."""
     out = run_app("gmt_kernel_bench", "--daxpy-n=4096", "--jacobi-n=64", "--iters=2",
-                  "--only=daxpy,jacobi,tb", "--tb-k=1,7,12,24").stdout
+                  "--only=daxpy,jacobi,tb", "--tb-k=1,7,12,20").stdout
     assert len(re.findall(r"^daxpy\s+v0", out, re.M)) == 1
     assert len(re.findall(r"^rocblas\s+v0", out, re.M)) == 1
     assert len(re.findall(r"^jacobi5\s+v0", out, re.M)) == 1
-    assert [int(k) for k in re.findall(r"^jacobi5tb\s+v(\d+)", out, re.M)] == [1, 7, 12, 24]
+    assert [int(k) for k in re.findall(r"^jacobi5tb\s+v(\d+)", out, re.M)] == [1, 7, 12, 20]
 
 
 def test_watchdog_aborts_hung_exchange():
