@@ -218,16 +218,36 @@ class IpcTransport : public Transport {
  public:
   IpcTransport(std::unique_ptr<Control> owned, Control* ctl)
       : Transport(ctl->rank(), ctl->size()), owned_(std::move(owned)), ctl_(ctl) {}
-  ~IpcTransport() override { gathers_.clear(); }
+  ~IpcTransport() override {
+    gathers_.clear();
+    gbuf_.clear();
+  }
   Kind kind() const override { return Kind::Ipc; }
   const char* name() const override { return "ipc"; }
   std::unique_ptr<Exchange> plan(const std::vector<Msg>& r, const std::vector<Msg>& s) override {
     return std::make_unique<IpcExchange>(*ctl_, &cache_, r, s);
   }
-  // Host-staged through one persistent pinned buffer (grown on demand): a
-  // device D2H, the control plane's rank-ordered sum, an H2D on the stream.
-  void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override { staged(buf, n, s, false); }
-  void allreduce_max(double* buf, size_t n, gmt_stream_t s) override { staged(buf, n, s, true); }
+  // All-reduce = the IPC all-gather of every rank's vector into a gather
+  // buffer (one exchange kernel), then one kernel reducing the slices in
+  // rank order: stream-ordered, no host round trip, the same bits on every
+  // rank.  Vectors above kDeviceReduceMax bytes go host-staged (one
+  // persistent pinned buffer, the control plane's rank-ordered reduction).
+  void allreduce_sum(double* buf, size_t n, gmt_stream_t s) override { reduce(buf, n, s, false); }
+  void allreduce_max(double* buf, size_t n, gmt_stream_t s) override { reduce(buf, n, s, true); }
+  void reduce(double* buf, size_t n, gmt_stream_t s, bool max) {
+    if (size_ == 1 || n == 0) return;
+    if (n * sizeof(double) > kDeviceReduceMax) return staged(buf, n, s, max);
+    // transport-owned buffers keyed by the length only (the same key on every
+    // rank, whatever the caller's pointers): the gather plan is created once
+    // per length, collectively
+    auto it = gbuf_.find(n);
+    if (it == gbuf_.end()) it = gbuf_.emplace(n, Buffer<double>(n * (size_ + 1), GMT_SPACE_DEVICE)).first;
+    double* g = it->second.data();
+    double* mine = g + n * size_;
+    GMT_CHECK("allreduce copy", gmt_rt_memcpy_async(mine, buf, n * sizeof(double), s));
+    allgather(mine, g, n * sizeof(double), s);
+    GMT_CHECK("slices reduce", gmt_slices_reduce(max ? 1 : 0, static_cast<int64_t>(n), size_, g, buf, s));
+  }
   void staged(double* buf, size_t n, gmt_stream_t s, bool max) {
     if (size_ == 1) return;
     double* h = stage(n * sizeof(double));
@@ -275,6 +295,8 @@ class IpcTransport : public Transport {
     return reinterpret_cast<double*>(staging_.data());
   }
   static constexpr int kGatherTag = 777;
+  static constexpr size_t kDeviceReduceMax = size_t(1) << 20;  // 1 MiB vectors
+  std::map<size_t, Buffer<double>> gbuf_;  // per length: size_ gathered slices + this rank's copy
   std::unique_ptr<Control> owned_;
   Control* ctl_;
   IpcCache cache_;

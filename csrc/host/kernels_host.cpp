@@ -106,6 +106,16 @@ int gmt_sum(int64_t n, const double* x, double* out, double*, void*) {
   return 0;
 }
 
+int gmt_slices_reduce(int op, int64_t n, int nslices, const double* in, double* out, void*) {
+  if (n < 0 || nslices < 1 || (op != 0 && op != 1)) return 1;
+  for (int64_t i = 0; i < n; ++i) {
+    double v = in[i];
+    for (int r = 1; r < nslices; ++r) v = op == 0 ? v + in[r * n + i] : std::max(v, in[r * n + i]);
+    out[i] = v;
+  }
+  return 0;
+}
+
 int gmt_abs_max(int64_t nx, int64_t ny, const double* z, int64_t ld, double* out, double*, void*) {
   double m = 0.0;
   for (int64_t y = 0; y < ny; ++y)

@@ -78,6 +78,11 @@ int gmt_diff_sq(int64_t nx, int64_t ny, const double* a, int64_t lda, const doub
 int64_t gmt_sum_workspace(int64_t n);
 int gmt_sum(int64_t n, const double* x, double* out, double* workspace, void* stream);
 
+/* ---- out[i] = sum (op 0) or max (op 1) over r = 0..nslices-1 of
+ *      in[r*n + i], in rank order (an all-gather + this = a deterministic
+ *      all-reduce; out may alias slice 0 of in only if it is in[0..n)) */
+int gmt_slices_reduce(int op, int64_t n, int nslices, const double* in, double* out, void* stream);
+
 /* ---- max over the nx x ny region of |z| -> out[0]; workspace of
  *      gmt_diff_sq_workspace(nx, ny) doubles */
 int gmt_abs_max(int64_t nx, int64_t ny, const double* z, int64_t ld, double* out, double* workspace,

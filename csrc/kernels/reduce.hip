@@ -171,6 +171,21 @@ __global__ __launch_bounds__(kBlock) void sum1d_pass1(int64_t n, const double* _
   if (threadIdx.x == 0) ws[b] = acc;
 }
 
+// ---------------- out[i] = sum (or max) over r of in[r * n + i], r in order:
+// the reduction half of an all-reduce built from an all-gather (the ipc
+// transport), the same bits on every rank
+__global__ __launch_bounds__(kBlock) void slices_kernel(int op, int64_t n, int ns, const double* __restrict__ in,
+                                                        double* __restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  double v = in[i];
+  for (int r = 1; r < ns; ++r) {
+    const double w = in[r * n + i];
+    v = op == 0 ? v + w : fmax(v, w);
+  }
+  out[i] = v;
+}
+
 // ---------------- max |z| over a 2-D region (the engine's exactness guard on
 // a measured field bound); same tiles and workspace as diff_sq
 __device__ __forceinline__ double block_max(double v) {
@@ -331,6 +346,15 @@ extern "C" int gmt_sum(int64_t n, const double* x, double* out, double* ws, void
   const int64_t nb = gmt_sum_workspace(n);
   sum1d_pass1<<<grid_1d(nb), kBlock, 0, s>>>(n, x, ws, aligned16(x));
   sum_all<<<1, kBlock, 0, s>>>(ws, nb, out);
+  GMT_RET_LAUNCH();
+}
+
+extern "C" int gmt_slices_reduce(int op, int64_t n, int nslices, const double* in, double* out, void* stream) {
+  using namespace gmt;
+  if (n < 0 || nslices < 1 || (op != 0 && op != 1)) return static_cast<int>(hipErrorInvalidValue);
+  if (n == 0) return 0;
+  slices_kernel<<<grid_1d((n + kBlock - 1) / kBlock), kBlock, 0, static_cast<hipStream_t>(stream)>>>(op, n, nslices,
+                                                                                                  in, out);
   GMT_RET_LAUNCH();
 }
 
