@@ -1,0 +1,629 @@
+// Temporal-blocking Jacobi kernel and its launch code (see jacobi5tb.hip for
+// the design).  Included by the jacobi5tb_k*.hip translation units, each of
+// which instantiates dispatch_k for a few K: the fully unrolled register
+// pipelines take minutes per K to compile, so they build in parallel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <utility>
+
+#include "common.hpp"
+#include "gmt/kernels.h"
+
+namespace gmt {
+namespace tb {
+
+constexpr int kMaxRect = 8;
+constexpr int kMaxThreads = 512;              // 8 waves: 2 per SIMD
+constexpr int kNC = 4;                        // columns per lane
+constexpr int kCols = kNC * kWave;            // 256 columns per strip
+constexpr uint32_t kRowBytes = kCols * 8;     // one row of a strip: 2 KB
+constexpr uint32_t kSlotBytes = kRowBytes;    // DMA ring slot: two full-wave 16-B DMAs
+constexpr uint32_t kDrop = 0x80000000u;       // buffer offset past num_records: no-op access
+constexpr int kP = 6;                         // input rows in flight
+constexpr int kRS = kP + 2;                   // DMA ring: rows s-2..s in use, s+1..s+P-1 in flight
+constexpr int kBarrier = 2;                   // two-stage strips: one s_barrier every kBarrier steps
+constexpr int kLag = kBarrier + 1;            // stage 1 runs kLag steps behind stage 0: its rows, read at the end of step s, are published by a barrier at the end of step s-2 or s-1
+constexpr int kHS = 8;                        // hand-off ring (2 stages): reads in flight across a barrier + a 2-step lead
+constexpr int kMaxK1 = 10;                    // largest single-wave K
+static_assert(kHS >= kLag + kBarrier + 2, "hand ring");
+
+constexpr int ring_left(int K) { return (K + kNC - 1) / kNC * kNC; }
+constexpr int strip_out(int K) { return kCols - 2 * ring_left(K); }
+constexpr int n_stages(int K) { return K <= kMaxK1 ? 1 : 2; }
+constexpr int stage0_levels(int K) { return (K + 1) / 2; }
+// Unroll of the step loop: the register cycle of the pipeline.  A level's
+// new row is live while its step-(s-2) row is still being read, so a step
+// frees one d4 at the top level and the rows move up one register slot per
+// step: a value's register passes through the two slots of each of the
+// NL - 1 stored levels plus the spare, 2(NL - 1) + 1 steps.  Unrolling by
+// exactly that lets the allocator keep every row in place (no copies at the
+// back edge) at 16 VGPRs per level; ring slots are then computed per step.
+constexpr int unroll_for(int NL) { return NL > 1 ? 2 * (NL - 1) + 1 : 2; }
+
+struct Args {
+  int64_t r[kMaxRect][4];        // output rects: x0, nx, y0, ny (absolute)
+  int64_t nstrip[kMaxRect];      // strips per rect
+  int64_t tstart[kMaxRect + 1];  // prefix sum of workgroups
+  int64_t dom[4];                // interior x0, nx, y0, ny
+  int64_t ld;                    // row pitch (elements)
+  int64_t last_row;              // last allocated row (load clamp)
+  int n;                         // rects
+  int mask;                      // halo sides: bit0..3 = W/E/S/N
+  // segments of rect k: an optional top edge segment of e0[k] rows and a
+  // bottom one of e1[k] rows (short: the only ones whose waves can need the
+  // Dirichlet rule in y), then nmid[k] interior segments of lmid[k] rows
+  int64_t e0[kMaxRect], e1[kMaxRect], nmid[kMaxRect], lmid[kMaxRect];
+  // the first and last strip groups (rule waves where a Dirichlet column is
+  // in reach) use their own, shorter interior segments
+  int64_t nmid_b[kMaxRect], lmid_b[kMaxRect];
+  int nw;                        // strips per workgroup
+  double quarter;                // 0.25 (EXACT): an SGPR operand
+  // completion signal of the leading workgroups (gmt_tb_opts.signal_rects):
+  // workgroups t < sig_wgs are dispatched first, unswizzled; the last of
+  // them to finish adds 1 to *signal once its stores are visible device-wide
+  int64_t sig_wgs;
+  unsigned* sig_count;
+  uint64_t* signal;
+  int prio;                      // single-round launch: stage-0 waves at raised priority
+};
+
+struct d4 {
+  double x, y, z, w;
+};
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double* p, uint32_t bytes) {
+  // 0x00020000: raw-buffer descriptor word 3 for gfx9 (32-bit data format)
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(p), 0, bytes, 0x00020000);
+}
+
+// LDS per strip: the DMA ring, plus the hand-off ring with 2 stages
+__host__ __device__ constexpr int64_t strip_lds(int stages) {
+  return static_cast<int64_t>(kRS) * kSlotBytes + (stages > 1 ? kHS * kRowBytes : 0);
+}
+
+// s_waitcnt vmcnt(n) only (expcnt / lgkmcnt left at their maxima), as a
+// compiler barrier for memory: the LDS-DMA'd rows are read by ds_read after
+// it, and the compiler does not track LDS-DMA -> ds_read dependencies
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// hand-off rows written by this wave are visible to the workgroup after it.
+// Outstanding DMAs and stores are not waited for (gfx950 has the back-off
+// barrier, so s_barrier needs no vmcnt(0)).
+__device__ __forceinline__ void step_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ d4 lds_row(const char* slot, int lane) {
+  const d2* p = reinterpret_cast<const d2*>(slot) + 2 * lane;
+  const d2 a = p[0], b = p[1];
+  return d4{a.x, a.y, b.x, b.y};
+}
+
+__device__ __forceinline__ u4 pack2(double a, double b) {
+  return u4{static_cast<unsigned>(__double2loint(a)), static_cast<unsigned>(__double2hiint(a)),
+            static_cast<unsigned>(__double2loint(b)), static_cast<unsigned>(__double2hiint(b))};
+}
+__device__ __forceinline__ u2 pack1(double a) {
+  return u2{static_cast<unsigned>(__double2loint(a)), static_cast<unsigned>(__double2hiint(a))};
+}
+
+// One wave = one stage of one strip: levels PB..PE of the K-level pipeline.
+// PB == 1: level 0 comes from the DMA ring; otherwise from the hand-off ring
+// (rows written by stage 0 two to four steps earlier; this stage runs two
+// steps behind, D = 2, so it can read them before the step barrier).  PE == K: level K is stored to `un`; otherwise level
+// PE goes to the hand-off ring.  Strip output columns [xs, xe), rows [ys, ye).
+template <int K, int PB, int PE, bool EXACT, bool EDGE, bool RULE, bool SYNC>
+__device__ __forceinline__ void run_stage(const Args& a, const double* __restrict__ u, double* __restrict__ un,
+                                          char* ring, char* hand, int lane, int64_t xs, int64_t xe, int64_t ys,
+                                          int64_t ye, int nsteps) {
+  constexpr bool kIn = PB == 1;
+  constexpr bool kOut = PE == K;
+  constexpr int D = kIn ? 0 : kLag;               // step lag behind stage 0
+  constexpr int SPS = kOut ? (EDGE ? 4 : 2) : 0;  // global stores per step
+  constexpr int DPS = kIn ? 2 : 0;                // DMAs per step
+  // every kernel argument the loop needs, as values: the asm memory clobbers
+  // below would otherwise force a reload of the kernarg segment per use
+  const int64_t ld = a.ld;
+  const int mask = a.mask;
+  const double quarter = a.quarter;
+  const int64_t dx0 = a.dom[0], dx1 = a.dom[0] + a.dom[1];
+  const int64_t dy0 = a.dom[2], dy1 = a.dom[2] + a.dom[3];
+  const int64_t cf = xs - ring_left(K);  // first column of the strip window
+  const int64_t c0 = cf + kNC * lane;    // this lane: columns c0 .. c0+3
+  const int64_t yl = ys - K;             // level-0 row of step 0
+  const int L = static_cast<int>(ye - ys);
+  const uint32_t ld8 = static_cast<uint32_t>(ld) * 8u;
+
+  //  loads: rows [yl, min(yl + L + 2K, last_row + 1)), 2048 contiguous bytes
+  //  from column cf (a column outside the row wraps into the neighbouring
+  //  row or is zero-filled: garbage outside every output cone)
+  const int64_t nrow_in = std::min<int64_t>(L + 2 * K, a.last_row + 1 - yl);
+  const __amdgpu_buffer_rsrc_t lrs = row_rsrc(u + yl * ld, static_cast<uint32_t>(nrow_in) * ld8);
+  const uint32_t loff = static_cast<uint32_t>(cf) * 8u + static_cast<uint32_t>(lane) * 16u;
+  auto dma = [&](int s, int slot) {
+    if constexpr (kIn) {
+      char* dst = ring + slot * kSlotBytes;
+      const uint32_t o = static_cast<uint32_t>(s) * ld8;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst, 16, loff + o, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + 1024, 16, loff + 1024u + o, 0, 0, 0);
+    }
+  };
+  //  stores: rows [ys, ye) from column xs.  The left output edge is a lane
+  //  boundary (KL = 0 mod 4): 16-B stores of columns 0-1 and 2-3 where both
+  //  are inside, and (EDGE: a rect of the launch ends inside a lane at an odd
+  //  column) 8-B stores of column 0 or 2 alone.  Lanes with nothing to store
+  //  get an offset past any row (dropped).
+  const __amdgpu_buffer_rsrc_t srs = row_rsrc(un + ys * ld + xs, static_cast<uint32_t>(L) * ld8);
+  const bool in0 = c0 >= xs && c0 < xe, in1 = c0 + 1 >= xs && c0 + 1 < xe;
+  const bool in2 = c0 + 2 >= xs && c0 + 2 < xe, in3 = c0 + 3 >= xs && c0 + 3 < xe;
+  const uint32_t sta = (in0 && in1) ? static_cast<uint32_t>(c0 - xs) * 8u : kDrop;
+  const uint32_t stb = (in2 && in3) ? static_cast<uint32_t>(c0 + 2 - xs) * 8u : kDrop;
+  const uint32_t stc = (in0 && !in1) ? static_cast<uint32_t>(c0 - xs) * 8u : kDrop;
+  const uint32_t std_ = (in2 && !in3) ? static_cast<uint32_t>(c0 + 2 - xs) * 8u : kDrop;
+  auto store_step = [&](int s, const d4& v) {  // level K of step s = output row ys + s - D - 2K
+    if constexpr (kOut) {
+      const uint32_t ro = static_cast<uint32_t>(s - D - 2 * K) * ld8;  // wraps for warm-up rows: out of range
+      __builtin_amdgcn_raw_buffer_store_b128(pack2(v.x, v.y), srs, sta + ro, 0, 2 /* nt */);
+      __builtin_amdgcn_raw_buffer_store_b128(pack2(v.z, v.w), srs, stb + ro, 0, 2);
+      if constexpr (EDGE) {
+        __builtin_amdgcn_raw_buffer_store_b64(pack1(v.x), srs, stc + ro, 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b64(pack1(v.z), srs, std_ + ro, 0, 2);
+      }
+    }
+  };
+
+  // Dirichlet rule (RULE only): a cell outside the interior on a side whose
+  // ghost ring is fixed keeps its value at every level
+  const bool gw = mask & 1, ge = mask & 2, gs = mask & 4, gn = mask & 8;
+  auto kept_col = [&](int64_t c) { return (c < dx0 && !gw) || (c >= dx1 && !ge); };
+  const bool kx0 = kept_col(c0), kx1 = kept_col(c0 + 1), kx2 = kept_col(c0 + 2), kx3 = kept_col(c0 + 3);
+
+  auto level = [&](const d4& up_, const d4& c, const d4& dn, int64_t row) -> d4 {
+#pragma clang fp contract(off)
+    const double w = dpp_from_lower(c.w), e = dpp_from_upper(c.x);
+    d4 v;
+    if constexpr (EXACT) {
+      v.x = quarter * ((w + c.y) + (up_.x + dn.x));
+      v.y = quarter * ((c.x + c.z) + (up_.y + dn.y));
+      v.z = quarter * ((c.y + c.w) + (up_.z + dn.z));
+      v.w = quarter * ((c.z + e) + (up_.w + dn.w));
+    } else {
+      v.x = (w + c.y) + (up_.x + dn.x);
+      v.y = (c.x + c.z) + (up_.y + dn.y);
+      v.z = (c.y + c.w) + (up_.z + dn.z);
+      v.w = (c.z + e) + (up_.w + dn.w);
+    }
+    if constexpr (RULE) {
+      const bool rk = (row < dy0 && !gs) || (row >= dy1 && !gn);
+      const double f = EXACT ? 1.0 : 4.0;  // a kept cell: V_p = 4 V_{p-1}
+      v.x = (rk || kx0) ? c.x * f : v.x;
+      v.y = (rk || kx1) ? c.y * f : v.y;
+      v.z = (rk || kx2) ? c.z * f : v.z;
+      v.w = (rk || kx3) ? c.w * f : v.w;
+    }
+    return v;
+  };
+
+  constexpr int NL = PE - PB + 1;
+  // W[p - PB][0 / 1]: level p (PB..PE-1) of the rows of steps s-2 / s-1
+  d4 W[NL > 1 ? NL - 1 : 1][2];
+#pragma unroll
+  for (int p = 0; p < (NL > 1 ? NL - 1 : 1); ++p)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) W[p][j] = d4{0.0, 0.0, 0.0, 0.0};
+
+  // prologue: rows 0..P-1 in flight, each preceded by the (dropped) stores a
+  // steady-state step issues, so every wait below counts the same
+  // (SPS + DPS)(P - 1) younger memory operations
+  if constexpr (kIn) {
+    // (each dummy store gets its own out-of-range row so the compiler cannot
+    // merge identical stores)
+    static_for<0, kP>([&](auto I) {
+      store_step(decltype(I)::value - kP, d4{0.0, 0.0, 0.0, 0.0});
+      dma(decltype(I)::value, decltype(I)::value);
+    });
+  }
+
+  // level PB-1 rows of step s (rows s-D-PB-1 .. s-D-PB+1), read one step
+  // ahead so the ds_reads are in flight across the step barrier
+  d4 r0, r1, r2;
+  auto load_rows = [&](int s) {
+    if constexpr (kIn) {
+      // the DMA of row s (issued at the end of step s-P) has landed once at
+      // most (SPS + DPS)(P - 1) younger memory operations are outstanding
+      wait_vmcnt<(SPS + DPS) * (kP - 1)>();
+      r0 = lds_row(ring + ((s + kRS - 2) % kRS) * kSlotBytes, lane);
+      r1 = lds_row(ring + ((s + kRS - 1) % kRS) * kSlotBytes, lane);
+      r2 = lds_row(ring + (s % kRS) * kSlotBytes, lane);
+    } else {
+      // stage 0's level-KA rows of steps s-4 .. s-2 (published by the
+      // barriers of those steps)
+      r0 = lds_row(hand + ((s + kHS - kLag - 2) % kHS) * kRowBytes, lane);
+      r1 = lds_row(hand + ((s + kHS - kLag - 1) % kHS) * kRowBytes, lane);
+      r2 = lds_row(hand + ((s + kHS - kLag) % kHS) * kRowBytes, lane);
+    }
+  };
+  load_rows(0);
+
+  auto step = [&](auto J, int s) {
+    (void)J;
+    const int64_t rbase = yl + s - D;  // level p is row rbase - p
+    d4 v = level(r0, r1, r2, rbase - PB);
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<PB + 1, PE + 1>([&](auto Q) {
+      constexpr int p = decltype(Q)::value;  // PB+1 .. PE, bottom-up
+      const d4 nv = level(W[p - 1 - PB][0], W[p - 1 - PB][1], v, rbase - p);
+      W[p - 1 - PB][0] = W[p - 1 - PB][1];  // rows of steps s-1 and s become s-2 and s-1
+      W[p - 1 - PB][1] = v;
+      v = nv;
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if constexpr (kOut) {
+      if constexpr (!EXACT) {
+        v.x = __builtin_amdgcn_ldexp(v.x, -2 * K);  // exact power-of-two unscale
+        v.y = __builtin_amdgcn_ldexp(v.y, -2 * K);
+        v.z = __builtin_amdgcn_ldexp(v.z, -2 * K);
+        v.w = __builtin_amdgcn_ldexp(v.w, -2 * K);
+      }
+      store_step(s, v);  // issued every step (warm-up rows are out of range)
+    } else {
+      d2* h = reinterpret_cast<d2*>(hand + (s % kHS) * kRowBytes) + 2 * lane;
+      h[0] = d2{v.x, v.y};
+      h[1] = d2{v.z, v.w};
+    }
+    // the ring slot of row s-2 is free (its ds_reads completed before level
+    // 1 used them): prefetch row s+P into it
+    dma(s + kP, (s + kP) % kRS);
+    // hand-off row written (visible to the workgroup after the barrier),
+    // then the next step's rows requested, then the barrier
+    const bool sync_step = SYNC && (s % kBarrier == kBarrier - 1);
+    if (sync_step) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    load_rows(s + 1);
+    if (sync_step) asm volatile("s_barrier" ::: "memory");
+  };
+
+  constexpr int kU = unroll_for(NL);
+  for (int s0 = 0; s0 < nsteps; s0 += kU) static_for<0, kU>([&](auto J) { step(J, s0 + decltype(J)::value); });
+  // no LDS-DMA may land after the workgroup's LDS is released
+  wait_vmcnt<0>();
+}
+
+// A workgroup = nw adjacent strips of one segment row, G waves per strip
+// (adjacent strips share their overlap columns in the CU's L1 / the XCD's
+// L2).  G == 1: every wave is independent (no barrier).
+template <int K, bool EXACT, bool EDGE>
+__device__ __forceinline__ void tb_block(const Args& a, const double* __restrict__ u, double* __restrict__ un,
+                                         int64_t t) {
+  constexpr int G = n_stages(K);
+  extern __shared__ d2 lds_dyn[];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
+  const int sl = wave / G, stage = wave % G;
+  int k = 0;
+  while (k + 1 < a.n && t >= a.tstart[k + 1]) ++k;
+  const int64_t lt = t - a.tstart[k];
+  const int64_t ngroups = (a.nstrip[k] + a.nw - 1) / a.nw;
+  // Dispatch order: every workgroup that can hold Dirichlet-rule waves
+  // (~1.5x the VALU per step) goes first, so the launch's tail is made of
+  // fast ones: (A) the edge segments, all strip groups; (B) the interior
+  // segments' first and last strip groups; (C) the rest.
+  const int64_t ry0 = a.r[k][2], ry1 = a.r[k][2] + a.r[k][3];
+  const int64_t e0 = a.e0[k], e1 = a.e1[k];
+  const int64_t nedge = (e0 > 0) + (e1 > 0), nbnd = ngroups < 2 ? ngroups : 2;
+  int64_t j, gi;
+  if (lt < nedge * ngroups) {
+    j = lt / ngroups;
+    gi = lt % ngroups;
+  } else if (lt < nedge * ngroups + a.nmid_b[k] * nbnd) {
+    const int64_t l2 = lt - nedge * ngroups;
+    j = nedge + l2 / nbnd;
+    gi = l2 % nbnd == 0 ? 0 : ngroups - 1;
+  } else {
+    const int64_t l3 = lt - nedge * ngroups - a.nmid_b[k] * nbnd;
+    j = nedge + l3 / (ngroups - 2);
+    gi = 1 + l3 % (ngroups - 2);
+  }
+  const int64_t lmid = (gi == 0 || gi == ngroups - 1) ? a.lmid_b[k] : a.lmid[k];
+  int64_t ys, ye;
+  if (e0 > 0 && j == 0) {
+    ys = ry0;
+    ye = ry0 + e0;
+  } else {
+    if (e0 > 0) --j;
+    if (e1 > 0 && j == 0) {
+      ys = ry1 - e1;
+      ye = ry1;
+    } else {
+      if (e1 > 0) --j;
+      ys = ry0 + e0 + j * lmid;
+      ye = ys + lmid < ry1 - e1 ? ys + lmid : ry1 - e1;
+    }
+  }
+  // L + 2K steps (stage 1 of a split strip runs two steps behind: two more)
+  constexpr int kU = unroll_for(G == 1 ? K : stage0_levels(K));
+  static_assert(G == 1 || unroll_for(stage0_levels(K)) == unroll_for(K - stage0_levels(K)), "stages step together");
+  const int nsteps = static_cast<int>((ye - ys + 2 * K + (G > 1 ? kLag : 0) + kU - 1) / kU * kU);
+  const int64_t strip = gi * a.nw + sl;
+  if (strip >= a.nstrip[k]) {  // no strip for this wave
+    if constexpr (G > 1) {
+      for (int s = 0; s < nsteps; ++s)  // the workgroup's barriers
+        if (s % kBarrier == kBarrier - 1) step_barrier();
+    }
+    return;
+  }
+  constexpr int64_t wout = strip_out(K);
+  const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
+  int64_t xs = rx0 + strip * wout;
+  if (xs + wout > rx1) xs = rx1 - wout > rx0 ? rx1 - wout : rx0;  // last strip: shifted left to end at rx1
+  const int64_t xe = xs + wout < rx1 ? xs + wout : rx1;
+  // the rule path only where a computed cell can be a fixed ring cell
+  const int64_t cx0 = xs - ring_left(K), cx1 = cx0 + kCols;
+  const bool rule = (cx0 < a.dom[0] && !(a.mask & 1)) || (cx1 > a.dom[0] + a.dom[1] && !(a.mask & 2)) ||
+                    (ys - K < a.dom[2] && !(a.mask & 4)) || (ye + K > a.dom[2] + a.dom[3] && !(a.mask & 8));
+  char* ring = reinterpret_cast<char*>(lds_dyn) + sl * strip_lds(G);
+  char* hand = ring + kRS * kSlotBytes;
+  if constexpr (G == 1) {
+    if (rule)
+      run_stage<K, 1, K, EXACT, EDGE, true, false>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
+    else
+      run_stage<K, 1, K, EXACT, EDGE, false, false>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
+  } else {
+    constexpr int KA = stage0_levels(K);
+    if (stage == 0) {
+      // a launch of one round has no later workgroups to fill the SIMDs
+      // while a strip's stage 1 waits on its stage 0: favour the producer
+      // (profiles/r02_tb.md 9.4)
+      if (a.prio) __builtin_amdgcn_s_setprio(2);
+      if (rule)
+        run_stage<K, 1, KA, EXACT, EDGE, true, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
+      else
+        run_stage<K, 1, KA, EXACT, EDGE, false, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
+    } else {
+      if (rule)
+        run_stage<K, KA + 1, K, EXACT, EDGE, true, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
+      else
+        run_stage<K, KA + 1, K, EXACT, EDGE, false, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
+    }
+  }
+}
+
+template <int K, bool EXACT, bool EDGE>
+__global__ __launch_bounds__(kMaxThreads) __attribute__((amdgpu_waves_per_eu(2)))
+void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__ un, int64_t nblocks) {
+  const int64_t ns = a.sig_wgs;
+  const int64_t b = blockIdx.x;
+  // signalling workgroups first, in dispatch order over all XCDs; the rest
+  // XCD-contiguous
+  const int64_t t = b < ns ? b : ns + xcd_swizzle(b - ns, nblocks - ns);
+  tb_block<K, EXACT, EDGE>(a, u, un, t);
+  if (t < ns) {
+    // every wave's stores written back past its XCD's L2, then one arrival
+    // per workgroup (vector atomics on uncached memory)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(a.sig_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+            static_cast<unsigned>(ns - 1)) {
+      __hip_atomic_store(a.sig_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(a.signal, uint64_t{1}, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace tb
+}  // namespace gmt
+
+namespace {
+
+using namespace gmt;
+using namespace gmt::tb;
+
+// Segment plan (rows per strip).  Every segment pays a 2K-step pipeline
+// warm-up, so interior segments should be long; but a wave whose segment
+// touches a Dirichlet row runs the rule path (~1.5x the VALU per step) for
+// the whole segment, and the launch ends with its slowest round.  Measured
+// (profiles/r02_tb4.md, K = 20, 32768^2): all-halo sides 4.41M MLUPS at 384
+// rows and 4.61M at 1024-2048; with Dirichlet sides 3.78M at 384, falling
+// to 2.38M at 4096.  So: short edge segments (max(64, K) rows) where the
+// rect touches a Dirichlet row, and interior segments whose length L
+// minimises rounds(L) x (L + 2K), rounds = ceil(workgroups / resident
+// workgroups), over L in [128, 2048].
+struct SegPlan {
+  int64_t e0[kMaxRect], e1[kMaxRect], nmid[kMaxRect], lmid[kMaxRect], nmid_b[kMaxRect], lmid_b[kMaxRect];
+};
+
+// Signalling rects (k < sig_rects: the boundary bands of a pass whose halo
+// exchange overlaps the rest of it) get short segments, max(128, L/3) rows
+// and no edge split: their workgroups must finish early in the launch.
+template <int K>
+SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t resident_wgs, int sig_rects) {
+  SegPlan p{};
+  const int64_t edge = std::max<int64_t>(64, K);
+  auto fill = [&](int64_t L, int64_t* wgs) {
+    int64_t w = 0;
+    for (int k = 0; k < a.n; ++k) {
+      const int64_t ny = a.r[k][3], ry0 = a.r[k][2], ry1 = ry0 + ny;
+      if (k < sig_rects) {
+        const int64_t lb = std::min<int64_t>(std::max<int64_t>(128, L / 3), lmax);
+        p.e0[k] = p.e1[k] = 0;
+        p.nmid[k] = p.nmid_b[k] = (ny + lb - 1) / lb;
+        p.lmid[k] = p.lmid_b[k] = (ny + p.nmid[k] - 1) / p.nmid[k];
+        w += (a.nstrip[k] + a.nw - 1) / a.nw * p.nmid[k];
+        continue;
+      }
+      const bool top = seg_rows == 0 && ry0 - K < a.dom[2] && !(a.mask & 4);
+      const bool bot = seg_rows == 0 && ry1 + K > a.dom[2] + a.dom[3] && !(a.mask & 8);
+      p.e0[k] = p.e1[k] = 0;
+      if (ny > 2 * edge + 64) {  // room for edges and an interior
+        p.e0[k] = top ? edge : 0;
+        p.e1[k] = bot ? edge : 0;
+      }
+      const int64_t mid = ny - p.e0[k] - p.e1[k];
+      p.nmid[k] = (mid + L - 1) / L;
+      p.lmid[k] = (mid + p.nmid[k] - 1) / p.nmid[k];  // balanced lengths
+      // strip groups that can reach a Dirichlet column run the rule path
+      // (~2x the VALU per step): half-length segments, so they finish with
+      // the others instead of ending the launch
+      const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
+      const bool xrule = seg_rows == 0 && ((rx0 - ring_left(K) < a.dom[0] && !(a.mask & 1)) ||
+                                           (rx1 + ring_left(K) > a.dom[0] + a.dom[1] && !(a.mask & 2)));
+      const int64_t lb = xrule ? std::max<int64_t>(64, p.lmid[k] / 2) : p.lmid[k];
+      p.nmid_b[k] = (mid + lb - 1) / lb;
+      p.lmid_b[k] = (mid + p.nmid_b[k] - 1) / p.nmid_b[k];
+      const int64_t groups = (a.nstrip[k] + a.nw - 1) / a.nw, nbnd = groups < 2 ? groups : 2;
+      w += groups * ((p.e0[k] > 0) + (p.e1[k] > 0)) + nbnd * p.nmid_b[k] + (groups - nbnd) * p.nmid[k];
+    }
+    *wgs = w;
+  };
+  int64_t wgs = 0;
+  if (seg_rows > 0) {
+    fill(std::min<int64_t>(seg_rows, lmax), &wgs);
+    return p;
+  }
+  int64_t best_l = 128;
+  double best = 1e300;
+  for (int64_t L = 128; L <= std::min<int64_t>(2048, lmax); L += 32) {
+    fill(L, &wgs);
+    const double rounds = static_cast<double>((wgs + resident_wgs - 1) / resident_wgs);
+    // a segment runs L + 2K (+2 with two stages) steps, rounded up to the unroll
+    constexpr int64_t u = unroll_for(n_stages(K) == 1 ? K : stage0_levels(K));
+    const double cost = rounds * static_cast<double>((L + 2 * K + kLag * (n_stages(K) > 1) + u - 1) / u * u);
+    if (cost < best) {
+      best = cost;
+      best_l = L;
+    }
+  }
+  fill(std::min<int64_t>(best_l, lmax), &wgs);
+  return p;
+}
+
+// Fills the kernel arguments and the launch shape; info (optional) gets
+// {workgroups, resident workgroups, threads per workgroup, rows per interior
+// segment and interior segments of the first rect, VGPRs per lane}.
+template <int K, bool EXACT, bool EDGE>
+int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int64_t* dom, int mask, const double* u,
+              double* un, int64_t ld, int64_t nrows, hipStream_t s, int64_t* info = nullptr) {
+  constexpr int G = n_stages(K);
+  constexpr int kMaxStrips = kMaxThreads / kWave / G;
+  Args a{};
+  a.nw = std::min(o.wg_waves > 0 ? o.wg_waves : (G == 1 ? 4 : 1), kMaxStrips);  // two-stage: one strip (profiles/r02_tb4/launch_shapes.txt)
+  a.ld = ld;
+  a.last_row = nrows - 1;
+  a.mask = mask;
+  a.quarter = 0.25;
+  for (int j = 0; j < 4; ++j) a.dom[j] = dom[j];
+  constexpr int64_t wout = strip_out(K);
+  int64_t maxh = 0;
+  for (int k = 0; k < n_rect; ++k) {
+    const int64_t* r = rects + 4 * k;
+    if (r[1] <= 0 || r[3] <= 0) continue;
+    for (int j = 0; j < 4; ++j) a.r[a.n][j] = r[j];
+    a.nstrip[a.n] = (r[1] + wout - 1) / wout;
+    maxh = std::max(maxh, r[3]);
+    ++a.n;
+  }
+  if (a.n == 0) return 0;
+  // all strips of a rect narrower than nw strips: fewer strips per workgroup
+  int64_t maxs = 0;
+  for (int k = 0; k < a.n; ++k) maxs = std::max(maxs, a.nstrip[k]);
+  if (a.nw > maxs) a.nw = static_cast<int>(maxs);
+  // the kernel addresses a segment's rows through 32-bit buffer offsets:
+  // (L + 3K + 2 unroll + prefetch) rows of ld doubles must stay below 2^31
+  const int64_t lmax = std::min<int64_t>(1 << 20, (int64_t(1) << 31) / (ld * 8) - 3 * K - 2 * unroll_for(K) - kP);
+  if (lmax < 1) return static_cast<int>(hipErrorInvalidValue);
+  (void)maxh;
+  const size_t smem = static_cast<size_t>(a.nw * strip_lds(G));
+  if (smem > 65536) {  // above the default dynamic-LDS limit (gfx950 has 160 KB per CU)
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem));
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  // resident workgroups on the device for this shape (registers, LDS);
+  // queried once per device, kernel and strips-per-workgroup (an idempotent
+  // cache: a process driving several devices keeps one entry per device)
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> resident[kMaxDev][kMaxThreads / kWave + 1] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::atomic<int>* slot = dev >= 0 && dev < kMaxDev ? &resident[dev][a.nw] : nullptr;
+  int per_cu = slot ? slot->load(std::memory_order_relaxed) : 0;
+  if (per_cu <= 0) {
+    int occ = 0, cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE>),
+                                                     a.nw * G * kWave, smem) != hipSuccess || occ < 1)
+      occ = 1;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    per_cu = occ * cus;
+    if (slot) slot->store(per_cu, std::memory_order_relaxed);
+  }
+  const int sig_rects = o.signal_rects;  // non-empty rects (checked): the same indices after the compaction
+  const SegPlan sp = plan_segments<K>(a, o.seg_rows, lmax, per_cu, sig_rects);
+  a.tstart[0] = 0;
+  for (int k = 0; k < a.n; ++k) {
+    a.e0[k] = sp.e0[k];
+    a.e1[k] = sp.e1[k];
+    a.nmid[k] = sp.nmid[k];
+    a.lmid[k] = sp.lmid[k];
+    a.nmid_b[k] = sp.nmid_b[k];
+    a.lmid_b[k] = sp.lmid_b[k];
+    const int64_t groups = (a.nstrip[k] + a.nw - 1) / a.nw, nbnd = groups < 2 ? groups : 2;
+    a.tstart[k + 1] = a.tstart[k] + groups * ((sp.e0[k] > 0) + (sp.e1[k] > 0)) + nbnd * sp.nmid_b[k] +
+                      (groups - nbnd) * sp.nmid[k];
+  }
+  for (int k = a.n + 1; k <= kMaxRect; ++k) a.tstart[k] = a.tstart[a.n];
+  const int64_t nb = a.tstart[a.n];
+  a.sig_wgs = a.tstart[sig_rects];
+  a.prio = nb <= per_cu ? 1 : 0;
+  a.sig_count = o.signal_count;
+  a.signal = o.signal;
+  if (info) {
+    hipFuncAttributes fa{};
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE>));
+    const int64_t v[6] = {nb, per_cu, a.nw * G * kWave, a.lmid[0], a.nmid[0], fa.numRegs};
+    for (int j = 0; j < 6; ++j) info[j] = v[j];
+    return 0;
+  }
+  jacobi5tb_kernel<K, EXACT, EDGE><<<grid_1d(nb), a.nw * G * kWave, smem, s>>>(a, u, un, nb);
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // namespace
+
+namespace gmt {
+namespace tb {
+
+template <int K>
+int dispatch_k(const gmt_tb_opts& o, bool exact, int n_rect, const int64_t* rects, const int64_t* dom, int mask,
+               const double* u, double* un, int64_t ld, int64_t nrows, hipStream_t s, int64_t* info) {
+  // a rect narrower than a strip whose width is odd ends inside a lane pair:
+  // that lane stores column 0 or 2 alone (wider rects end on a lane
+  // boundary: their last strip is shifted to end at the rect's edge)
+  bool edge = false;
+  for (int k = 0; k < n_rect; ++k)
+    if (rects[4 * k + 1] > 0 && rects[4 * k + 3] > 0 && rects[4 * k + 1] < strip_out(K) && rects[4 * k + 1] % 2 == 1)
+      edge = true;
+  if (edge)
+    return exact ? launch_tb<K, true, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
+                 : launch_tb<K, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
+  return exact ? launch_tb<K, true, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
+               : launch_tb<K, false, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
+}
+
+}  // namespace tb
+}  // namespace gmt

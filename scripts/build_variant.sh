@@ -5,6 +5,7 @@
 # LD_LIBRARY_PATH=build/var/NAME: the apps' RUNPATH yields to it).
 #   scripts/build_variant.sh p4 's/constexpr int kP = 6;/constexpr int kP = 4;/'
 #   scripts/build_variant.sh head git:HEAD     (jacobi5tb.hpp as committed at HEAD)
+#   scripts/build_variant.sh b2 file:build/var_src/jacobi5tb_b2.hpp   (a whole edited copy)
 set -e
 cd "$(dirname "$0")/.."
 name=$1; expr=$2
@@ -13,6 +14,7 @@ rm -rf $D && mkdir -p $D/src $D/obj
 cp csrc/kernels/*.hpp csrc/kernels/jacobi5tb*.hip $D/src/
 case "$expr" in
   git:*) git show "${expr#git:}:csrc/kernels/jacobi5tb.hpp" > $D/src/jacobi5tb.hpp ;;
+  file:*) cp "${expr#file:}" $D/src/jacobi5tb.hpp ;;
   *) sed -i "$expr" $D/src/jacobi5tb.hpp ;;
 esac
 cmp -s csrc/kernels/jacobi5tb.hpp $D/src/jacobi5tb.hpp && { echo "sed changed nothing"; exit 1; }

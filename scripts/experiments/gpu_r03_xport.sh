@@ -18,3 +18,7 @@ done
 run 120 halo_ipc2 $M -np 2 build/bin/mpi_halo_bench 16 1024 200 --transport=ipc
 run 120 host_mpi_ceiling $M -np 2 build/bin-host/mpi_halo_bench 65536 16777216 20 --transport=mpi-direct
 grep -E "^ +[0-9]+ +2 |exchange time|===" $OUT/summary.txt
+# oversubscribed bench at 2 ranks: the IPC all-reduces (residual, DAXPY partial sums, 1024-double test_sum)
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
+  bench.py --gpus 2 --size 8192 --steps 20 --warmup 5 --daxpy-n 16777216 --ref-iters 20 > $OUT/bench_n2.json 2> $OUT/bench_n2.err &&
+python -c "import json;d=json.load(open('$OUT/bench_n2.json'));print({k:d[k] for k in ('value','check_max_diff','daxpy_allreduce_us','ref_allreduce_1024_us','daxpy_allsum_rel_err','halo_exchange_us','ref_halo_dim0_us','ref_halo_dim1_us')})"
