@@ -12,7 +12,7 @@
 //   --dims=PYxPX            process grid (default: minimise halo bytes)
 //   --transport=auto|rccl|ipc|mpi-host|mpi-direct
 //   --overlap=auto          time overlapped and serial passes once, keep the faster
-//   --no-overlap --graph --periodic --warmup=W
+//   --no-overlap --graph --periodic[=x|y] --warmup=W
 //   --tblock                temporal blocking (gmt_jacobi5tb): K sweeps per memory pass
 //                           and per (K-wide) halo exchange
 //   --tsteps=K              sweeps per fused pass with --tblock (2-20; default 2; odd
@@ -37,7 +37,7 @@
 using namespace gmt;
 
 // Serial host reference of the same problem (init, boundary, update order).
-static std::vector<double> serial_jacobi(int64_t ny, int64_t nx, int steps, bool periodic) {
+static std::vector<double> serial_jacobi(int64_t ny, int64_t nx, int steps, bool periodic, int axes = 3) {
   const int64_t ld = nx + 2;
   const double h = 1.0 / (static_cast<double>(ny > nx ? ny : nx) + 1);
   std::vector<double> u((ny + 2) * ld), un;
@@ -48,16 +48,16 @@ static std::vector<double> serial_jacobi(int64_t ny, int64_t nx, int steps, bool
     }
   un = u;
   for (int s = 0; s < steps; ++s) {
-    if (periodic) {
+    if (periodic && (axes & 1))
       for (int64_t j = 1; j <= ny; ++j) {
         u[j * ld] = u[j * ld + nx];
         u[j * ld + nx + 1] = u[j * ld + 1];
       }
+    if (periodic && (axes & 2))
       for (int64_t i = 1; i <= nx; ++i) {
         u[i] = u[ny * ld + i];
         u[(ny + 1) * ld + i] = u[ld + i];
       }
-    }
     for (int64_t j = 1; j <= ny; ++j)
       for (int64_t i = 1; i <= nx; ++i) {
         const double* p = &u[j * ld + i];
@@ -98,7 +98,12 @@ int main(int argc, char** argv) {
     c.ny_global *= c.py;
     c.nx_global *= c.px;
   }
-  c.periodic = cli.flag("periodic");
+  // --periodic wraps both axes, --periodic=x / =y one of them
+  c.periodic = cli.has("periodic") && cli.get("periodic", "1") != "0";
+  {
+    const std::string pa = cli.get("periodic", "1");
+    c.periodic_axes = pa == "x" ? 1 : (pa == "y" ? 2 : 3);
+  }
   c.overlap = !cli.flag("no-overlap");
   c.overlap_auto = cli.get("overlap", "") == "auto";  // --overlap=auto: time both, keep the faster
   c.graph = cli.flag("graph");
@@ -149,7 +154,7 @@ int main(int argc, char** argv) {
       MPI_Gatherv(loc.data(), static_cast<int>(loc.size()), MPI_DOUBLE, g.data(), counts.data(),
                   displs.data(), MPI_DOUBLE, 0, MPI_COMM_WORLD);
       if (rank == 0) {
-        std::vector<double> ref = serial_jacobi(c.ny_global, c.nx_global, n_warmup + n_iter, c.periodic);
+        std::vector<double> ref = serial_jacobi(c.ny_global, c.nx_global, n_warmup + n_iter, c.periodic, c.periodic_axes);
         max_diff = 0;
         for (int r = 0; r < world; ++r) {
           const long long oy = all[4 * r], ox = all[4 * r + 1], ny = all[4 * r + 2], nx = all[4 * r + 3];

@@ -48,21 +48,22 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
     abort_job(EXIT_FAILURE);
   }
   auto at = [&](int y, int x) { return y * c.px + x; };
-  nb_.west = cx > 0 ? at(cy, cx - 1) : (c.periodic ? at(cy, c.px - 1) : -1);
-  nb_.east = cx < c.px - 1 ? at(cy, cx + 1) : (c.periodic ? at(cy, 0) : -1);
-  nb_.south = cy > 0 ? at(cy - 1, cx) : (c.periodic ? at(c.py - 1, cx) : -1);
-  nb_.north = cy < c.py - 1 ? at(cy + 1, cx) : (c.periodic ? at(0, cx) : -1);
+  const bool wx = c.periodic && (c.periodic_axes & 1), wy = c.periodic && (c.periodic_axes & 2);
+  nb_.west = cx > 0 ? at(cy, cx - 1) : (wx ? at(cy, c.px - 1) : -1);
+  nb_.east = cx < c.px - 1 ? at(cy, cx + 1) : (wx ? at(cy, 0) : -1);
+  nb_.south = cy > 0 ? at(cy - 1, cx) : (wy ? at(c.py - 1, cx) : -1);
+  nb_.north = cy < c.py - 1 ? at(cy + 1, cx) : (wy ? at(0, cx) : -1);
   // diagonal neighbours: the K-wide corner ghosts travel in the same single
   // exchange phase as the faces (gmt/halo.hpp one-phase corner mode);
   // GMT_HALO_TWO_PHASE=1 restores the two-phase exchange (A/B)
-  auto wrap = [&](int v, int n, bool& ok) {
+  auto wrap = [&](int v, int n, bool periodic, bool& ok) {
     if (v >= 0 && v < n) return v;
-    if (!c.periodic) ok = false;
+    if (!periodic) ok = false;
     return (v + n) % n;
   };
   auto diag = [&](int dy, int dx) {
     bool ok = true;
-    const int y = wrap(cy + dy, c.py, ok), x = wrap(cx + dx, c.px, ok);
+    const int y = wrap(cy + dy, c.py, wy, ok), x = wrap(cx + dx, c.px, wx, ok);
     return ok ? at(y, x) : -1;
   };
   const char* tp = std::getenv("GMT_HALO_TWO_PHASE");
@@ -276,41 +277,43 @@ int JacobiSolver::halo_mask() const {
          (nb_.north >= 0 ? 8 : 0);
 }
 
-void JacobiSolver::xk_launch(int K, int n, const int64_t* rects, int parity, int sig_rects) {
+void JacobiSolver::xk_launch(int K, int n, const int64_t* rects, int parity, int sig_rects, int sig_rows) {
   const double* u = buf_[parity].data();
   double* un = buf_[parity ^ 1].data();
   const int64_t dom[4] = {xo_, nx_, yo_, ny_};
   const int mask = halo_mask();
   unsigned* count = reinterpret_cast<unsigned*>(sig_.data());
-  gmt_tb_opts o{K,         cfg_.wg_waves, cfg_.seg_rows, exact_ ? 1 : 0, sig_rects, sig_rects ? count : nullptr,
-                sig_rects ? sig_.data() + 1 : nullptr};
+  const bool sig = sig_rects > 0 || sig_rows > 0;
+  gmt_tb_opts o{K,   cfg_.wg_waves, cfg_.seg_rows, exact_ ? 1 : 0, sig_rects, sig ? count : nullptr,
+                sig ? sig_.data() + 1 : nullptr, sig_rows};
   GMT_CHECK("jacobi tb", gmt_jacobi5tb(&o, n, rects, dom, mask, u, un, ld_, ny_ + 2 * g_, s_));
 }
 
-// Output rects of a band-first pass: the bands along the halo sides (deep
-// enough for the g_-wide faces and corners the next exchange sends) first,
-// then the interior.  False when the domain is too small for an interior.
-bool JacobiSolver::band_rects(int K, int64_t* rects, int* n_bands) const {
+// Output rects of a band-first pass.  W/E halo sides: full-height bands one
+// workgroup's strips wide (the signalling rects, short segments), first.
+// S/N halo sides: no rects of their own — the main rect's segments next to
+// those sides are its row bands (gmt_tb_opts.signal_rows = g_: dispatched
+// first, N ones walked bottom-up, each output wave signals once its first
+// g_ rows are stored), so the S/N bands cost no extra workgroups or
+// pipeline warm-ups.  False when the domain is too small for the bands.
+bool JacobiSolver::band_rects(int K, int64_t* rects, int* n_bands, int* sig_rows) const {
   const int mask = halo_mask();
   const bool hw = mask & 1, he = mask & 2, hs = mask & 4, hn = mask & 8;
-  // W/E bands: one workgroup's strips wide, so their workgroups are full
   const int64_t wb = std::max<int64_t>(gmt_jacobi5tb_group_cols(K, cfg_.wg_waves), g_);
-  const int64_t hb = g_;
   const int64_t x0 = xo_ + (hw ? wb : 0), x1 = xo_ + nx_ - (he ? wb : 0);
-  const int64_t y0 = yo_ + (hs ? hb : 0), y1 = yo_ + ny_ - (hn ? hb : 0);
-  if (wb <= 0 || x1 - x0 < wb || y1 - y0 < 2 * hb + 64) return false;
+  const int rb = (hs ? 1 : 0) + (hn ? 1 : 0);
+  if (wb <= 0 || x1 - x0 < wb || (rb > 0 && ny_ < rb * std::max<int64_t>(32, g_)) || ny_ < 64) return false;
   int n = 0;
   auto add = [&](int64_t ax, int64_t anx, int64_t ay, int64_t any) {
     const int64_t r[4] = {ax, anx, ay, any};
     std::copy(r, r + 4, rects + 4 * n++);
   };
-  if (hs) add(xo_, nx_, yo_, hb);
-  if (hn) add(xo_, nx_, y1, hb);
-  if (hw) add(xo_, wb, y0, y1 - y0);
-  if (he) add(x1, wb, y0, y1 - y0);
+  if (hw) add(xo_, wb, yo_, ny_);
+  if (he) add(x1, wb, yo_, ny_);
   *n_bands = n;
-  add(x0, x1 - x0, y0, y1 - y0);
-  return n > 0;
+  *sig_rows = rb > 0 ? g_ : 0;
+  add(x0, x1 - x0, yo_, ny_);
+  return n > 0 || rb > 0;
 }
 
 void JacobiSolver::exchange_now(int parity) {
@@ -335,14 +338,14 @@ void JacobiSolver::enqueue_block(int parity, int K) {
   Halo2D& h = *halo_[parity];
   const int64_t dom[4] = {xo_, nx_, yo_, ny_};
   if (!h.active()) {
-    xk_launch(K, 1, dom, parity, 0);
+    xk_launch(K, 1, dom, parity, 0, 0);
     return;
   }
   if (!fresh_[parity]) exchange_now(parity);
   int64_t rects[4 * 5];
-  int nb = 0;
-  if (!cfg_.overlap || !band_rects(K, rects, &nb)) {
-    xk_launch(K, 1, dom, parity, 0);
+  int nb = 0, rows = 0;
+  if (!cfg_.overlap || !band_rects(K, rects, &nb, &rows)) {
+    xk_launch(K, 1, dom, parity, 0, 0);
     fresh_[parity ^ 1] = false;
     return;
   }
@@ -350,7 +353,7 @@ void JacobiSolver::enqueue_block(int parity, int K) {
   // pass), and its wait kernel is enqueued after it
   GMT_CHECK("event", gmt_rt_event_record(ev_start_, s_));
   GMT_CHECK("wait", gmt_rt_stream_wait_event(cs_, ev_start_));
-  xk_launch(K, nb + 1, rects, parity, nb);
+  xk_launch(K, nb + 1, rects, parity, nb, rows);
   GMT_CHECK("signal wait", gmt_signal_wait(sig_.data() + 1, sig_.data() + 2,
                                            reinterpret_cast<unsigned*>(sig_.data() + 3), cs_));
   Halo2D& hn = *halo_[parity ^ 1];
@@ -363,8 +366,8 @@ void JacobiSolver::enqueue_block(int parity, int K) {
 
 bool JacobiSolver::band_mode(int K) const {
   int64_t rects[4 * 5];
-  int nb = 0;
-  return cfg_.overlap && halo_[0] && halo_[0]->active() && band_rects(K, rects, &nb);
+  int nb = 0, rows = 0;
+  return cfg_.overlap && halo_[0] && halo_[0]->active() && band_rects(K, rects, &nb, &rows);
 }
 
 void JacobiSolver::step_block() {

@@ -63,8 +63,13 @@ class Halo2D {
                               (nb.south >= 0 || nb.north >= 0);
     one_phase_ = corner_cells && nb.diagonals_known();
     corners_ = corner_cells && !one_phase_;  // two-phase mode
-    // x faces span the y ghosts too in two-phase corner mode
-    const size_t xrow0 = corners_ ? 0 : gy, xrows = corners_ ? ny_ + 2 * gy : ny_;
+    // x faces span the y ghosts too in two-phase corner mode, and on each y
+    // side without a neighbour when corner cells matter: no diagonal fills
+    // that corner, so it takes the x neighbour's fixed rows (the wrapped ones
+    // on an x-periodic domain)
+    const bool cx = corners && gx > 0 && gy > 0;
+    const bool lo_full = corners_ || (cx && nb.south < 0), hi_full = corners_ || (cx && nb.north < 0);
+    const size_t xrow0 = lo_full ? 0 : gy, xrows = ny_ + (lo_full ? gy : 0) + (hi_full ? gy : 0);
     std::vector<comm::Msg> recvs, sends;
     auto x_face = [&](int peer, size_t send_row, size_t recv_row, int send_tag, int recv_tag) {
       Face fc;

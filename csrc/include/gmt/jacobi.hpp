@@ -43,6 +43,7 @@ struct JacobiConfig {
   int64_t ny_global = 8192, nx_global = 8192;  // global interior extent
   int py = 1, px = 1;                            // process grid (rank = cy*px + cx)
   bool periodic = false;                         // else Dirichlet (fixed ghost ring)
+  int periodic_axes = 3;                         // with periodic: bit0 wraps x (W/E), bit1 wraps y (S/N)
   bool overlap = true;
   // overlap_auto: time a few fused passes with and without overlap at
   // construction (then restore the initial field) and keep the faster — the
@@ -129,8 +130,8 @@ class JacobiSolver {
   void enqueue_step(int parity);
   void enqueue_block(int parity, int k);  // k <= ks_ fused sweeps
   // one fused k-sweep launch on `n` output rects (gmt_jacobi5tb)
-  void xk_launch(int k, int n, const int64_t* rects, int parity, int sig_rects);
-  bool band_rects(int k, int64_t* rects, int* n_bands) const;
+  void xk_launch(int k, int n, const int64_t* rects, int parity, int sig_rects, int sig_rows);
+  bool band_rects(int k, int64_t* rects, int* n_bands, int* sig_rows) const;
   bool band_mode(int k) const;  // the fused k-sweep pass runs band-first (overlap)
   void exchange_now(int parity);  // blocking-order halo exchange of buf_[parity] on the compute stream
   void step_block();

@@ -147,6 +147,14 @@ typedef struct gmt_tb_opts {
   int signal_rects;
   unsigned* signal_count;
   uint64_t* signal;
+  /* Row bands (0 = none): rect signal_rects (the first rect after the
+     signalling ones) keeps its S / N halo sides' segments separate, walks
+     the N ones bottom-up, and dispatches all of them first; each of their
+     output waves counts once toward the same signal after storing its
+     first signal_rows output rows — the rect's signal_rows-deep row bands
+     are ready long before the rect is.  No extra workgroups (the band
+     rects of signal_rects each cost a pipeline warm-up and launch slots). */
+  int signal_rows;
 } gmt_tb_opts;
 int gmt_jacobi5tb_supported(int sweeps);
 /* Largest sweep count whose kernel runs without scratch: GMT_TB_MAX_SWEEPS

@@ -66,6 +66,16 @@ struct Args {
   unsigned* sig_count;
   uint64_t* signal;
   int prio;                      // single-round launch: stage-0 waves at raised priority
+  // row bands (gmt_tb_opts.signal_rows): rect rb_rect's segments next to a
+  // halo row side (S: its first segment of every strip group, N: its last,
+  // walked bottom-up) are dispatched right after the signalling rects; each
+  // of their output waves adds 1 to *sig_count once its first sig_rows
+  // output rows are stored.  sig_total: arrivals that raise *signal (the
+  // signalling rects' workgroups + these waves); sig_dispatch: leading
+  // workgroups dispatched unswizzled.
+  int rb_rect;                   // -1: none
+  int rb_s, rb_n;                // the rect's first / last segments are row bands
+  int64_t sig_rows, sig_total, sig_dispatch;
 };
 
 struct d4 {
@@ -126,10 +136,15 @@ __device__ __forceinline__ u2 pack1(double a) {
 // (rows written by stage 0 two to four steps earlier; this stage runs two
 // steps behind, D = 2, so it can read them before the step barrier).  PE == K: level K is stored to `un`; otherwise level
 // PE goes to the hand-off ring.  Strip output columns [xs, xe), rows [ys, ye).
-template <int K, int PB, int PE, bool EXACT, bool EDGE, bool RULE, bool SYNC>
+// UP walks the segment bottom-up (a row band at the segment's top edge is
+// then output first; a compile-time direction: a runtime one costs the
+// unrolled body its register allocation, tests/test_kernel_resources.py);
+// sig_step >= 0: once that step's row is stored, this (output) wave
+// publishes a row-band arrival (Args::rb_rect).
+template <int K, int PB, int PE, bool EXACT, bool EDGE, bool RULE, bool SYNC, bool UP>
 __device__ __forceinline__ void run_stage(const Args& a, const double* __restrict__ u, double* __restrict__ un,
                                           char* ring, char* hand, int lane, int64_t xs, int64_t xe, int64_t ys,
-                                          int64_t ye, int nsteps) {
+                                          int64_t ye, int nsteps, int sig_step) {
   constexpr bool kIn = PB == 1;
   constexpr bool kOut = PE == K;
   constexpr int D = kIn ? 0 : 2;                  // step lag behind stage 0
@@ -144,9 +159,17 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   const int64_t dy0 = a.dom[2], dy1 = a.dom[2] + a.dom[3];
   const int64_t cf = xs - ring_left(K);  // first column of the strip window
   const int64_t c0 = cf + kNC * lane;    // this lane: columns c0 .. c0+3
-  const int64_t yl = ys - K;             // level-0 row of step 0
+  const int64_t yl = ys - K;             // the window's first row
   const int L = static_cast<int>(ye - ys);
   const uint32_t ld8 = static_cast<uint32_t>(ld) * 8u;
+  // row offsets of step s in the window / in the output: base + s * step
+  // (bottom-up: from the last row, a negative step; rows past either end
+  // wrap to offsets beyond the buffer range: zero-filled / dropped)
+  constexpr bool up = UP;
+  constexpr int dir = UP ? -1 : 1;
+  const uint32_t rstep = up ? 0u - ld8 : ld8;
+  const uint32_t dbase = up ? static_cast<uint32_t>(L + 2 * K - 1) * ld8 : 0u;
+  const uint32_t sbase = up ? static_cast<uint32_t>(L - 1) * ld8 : 0u;
 
   //  loads: rows [yl, min(yl + L + 2K, last_row + 1)), 2048 contiguous bytes
   //  from column cf (a column outside the row wraps into the neighbouring
@@ -157,7 +180,7 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   auto dma = [&](int s, int slot) {
     if constexpr (kIn) {
       char* dst = ring + slot * kSlotBytes;
-      const uint32_t o = static_cast<uint32_t>(s) * ld8;
+      const uint32_t o = dbase + static_cast<uint32_t>(s) * rstep;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst, 16, loff + o, 0, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + 1024, 16, loff + 1024u + o, 0, 0, 0);
     }
@@ -174,9 +197,9 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   const uint32_t stb = (in2 && in3) ? static_cast<uint32_t>(c0 + 2 - xs) * 8u : kDrop;
   const uint32_t stc = (in0 && !in1) ? static_cast<uint32_t>(c0 - xs) * 8u : kDrop;
   const uint32_t std_ = (in2 && !in3) ? static_cast<uint32_t>(c0 + 2 - xs) * 8u : kDrop;
-  auto store_step = [&](int s, const d4& v) {  // level K of step s = output row ys + s - D - 2K
+  auto store_step = [&](int s, const d4& v) {  // level K of step s = output row s - D - 2K of the walk
     if constexpr (kOut) {
-      const uint32_t ro = static_cast<uint32_t>(s - D - 2 * K) * ld8;  // wraps for warm-up rows: out of range
+      const uint32_t ro = sbase + static_cast<uint32_t>(s - D - 2 * K) * rstep;  // warm-up rows: out of range
       __builtin_amdgcn_raw_buffer_store_b128(pack2(v.x, v.y), srs, sta + ro, 0, 2 /* nt */);
       __builtin_amdgcn_raw_buffer_store_b128(pack2(v.z, v.w), srs, stb + ro, 0, 2);
       if constexpr (EDGE) {
@@ -259,14 +282,16 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   };
   load_rows(0);
 
+  // rows of the walk: level p of step s is row rbase(s) - dir * p
+  const int64_t yanchor = up ? ye - 1 + K : yl;
   auto step = [&](auto J, int s) {
     (void)J;
-    const int64_t rbase = yl + s - D;  // level p is row rbase - p
-    d4 v = level(r0, r1, r2, rbase - PB);
+    const int64_t rbase = yanchor + dir * (s - D);
+    d4 v = level(r0, r1, r2, rbase - dir * PB);
     __builtin_amdgcn_sched_barrier(0);
     static_for<PB + 1, PE + 1>([&](auto Q) {
       constexpr int p = decltype(Q)::value;  // PB+1 .. PE, bottom-up
-      const d4 nv = level(W[p - 1 - PB][0], W[p - 1 - PB][1], v, rbase - p);
+      const d4 nv = level(W[p - 1 - PB][0], W[p - 1 - PB][1], v, rbase - dir * p);
       W[p - 1 - PB][0] = W[p - 1 - PB][1];  // rows of steps s-1 and s become s-2 and s-1
       W[p - 1 - PB][1] = v;
       v = nv;
@@ -296,7 +321,25 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   };
 
   constexpr int kU = unroll_for(NL);
-  for (int s0 = 0; s0 < nsteps; s0 += kU) static_for<0, kU>([&](auto J) { step(J, s0 + decltype(J)::value); });
+  for (int s0 = 0; s0 < nsteps; s0 += kU) {
+    static_for<0, kU>([&](auto J) { step(J, s0 + decltype(J)::value); });
+    // A row band's output wave: once the unrolled block holding step
+    // sig_step is done, the band's rows are written — visible device-wide,
+    // then one arrival (the last raises *signal).  Checked at the block
+    // boundary, not per step: the register allocation of the unrolled body
+    // has no room for a branch per step (tests/test_kernel_resources.py).
+    if constexpr (kOut) {
+      if (static_cast<unsigned>(sig_step - s0) < static_cast<unsigned>(kU)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (lane == 0 && __hip_atomic_fetch_add(a.sig_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                             static_cast<unsigned>(a.sig_total - 1)) {
+          __hip_atomic_store(a.sig_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(a.signal, uint64_t{1}, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  }
   // no LDS-DMA may land after the workgroup's LDS is released
   wait_vmcnt<0>();
 }
@@ -316,44 +359,53 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   while (k + 1 < a.n && t >= a.tstart[k + 1]) ++k;
   const int64_t lt = t - a.tstart[k];
   const int64_t ngroups = (a.nstrip[k] + a.nw - 1) / a.nw;
-  // Dispatch order: every workgroup that can hold Dirichlet-rule waves
-  // (~1.5x the VALU per step) goes first, so the launch's tail is made of
-  // fast ones: (A) the edge segments, all strip groups; (B) the interior
-  // segments' first and last strip groups; (C) the rest.
+  // Dispatch order: (R) the row bands of a band-first pass (Args::rb_rect:
+  // every strip group's segment next to a halo row side), then every
+  // workgroup that can hold Dirichlet-rule waves (~1.5x the VALU per step),
+  // so the launch's tail is made of fast ones: (A) the edge segments, all
+  // strip groups; (B) the interior segments' first and last strip groups;
+  // (C) the rest.
   const int64_t ry0 = a.r[k][2], ry1 = a.r[k][2] + a.r[k][3];
   const int64_t e0 = a.e0[k], e1 = a.e1[k];
   const int64_t nedge = (e0 > 0) + (e1 > 0), nbnd = ngroups < 2 ? ngroups : 2;
-  int64_t j, gi;
-  if (lt < nedge * ngroups) {
-    j = lt / ngroups;
+  const int rbs = k == a.rb_rect ? a.rb_s : 0, rbn = k == a.rb_rect ? a.rb_n : 0, rb = rbs + rbn;
+  int64_t gi, m = -1;  // m: interior segment index, -1: edge segment `edge`
+  int edge = 0, dir = 1;
+  bool band = false;
+  if (lt < rb * ngroups) {  // (R): S band = first interior segment, N band = last (walked bottom-up)
     gi = lt % ngroups;
-  } else if (lt < nedge * ngroups + a.nmid_b[k] * nbnd) {
-    const int64_t l2 = lt - nedge * ngroups;
-    j = nedge + l2 / nbnd;
+    const bool north = lt >= ngroups || !rbs;
+    const int64_t nm = (gi == 0 || gi == ngroups - 1) ? a.nmid_b[k] : a.nmid[k];
+    m = north ? nm - 1 : 0;
+    dir = north ? -1 : 1;
+    band = true;
+  } else if (lt < rb * ngroups + nedge * ngroups) {  // (A)
+    const int64_t l1 = lt - rb * ngroups;
+    edge = (l1 / ngroups == 0 && e0 > 0) ? 0 : 1;
+    gi = l1 % ngroups;
+  } else if (lt < rb * ngroups + nedge * ngroups + (a.nmid_b[k] - rb) * nbnd) {  // (B)
+    const int64_t l2 = lt - rb * ngroups - nedge * ngroups;
+    m = rbs + l2 / nbnd;
     gi = l2 % nbnd == 0 ? 0 : ngroups - 1;
-  } else {
-    const int64_t l3 = lt - nedge * ngroups - a.nmid_b[k] * nbnd;
-    j = nedge + l3 / (ngroups - 2);
+  } else {  // (C)
+    const int64_t l3 = lt - rb * ngroups - nedge * ngroups - (a.nmid_b[k] - rb) * nbnd;
+    m = rbs + l3 / (ngroups - 2);
     gi = 1 + l3 % (ngroups - 2);
   }
   const int64_t lmid = (gi == 0 || gi == ngroups - 1) ? a.lmid_b[k] : a.lmid[k];
   int64_t ys, ye;
-  if (e0 > 0 && j == 0) {
-    ys = ry0;
-    ye = ry0 + e0;
+  if (m < 0) {
+    ys = edge == 0 ? ry0 : ry1 - e1;
+    ye = edge == 0 ? ry0 + e0 : ry1;
   } else {
-    if (e0 > 0) --j;
-    if (e1 > 0 && j == 0) {
-      ys = ry1 - e1;
-      ye = ry1;
-    } else {
-      if (e1 > 0) --j;
-      ys = ry0 + e0 + j * lmid;
-      ye = ys + lmid < ry1 - e1 ? ys + lmid : ry1 - e1;
-    }
+    ys = ry0 + e0 + m * lmid;
+    ye = ys + lmid < ry1 - e1 ? ys + lmid : ry1 - e1;
   }
   // L + 2K steps (stage 1 of a split strip runs two steps behind: two more)
   constexpr int kU = unroll_for(G == 1 ? K : stage0_levels(K));
+  // a row band's output wave publishes its arrival at the step that stores
+  // the band's last row (the first sig_rows rows of its walk)
+  const int sig_step = band ? static_cast<int>((G > 1 ? 2 : 0) + 2 * K + a.sig_rows - 1) : -1;
   static_assert(G == 1 || unroll_for(stage0_levels(K)) == unroll_for(K - stage0_levels(K)), "stages step together");
   const int nsteps = static_cast<int>((ye - ys + 2 * K + (G > 1 ? 2 : 0) + kU - 1) / kU * kU);
   const int64_t strip = gi * a.nw + sl;
@@ -374,11 +426,28 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
                     (ys - K < a.dom[2] && !(a.mask & 4)) || (ye + K > a.dom[2] + a.dom[3] && !(a.mask & 8));
   char* ring = reinterpret_cast<char*>(lds_dyn) + sl * strip_lds(G);
   char* hand = ring + kRS * kSlotBytes;
+  // one instantiation per (stage, rule path, direction); the direction is
+  // bottom-up only for the N row bands
+  auto go = [&](auto pb, auto pe, auto sync, auto rule_c, auto up_c, int sstep) {
+    run_stage<K, decltype(pb)::value, decltype(pe)::value, EXACT, EDGE, decltype(rule_c)::value,
+              decltype(sync)::value, decltype(up_c)::value>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps,
+                                                            sstep);
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  auto stage_go = [&](auto pb, auto pe, auto sync, int sstep) {
+    if (dir < 0) {
+      if (rule) go(pb, pe, sync, T{}, T{}, sstep);
+      else go(pb, pe, sync, F{}, T{}, sstep);
+    } else {
+      if (rule) go(pb, pe, sync, T{}, F{}, sstep);
+      else go(pb, pe, sync, F{}, F{}, sstep);
+    }
+  };
+  using C1 = std::integral_constant<int, 1>;
+  using CK = std::integral_constant<int, K>;
   if constexpr (G == 1) {
-    if (rule)
-      run_stage<K, 1, K, EXACT, EDGE, true, false>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
-    else
-      run_stage<K, 1, K, EXACT, EDGE, false, false>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
+    stage_go(C1{}, CK{}, F{}, sig_step);
   } else {
     constexpr int KA = stage0_levels(K);
     if (stage == 0) {
@@ -386,15 +455,9 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
       // while a strip's stage 1 waits on its stage 0: favour the producer
       // (profiles/r02_tb.md 9.4)
       if (a.prio) __builtin_amdgcn_s_setprio(2);
-      if (rule)
-        run_stage<K, 1, KA, EXACT, EDGE, true, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
-      else
-        run_stage<K, 1, KA, EXACT, EDGE, false, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
+      stage_go(C1{}, std::integral_constant<int, KA>{}, T{}, -1);
     } else {
-      if (rule)
-        run_stage<K, KA + 1, K, EXACT, EDGE, true, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
-      else
-        run_stage<K, KA + 1, K, EXACT, EDGE, false, true>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps);
+      stage_go(std::integral_constant<int, KA + 1>{}, CK{}, T{}, sig_step);
     }
   }
 }
@@ -402,11 +465,11 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
 template <int K, bool EXACT, bool EDGE>
 __global__ __launch_bounds__(kMaxThreads) __attribute__((amdgpu_waves_per_eu(2)))
 void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__ un, int64_t nblocks) {
-  const int64_t ns = a.sig_wgs;
+  const int64_t ns = a.sig_wgs, nd = a.sig_dispatch;
   const int64_t b = blockIdx.x;
-  // signalling workgroups first, in dispatch order over all XCDs; the rest
-  // XCD-contiguous
-  const int64_t t = b < ns ? b : ns + xcd_swizzle(b - ns, nblocks - ns);
+  // signalling workgroups (and row bands) first, in dispatch order over all
+  // XCDs; the rest XCD-contiguous
+  const int64_t t = b < nd ? b : nd + xcd_swizzle(b - nd, nblocks - nd);
   tb_block<K, EXACT, EDGE>(a, u, un, t);
   if (t < ns) {
     // every wave's stores written back past its XCD's L2, then one arrival
@@ -415,7 +478,7 @@ void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__
     __syncthreads();
     if (threadIdx.x == 0 &&
         __hip_atomic_fetch_add(a.sig_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-            static_cast<unsigned>(ns - 1)) {
+            static_cast<unsigned>(a.sig_total - 1)) {
       __hip_atomic_store(a.sig_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add(a.signal, uint64_t{1}, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -447,13 +510,18 @@ struct SegPlan {
 // Signalling rects (k < sig_rects: the boundary bands of a pass whose halo
 // exchange overlaps the rest of it) get short segments, max(128, L/3) rows
 // and no edge split: their workgroups must finish early in the launch.
+// A row-band rect (rb_rect, gmt_tb_opts.signal_rows) keeps at least `rb`
+// interior segments per strip group, each at least rb_min rows long, so its
+// S and N bands are separate segments that finish early.
 template <int K>
-SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t resident_wgs, int sig_rects) {
+SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t resident_wgs, int sig_rects, int rb_rect = -1,
+                      int rb = 0, int64_t rb_min = 0) {
   SegPlan p{};
   const int64_t edge = std::max<int64_t>(64, K);
-  auto fill = [&](int64_t L, int64_t* wgs) {
+  auto fill = [&](int64_t L0, int64_t* wgs) {
     int64_t w = 0;
     for (int k = 0; k < a.n; ++k) {
+      int64_t L = L0;
       const int64_t ny = a.r[k][3], ry0 = a.r[k][2], ry1 = ry0 + ny;
       if (k < sig_rects) {
         const int64_t lb = std::min<int64_t>(std::max<int64_t>(128, L / 3), lmax);
@@ -471,6 +539,7 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
         p.e1[k] = bot ? edge : 0;
       }
       const int64_t mid = ny - p.e0[k] - p.e1[k];
+      if (k == rb_rect && rb > 0) L = std::min<int64_t>(L, std::max<int64_t>(rb_min, mid / rb));
       p.nmid[k] = (mid + L - 1) / L;
       p.lmid[k] = (mid + p.nmid[k] - 1) / p.nmid[k];  // balanced lengths
       // strip groups that can reach a Dirichlet column run the rule path
@@ -479,7 +548,8 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
       const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
       const bool xrule = seg_rows == 0 && ((rx0 - ring_left(K) < a.dom[0] && !(a.mask & 1)) ||
                                            (rx1 + ring_left(K) > a.dom[0] + a.dom[1] && !(a.mask & 2)));
-      const int64_t lb = xrule ? std::max<int64_t>(64, p.lmid[k] / 2) : p.lmid[k];
+      int64_t lb = xrule ? std::max<int64_t>(64, p.lmid[k] / 2) : p.lmid[k];
+      if (k == rb_rect && rb > 0) lb = std::min<int64_t>(lb, std::max<int64_t>(rb_min, mid / rb));
       p.nmid_b[k] = (mid + lb - 1) / lb;
       p.lmid_b[k] = (mid + p.nmid_b[k] - 1) / p.nmid_b[k];
       const int64_t groups = (a.nstrip[k] + a.nw - 1) / a.nw, nbnd = groups < 2 ? groups : 2;
@@ -569,7 +639,13 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     if (slot) slot->store(per_cu, std::memory_order_relaxed);
   }
   const int sig_rects = o.signal_rects;  // non-empty rects (checked): the same indices after the compaction
-  const SegPlan sp = plan_segments<K>(a, o.seg_rows, lmax, per_cu, sig_rects);
+  // row bands: the first rect after the signalling ones (checked non-empty)
+  const int rbk = o.signal_rows > 0 ? sig_rects : -1;
+  const int rbs = rbk >= 0 && (mask & 4) ? 1 : 0, rbn = rbk >= 0 && (mask & 8) ? 1 : 0;
+  const int64_t rb_min = std::max<int64_t>(32, o.signal_rows);
+  if (rbk >= 0 && (rbk >= a.n || rbs + rbn == 0 || a.r[rbk][3] < (rbs + rbn) * rb_min))
+    return static_cast<int>(hipErrorInvalidValue);
+  const SegPlan sp = plan_segments<K>(a, o.seg_rows, lmax, per_cu, sig_rects, rbk, rbs + rbn, rb_min);
   a.tstart[0] = 0;
   for (int k = 0; k < a.n; ++k) {
     a.e0[k] = sp.e0[k];
@@ -585,6 +661,24 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   for (int k = a.n + 1; k <= kMaxRect; ++k) a.tstart[k] = a.tstart[a.n];
   const int64_t nb = a.tstart[a.n];
   a.sig_wgs = a.tstart[sig_rects];
+  a.rb_rect = -1;
+  a.sig_total = a.sig_wgs;
+  a.sig_dispatch = a.sig_wgs;
+  if (rbk >= 0) {
+    // the band segments exist separately: halo row sides have no edge
+    // segments, and the planner kept >= rbs + rbn interior segments of >= rb_min rows
+    const int rb = rbs + rbn;
+    if ((rbs && sp.e0[rbk] > 0) || (rbn && sp.e1[rbk] > 0) || sp.nmid[rbk] < rb || sp.nmid_b[rbk] < rb ||
+        (sp.nmid[rbk] > 1 && sp.lmid[rbk] < o.signal_rows) || (sp.nmid_b[rbk] > 1 && sp.lmid_b[rbk] < o.signal_rows))
+      return static_cast<int>(hipErrorInvalidValue);
+    a.rb_rect = rbk;
+    a.rb_s = rbs;
+    a.rb_n = rbn;
+    a.sig_rows = o.signal_rows;
+    const int64_t groups = (a.nstrip[rbk] + a.nw - 1) / a.nw;
+    a.sig_total += rb * a.nstrip[rbk];   // one arrival per output wave (= strip) of every band
+    a.sig_dispatch += rb * groups;       // rect rbk's band tiles follow the signalling rects
+  }
   a.prio = nb <= per_cu ? 1 : 0;
   a.sig_count = o.signal_count;
   a.signal = o.signal;

@@ -291,6 +291,16 @@ def test_mpi_stencil2d_sycl_oo_strong_scaling_and_debug():
     (["--ny=400", "--nx=300", "0", "17", "--tblock", "--tsteps=8", "--wg-strips=1", "--dims=2x1",
       "--transport=mpi-host"], 2),
     (["--ny=130", "--nx=800", "0", "11", "--tblock", "--tsteps=5", "--wg-strips=1", "--periodic"], 1),
+    # one periodic axis: y-only gives S/N-only shares (row bands, no W/E
+    # bands); x-only needs the x faces to carry the corner rows when the rank
+    # has no y neighbours (Halo2D x_full)
+    (["--ny=300", "--nx=700", "0", "13", "--tblock", "--tsteps=6", "--wg-strips=1", "--dims=2x1",
+      "--periodic=y", "--transport=ipc"], 2),
+    (["--ny=260", "--nx=900", "0", "9", "--tblock", "--tsteps=4", "--wg-strips=1", "--periodic=y"], 1),
+    (["--ny=200", "--nx=1600", "0", "11", "--tblock", "--tsteps=5", "--wg-strips=1", "--dims=1x2",
+      "--periodic=x", "--transport=ipc"], 2),
+    (["53", "9", "--tblock", "--dims=2x2", "--periodic=x"], 4),
+    (["47", "7", "--dims=1x3", "--periodic=y", "--transport=mpi-host"], 3),
 ])
 def test_mpi_jacobi2d_matches_serial(args, np_):
     out = run_app("mpi_jacobi2d", *args, "--check", "--warmup=2", "--halo-iters=3", np=np_).stdout
