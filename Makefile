@@ -148,7 +148,7 @@ asan-host:
 
 # tuning harnesses (standalone, not part of the libraries): stream_sweep, and
 # variant_bench — the A/B kernel variants checked and timed against libgmt
-sweep: $(BUILD)/bench/stream_sweep $(BUILD)/bench/variant_bench
+sweep: $(BUILD)/bench/stream_sweep $(BUILD)/bench/variant_bench $(BUILD)/bench/d1_walk
 $(BUILD)/bench/stream_sweep: csrc/bench/stream_sweep.hip
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
@@ -156,6 +156,10 @@ $(BUILD)/bench/variant_bench: csrc/bench/variant_bench.hip $(KERNEL_HDRS) $(LIB)
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Icsrc/include -o $@ $< -L$(LIBDIR) -lgmt \
 	  -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
+
+$(BUILD)/bench/d1_walk: csrc/bench/d1_walk.hip csrc/kernels/stencil5_d1.hpp csrc/kernels/common.hpp
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Icsrc/include -o $@ $<
 
 .SECONDARY:
 

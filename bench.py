@@ -395,6 +395,20 @@ def main(argv=None):
             extras["halo_exchange_us"] = round(t * 1e6, 2)
             extras["halo_exchange_kind"] = (f"1-rank periodic {kind} self-exchange, {tsteps}-wide faces + "
                                             f"corners of the {shape[0]}x{shape[1]} field ({nbytes} bytes)")
+        # the other orientation of a non-square process grid (BASELINE names
+        # "2x4"; choose_dims may pick 4x2): the same run with PY and PX
+        # swapped, so both rates are on record (profiles/r03_shares.md)
+        hp, hx = info["dims"]
+        if env.world_size > 1 and hp != hx and args.scaling == "strong":
+            eng3, dt3, info3 = bench_native(env, shape, args.steps, args.warmup, overlap, (hx, hp), graph,
+                                            tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows,
+                                            args.init, args.seed, not args.no_calibrate)
+            eng3.close()
+            extras["stencil_alt_dims"] = f"{hx}x{hp}"
+            extras["stencil_alt_dims_MLUPS"] = round(points * args.steps / dt3 / 1e6, 1)
+            extras["stencil_alt_dims_overlap"] = info3["overlap"]
+            if env.is_gpu:
+                torch.cuda.empty_cache()
         if args.small_size:
             s2 = (args.small_size, args.small_size)
             steps2 = max(100, 4 * args.steps)

@@ -82,6 +82,9 @@ def test_bench_two_ranks_torchrun_cpu(transport):
     assert rec["ref_halo_dim0_err_norm"] < 1e-6 and rec["ref_halo_dim1_err_norm"] < 1e-6
     assert rec["ref_halo_dim0_rel_err"] < 1e-9 and rec["ref_halo_dim1_rel_err"] < 1e-9
     assert rec["ref_allreduce_1024_us"] > 0
+    # the swapped orientation of the non-square process grid is on record too
+    py, px = (int(v) for v in rec["config"]["parallelism"].split(",")[0].replace("spatial2d py", "").split(" x px"))
+    assert rec["stencil_alt_dims"] == f"{px}x{py}" and rec["stencil_alt_dims_MLUPS"] > 0
 
 
 def test_bench_two_ranks_weak_scaling_cpu():
