@@ -14,6 +14,8 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--last", type=int, default=200)
     ap.add_argument("--skip-tail", type=int, default=6, help="drop the final N dispatches (residual etc.)")
+    ap.add_argument("--timeline", default="", help="also list every dispatch whose name contains this "
+                    "(duration, gap to the previous one of them): clock drift over back-to-back passes")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -41,6 +43,15 @@ def main():
             ce = max(ce, e)
     busy += ce - cs
     print(f"busy {busy / 1e3:.1f} us, idle {(t1 - t0 - busy) / 1e3:.1f} us")
+    if a.timeline:
+        prev = None
+        for r in rows:
+            if a.timeline not in r["Kernel_Name"]:
+                continue
+            s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            gap = (s0 - prev) / 1e3 if prev is not None else 0.0
+            print(f"  {(e0 - s0) / 1e3:9.1f} us  gap {gap:8.1f} us  {r['Kernel_Name'].split('(')[0].replace('void ', '')}")
+            prev = e0
 
 
 if __name__ == "__main__":
