@@ -1,0 +1,910 @@
+// Temporal-blocking Jacobi kernel and its launch code (see jacobi5tb.hip for
+// the design).  Included by the jacobi5tb_k*.hip translation units, each of
+// which instantiates dispatch_k for a few K: the fully unrolled register
+// pipelines take minutes per K to compile, so they build in parallel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <utility>
+
+#include "common.hpp"
+#include "gmt/kernels.h"
+
+namespace gmt {
+namespace tb {
+
+constexpr int kMaxRect = 8;
+constexpr int kMaxThreads = 512;              // 8 waves: 2 per SIMD
+constexpr int kNC = 4;                        // columns per lane
+constexpr int kCols = kNC * kWave;            // 256 columns per strip
+constexpr uint32_t kRowBytes = kCols * 8;     // one row of a strip: 2 KB
+constexpr uint32_t kSlotBytes = kRowBytes;    // DMA ring slot: two full-wave 16-B DMAs
+constexpr uint32_t kDrop = 0x80000000u;       // buffer offset past num_records: no-op access
+constexpr int kP = 6;                         // input rows in flight
+constexpr int kRS = kP + 2;                   // DMA ring: rows s-2..s in use, s+1..s+P-1 in flight
+constexpr int kHS = 6;                        // hand-off ring (2 stages): rows of steps s-4..s
+constexpr int kMaxK1 = 10;                    // largest single-wave K
+static_assert(kHS >= 5, "hand ring: rows of steps s-4..s");
+
+constexpr int n_stages(int K) { return K <= kMaxK1 ? 1 : 2; }
+constexpr int stage0_levels(int K) { return (K + 1) / 2; }
+// Two-stage strips run in PAIRS: the two 256-column windows of a workgroup
+// sit side by side and trade their inner edge column of every level through
+// LDS, so a pair computes 512 columns and outputs 512 - 2 KL instead of two
+// strips' 2 (256 - 2 KL): 464 instead of 432 output columns per 512
+// computed at K = 20 (the recomputed overlap is most of the VALU the kernel
+// spends beyond its arithmetic, profiles/r03_pair.md).
+constexpr int kPair = 2;
+// KL: the margin each outer side of a window loses (a multiple of 4, so the
+// output edges fall on lane boundaries).  A pair keeps one lane more than K
+// needs: its outermost lane is then outside every output cone at EVERY
+// level, level 0 included, and serves as the scratch slot the neighbour's
+// edge value is loaded into (run_stage PAIR).
+constexpr int ring_left(int K) { return n_stages(K) > 1 ? (K + 2 * kNC - 1) / kNC * kNC : (K + kNC - 1) / kNC * kNC; }
+constexpr int strip_span(int K) { return n_stages(K) > 1 ? kPair * kCols : kCols; }
+constexpr int strip_out(int K) { return strip_span(K) - 2 * ring_left(K); }
+// Unroll of the step loop: the register cycle of the pipeline.  A level's
+// new row is live while its step-(s-2) row is still being read, so a step
+// frees one d4 at the top level and the rows move up one register slot per
+// step: a value's register passes through the two slots of each of the
+// NL - 1 stored levels plus the spare, 2(NL - 1) + 1 steps.  Unrolling by
+// exactly that lets the allocator keep every row in place (no copies at the
+// back edge) at 16 VGPRs per level; ring slots are then computed per step.
+constexpr int unroll_for(int NL) { return NL > 1 ? 2 * (NL - 1) + 1 : 2; }
+
+struct Args {
+  int64_t r[kMaxRect][4];        // output rects: x0, nx, y0, ny (absolute)
+  int64_t nstrip[kMaxRect];      // strips per rect
+  int64_t tstart[kMaxRect + 1];  // prefix sum of workgroups
+  int64_t dom[4];                // interior x0, nx, y0, ny
+  int64_t ld;                    // row pitch (elements)
+  int64_t last_row;              // last allocated row (load clamp)
+  int n;                         // rects
+  int mask;                      // halo sides: bit0..3 = W/E/S/N
+  // segments of rect k: an optional top edge segment of e0[k] rows and a
+  // bottom one of e1[k] rows (short: the only ones whose waves can need the
+  // Dirichlet rule in y), then nmid[k] interior segments of lmid[k] rows
+  int64_t e0[kMaxRect], e1[kMaxRect], nmid[kMaxRect], lmid[kMaxRect];
+  // the first and last strip groups (rule waves where a Dirichlet column is
+  // in reach) use their own, shorter interior segments
+  int64_t nmid_b[kMaxRect], lmid_b[kMaxRect];
+  int nw;                        // strips per workgroup
+  double quarter;                // 0.25 (EXACT): an SGPR operand
+  // completion signal of the leading workgroups (gmt_tb_opts.signal_rects):
+  // workgroups t < sig_wgs are dispatched first, unswizzled; the last of
+  // them to finish adds 1 to *signal once its stores are visible device-wide
+  int64_t sig_wgs;
+  unsigned* sig_count;
+  uint64_t* signal;
+  int prio;                      // single-round launch: stage-0 waves at raised priority
+  // row bands (gmt_tb_opts.signal_rows): rect rb_rect's segments next to a
+  // halo row side (S: its first segment of every strip group, N: its last,
+  // walked bottom-up) are dispatched right after the signalling rects; each
+  // of their output waves adds 1 to *sig_count once its first sig_rows
+  // output rows are stored.  sig_total: arrivals that raise *signal (the
+  // signalling rects' workgroups + these waves); sig_dispatch: leading
+  // workgroups dispatched unswizzled.
+  int rb_rect;                   // -1: none
+  int rb_s, rb_n;                // the rect's first / last segments are row bands
+  int64_t sig_rows, sig_total, sig_dispatch;
+};
+
+struct d4 {
+  double x, y, z, w;
+};
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double* p, uint32_t bytes) {
+  // 0x00020000: raw-buffer descriptor word 3 for gfx9 (32-bit data format)
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(p), 0, bytes, 0x00020000);
+}
+
+// LDS per strip: the DMA ring, plus the hand-off ring with 2 stages
+__host__ __device__ constexpr int64_t strip_lds(int stages) {
+  return static_cast<int64_t>(kRS) * kSlotBytes + (stages > 1 ? kHS * kRowBytes : 0);
+}
+// Edge hand-off ring of a pair: [slot][writer side][component][level]
+// doubles (run_stage: a strip stores both end components of its edge lane,
+// the reader takes the one that is its neighbour's edge column), one slot
+// per step of the unrolled step block (a block starts at a multiple of its
+// length, so step s uses slot s mod kU = its position in the block: every
+// address is a compile-time offset from one base register).
+template <int K>
+__host__ __device__ constexpr int64_t edge_bytes() {
+  return n_stages(K) > 1 ? static_cast<int64_t>(unroll_for(stage0_levels(K))) * 4 * K * 8 : 0;
+}
+// LDS per workgroup unit: one strip (one stage), or a pair of two-stage
+// strips and their edge hand-off ring
+template <int K>
+__host__ __device__ constexpr int64_t unit_lds() {
+  return n_stages(K) > 1 ? kPair * strip_lds(2) + edge_bytes<K>() : strip_lds(1);
+}
+
+// One lane's 8-B LDS store / load, with no branch: the exec mask is swapped
+// inside one asm statement, so the unrolled pipeline stays one basic block
+// (a divergent `if (lane == ...)` splits it per level and breaks the
+// register cycle of the allocation).  The load writes its register in place
+// ("+v": the other lanes keep their values) and is not tracked by the
+// compiler's lgkmcnt accounting: lds_wait() before the value is used.  An
+// LDS op the compiler does not count only makes its own waits conservative.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  typedef __attribute__((address_space(3))) const char* lds_cptr;
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_cptr)(p)));
+}
+// Both run with the whole wave active (the pipelines have no divergent
+// branch) and restore exec to all lanes: no SGPRs for a saved mask (SGPR
+// pressure spills the pipelines' VGPRs, through the v_writelane slots).
+template <uint32_t OFF>
+__device__ __forceinline__ void lds_store_lane(uint32_t addr, double v, uint64_t lane_mask) {
+  static_assert(OFF < 65536, "ds offset");
+  asm volatile(
+      "s_mov_b64 exec, %0\n\t"
+      "ds_write_b64 %1, %2 offset:%3\n\t"
+      "s_mov_b64 exec, -1"
+      :
+      : "s"(lane_mask), "v"(addr), "v"(v), "n"(OFF));
+}
+// a lane's 32 B of a hand-off row, by every lane but the scratch lane (the
+// bit reverse of `edge_mask`)
+__device__ __forceinline__ void lds_store_row_noscratch(uint32_t addr, d2 a, d2 b, uint64_t edge_mask) {
+  asm volatile(
+      "s_brev_b64 exec, %0\n\t"
+      "s_not_b64 exec, exec\n\t"
+      "ds_write_b128 %1, %2\n\t"
+      "ds_write_b128 %1, %3 offset:16\n\t"
+      "s_mov_b64 exec, -1"
+      :
+      : "s"(edge_mask), "v"(addr), "v"(a), "v"(b));
+}
+// (the exec mask is the bit-reverse of `lane_mask`: lane 0 <-> lane 63)
+template <uint32_t OFF>
+__device__ __forceinline__ void lds_load_lane(uint32_t addr, double& v, uint64_t lane_mask) {
+  static_assert(OFF < 65536, "ds offset");
+  asm volatile(
+      "s_brev_b64 exec, %1\n\t"
+      "ds_read_b64 %0, %2 offset:%3\n\t"
+      "s_mov_b64 exec, -1"
+      : "+v"(v)
+      : "s"(lane_mask), "v"(addr), "n"(OFF));
+}
+// every LDS op of this wave complete; `v` is tied so its uses stay after it
+__device__ __forceinline__ void lds_wait(double& a, double& b) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b)); }
+// a uniform value in a VGPR the compiler cannot rematerialise (an LDS base
+// address used by many asm operands: no v_mov per use)
+__device__ __forceinline__ uint32_t to_vgpr(uint32_t x) {
+  uint32_t r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+  return r;
+}
+
+// Whole-wave rotates (wave_rol:1 / wave_ror:1): the edge lane takes the
+// other end's value — a pair's scratch column, holding the neighbour's
+// edge column (run_stage PAIR)
+__device__ __forceinline__ double dpp_rot_from_upper(double v) {  // lane i <- lane i+1, lane 63 <- lane 0
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x134, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x134, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_rot_from_lower(double v) {  // lane i <- lane i-1, lane 0 <- lane 63
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x13c, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x13c, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+
+// s_waitcnt vmcnt(n) only (expcnt / lgkmcnt left at their maxima), as a
+// compiler barrier for memory: the LDS-DMA'd rows are read by ds_read after
+// it, and the compiler does not track LDS-DMA -> ds_read dependencies
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// hand-off rows written by this wave are visible to the workgroup after it.
+// Outstanding DMAs and stores are not waited for (gfx950 has the back-off
+// barrier, so s_barrier needs no vmcnt(0)).
+__device__ __forceinline__ void step_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ d4 lds_row(const char* slot, int lane) {
+  const d2* p = reinterpret_cast<const d2*>(slot) + 2 * lane;
+  const d2 a = p[0], b = p[1];
+  return d4{a.x, a.y, b.x, b.y};
+}
+
+__device__ __forceinline__ u4 pack2(double a, double b) {
+  return u4{static_cast<unsigned>(__double2loint(a)), static_cast<unsigned>(__double2hiint(a)),
+            static_cast<unsigned>(__double2loint(b)), static_cast<unsigned>(__double2hiint(b))};
+}
+__device__ __forceinline__ u2 pack1(double a) {
+  return u2{static_cast<unsigned>(__double2loint(a)), static_cast<unsigned>(__double2hiint(a))};
+}
+
+// One wave = one stage of one strip: levels PB..PE of the K-level pipeline.
+// PB == 1: level 0 comes from the DMA ring; otherwise from the hand-off ring
+// (rows written by stage 0 two to four steps earlier; this stage runs two
+// steps behind, D = 2, so it can read them before the step barrier).  PE == K: level K is stored to `un`; otherwise level
+// PE goes to the hand-off ring.  Strip output columns [xs, xe), rows [ys, ye).
+// UP walks the segment bottom-up (a row band at the segment's top edge is
+// then output first; a compile-time direction: a runtime one costs the
+// unrolled body its register allocation, tests/test_kernel_resources.py);
+// sig_step >= 0: once that step's row is stored, this (output) wave
+// publishes a row-band arrival (Args::rb_rect).
+// PAIR: false = a lone strip (DPP shifts, edge lanes read 0); true = one
+// strip of a pair (`right`: which one).  The inner edge lane (left: 63,
+// right: 0) needs the other strip's edge column; both edge lanes take their
+// W / E value from a whole-wave DPP ROTATE, i.e. out of the other end of the
+// wave, and the strip's outermost column (left: lane 0's x, right: lane
+// 63's w) is a scratch slot — outside every output cone at every level
+// (ring_left) — into which that one lane LOADS the neighbour's column before
+// a level reads it: for level PB from the neighbour's ring (hand) row, for
+// later levels from the edge hand-off ring (base xbv), which each strip
+// fills with its own edge column of every level it computes (one lane, one
+// 8-B LDS store).  The outer edge lane's rotated value is garbage, as the
+// shifted-in 0 was.  No VALU is added (the rotates replace the shifts, the
+// loads and stores go to the LDS pipe, the step barrier orders them), and
+// both strips run the same code: the side is only in exec masks and
+// addresses (a second instantiation per side spills the whole kernel: the
+// allocator handles 8 unrolled pipelines in one function, not 16).
+// cf: first column of the wave's window.
+template <int K, int PB, int PE, bool EXACT, bool EDGE, bool RULE, bool SYNC, bool UP, bool PAIR>
+__device__ __forceinline__ void run_stage(const Args& a, const double* __restrict__ u, double* __restrict__ un,
+                                          char* ring, char* hand, const char* nring, const char* nhand,
+                                          uint32_t xbv, bool right, int lane, int64_t cf, int64_t xs, int64_t xe,
+                                          int64_t ys, int64_t ye, int nsteps, int sig_step) {
+  constexpr bool kIn = PB == 1;
+  constexpr bool kOut = PE == K;
+  constexpr int D = kIn ? 0 : 2;                  // step lag behind stage 0
+  constexpr int SPS = kOut ? (EDGE ? 4 : 2) : 0;  // global stores per step
+  constexpr int DPS = kIn ? 2 : 0;                // DMAs per step
+  // every kernel argument the loop needs, as values: the asm memory clobbers
+  // below would otherwise force a reload of the kernarg segment per use
+  const int64_t ld = a.ld;
+  const int mask = a.mask;
+  const double quarter = a.quarter;
+  const int64_t dx0 = a.dom[0], dx1 = a.dom[0] + a.dom[1];
+  const int64_t dy0 = a.dom[2], dy1 = a.dom[2] + a.dom[3];
+  static_assert(!PAIR || SYNC, "a pair's edge hand-off needs the step barrier");
+  const int64_t c0 = cf + kNC * lane;    // this lane: columns c0 .. c0+3
+  const int64_t yl = ys - K;             // the window's first row
+  const int L = static_cast<int>(ye - ys);
+  const uint32_t ld8 = static_cast<uint32_t>(ld) * 8u;
+  // row offsets of step s in the window / in the output: base + s * step
+  // (bottom-up: from the last row, a negative step; rows past either end
+  // wrap to offsets beyond the buffer range: zero-filled / dropped)
+  constexpr bool up = UP;
+  constexpr int dir = UP ? -1 : 1;
+  const uint32_t rstep = up ? 0u - ld8 : ld8;
+  const uint32_t dbase = up ? static_cast<uint32_t>(L + 2 * K - 1) * ld8 : 0u;
+  const uint32_t sbase = up ? static_cast<uint32_t>(L - 1) * ld8 : 0u;
+
+  //  loads: rows [yl, min(yl + L + 2K, last_row + 1)), 2048 contiguous bytes
+  //  from column cf (a column outside the row wraps into the neighbouring
+  //  row or is zero-filled: garbage outside every output cone)
+  const int64_t nrow_in = std::min<int64_t>(L + 2 * K, a.last_row + 1 - yl);
+  const __amdgpu_buffer_rsrc_t lrs = row_rsrc(u + yl * ld, static_cast<uint32_t>(nrow_in) * ld8);
+  const uint32_t loff0 = static_cast<uint32_t>(cf) * 8u + static_cast<uint32_t>(lane) * 16u;
+  // a pair's scratch lane loads the neighbour's edge column in place of its
+  // own outermost one (the DMA source is per lane, its LDS destination is
+  // not): the left's lane 0 takes columns 256-257 as its 0-1, the right's
+  // lane 63 columns -2..-1 as its 254-255 — level 0 arrives patched
+  const uint32_t loff = loff0 + (PAIR && !right && lane == 0 ? 2048u : 0u);
+  const uint32_t loffb = loff0 + 1024u - (PAIR && right && lane == kWave - 1 ? 2048u : 0u);
+  auto dma = [&](int s, int slot) {
+    if constexpr (kIn) {
+      char* dst = ring + slot * kSlotBytes;
+      const uint32_t o = dbase + static_cast<uint32_t>(s) * rstep;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst, 16, loff + o, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + 1024, 16, loffb + o, 0, 0, 0);
+    }
+  };
+  //  stores: rows [ys, ye) from column xs.  The left output edge is a lane
+  //  boundary (KL = 0 mod 4): 16-B stores of columns 0-1 and 2-3 where both
+  //  are inside, and (EDGE: a rect of the launch ends inside a lane at an odd
+  //  column) 8-B stores of column 0 or 2 alone.  Lanes with nothing to store
+  //  get an offset past any row (dropped).
+  const __amdgpu_buffer_rsrc_t srs = row_rsrc(un + ys * ld + xs, static_cast<uint32_t>(L) * ld8);
+  const bool in0 = c0 >= xs && c0 < xe, in1 = c0 + 1 >= xs && c0 + 1 < xe;
+  const bool in2 = c0 + 2 >= xs && c0 + 2 < xe, in3 = c0 + 3 >= xs && c0 + 3 < xe;
+  const uint32_t sta = (in0 && in1) ? static_cast<uint32_t>(c0 - xs) * 8u : kDrop;
+  const uint32_t stb = (in2 && in3) ? static_cast<uint32_t>(c0 + 2 - xs) * 8u : kDrop;
+  const uint32_t stc = (in0 && !in1) ? static_cast<uint32_t>(c0 - xs) * 8u : kDrop;
+  const uint32_t std_ = (in2 && !in3) ? static_cast<uint32_t>(c0 + 2 - xs) * 8u : kDrop;
+  auto store_step = [&](int s, const d4& v) {  // level K of step s = output row s - D - 2K of the walk
+    if constexpr (kOut) {
+      const uint32_t ro = sbase + static_cast<uint32_t>(s - D - 2 * K) * rstep;  // warm-up rows: out of range
+      __builtin_amdgcn_raw_buffer_store_b128(pack2(v.x, v.y), srs, sta + ro, 0, 2 /* nt */);
+      __builtin_amdgcn_raw_buffer_store_b128(pack2(v.z, v.w), srs, stb + ro, 0, 2);
+      if constexpr (EDGE) {
+        __builtin_amdgcn_raw_buffer_store_b64(pack1(v.x), srs, stc + ro, 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b64(pack1(v.z), srs, std_ + ro, 0, 2);
+      }
+    }
+  };
+
+  // Dirichlet rule (RULE only): a cell outside the interior on a side whose
+  // ghost ring is fixed keeps its value at every level
+  const bool gw = mask & 1, ge = mask & 2, gs = mask & 4, gn = mask & 8;
+  auto kept_col = [&](int64_t c) { return (c < dx0 && !gw) || (c >= dx1 && !ge); };
+  const bool kx0 = kept_col(c0), kx1 = kept_col(c0 + 1), kx2 = kept_col(c0 + 2), kx3 = kept_col(c0 + 3);
+
+  auto level = [&](const d4& up_, const d4& c, const d4& dn, int64_t row) -> d4 {
+#pragma clang fp contract(off)
+    // a pair: lane 0 <- lane 63's w, lane 63 <- lane 0's x (the scratch
+    // column on the inner side, the other edge column on the outer side)
+    const double w = PAIR ? dpp_rot_from_lower(c.w) : dpp_from_lower(c.w);
+    const double e = PAIR ? dpp_rot_from_upper(c.x) : dpp_from_upper(c.x);
+    d4 v;
+    if constexpr (EXACT) {
+      v.x = quarter * ((w + c.y) + (up_.x + dn.x));
+      v.y = quarter * ((c.x + c.z) + (up_.y + dn.y));
+      v.z = quarter * ((c.y + c.w) + (up_.z + dn.z));
+      v.w = quarter * ((c.z + e) + (up_.w + dn.w));
+    } else {
+      v.x = (w + c.y) + (up_.x + dn.x);
+      v.y = (c.x + c.z) + (up_.y + dn.y);
+      v.z = (c.y + c.w) + (up_.z + dn.z);
+      v.w = (c.z + e) + (up_.w + dn.w);
+    }
+    if constexpr (RULE) {
+      const bool rk = (row < dy0 && !gs) || (row >= dy1 && !gn);
+      const double f = EXACT ? 1.0 : 4.0;  // a kept cell: V_p = 4 V_{p-1}
+      v.x = (rk || kx0) ? c.x * f : v.x;
+      v.y = (rk || kx1) ? c.y * f : v.y;
+      v.z = (rk || kx2) ? c.z * f : v.z;
+      v.w = (rk || kx3) ? c.w * f : v.w;
+    }
+    return v;
+  };
+
+  constexpr int NL = PE - PB + 1;
+  // W[p - PB][0 / 1]: level p (PB..PE-1) of the rows of steps s-2 / s-1
+  d4 W[NL > 1 ? NL - 1 : 1][2];
+#pragma unroll
+  for (int p = 0; p < (NL > 1 ? NL - 1 : 1); ++p)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) W[p][j] = d4{0.0, 0.0, 0.0, 0.0};
+
+  // prologue: rows 0..P-1 in flight, each preceded by the (dropped) stores a
+  // steady-state step issues, so every wait below counts the same
+  // (SPS + DPS)(P - 1) younger memory operations
+  if constexpr (kIn) {
+    // (each dummy store gets its own out-of-range row so the compiler cannot
+    // merge identical stores)
+    static_for<0, kP>([&](auto I) {
+      store_step(decltype(I)::value - kP, d4{0.0, 0.0, 0.0, 0.0});
+      dma(decltype(I)::value, decltype(I)::value);
+    });
+  }
+
+  // A pair strip's edge lane (left: 63, right: 0; one SGPR pair, its bit
+  // reverse is the scratch lane).  With KL = K + 4 > K + 1 the WHOLE
+  // scratch lane is outside every output cone, so both strips run the same
+  // ops: loads into both end components of the scratch lane (the one the
+  // rotate reads is the left's x / the right's w), stores of both end
+  // components of the edge lane (to separate entries; the reader's base
+  // picks the right one: the left's w, the right's x)
+  static_assert(!PAIR || ring_left(K) >= K + kNC, "a pair's scratch lane is its whole outermost lane");
+  const uint64_t m_edge = __builtin_amdgcn_readfirstlane(right ? 1 : 0) ? uint64_t{1} : uint64_t{1} << (kWave - 1);
+  // stage 0 of a pair stores its level-KA edge (both end components of its
+  // edge lane) into the NEIGHBOUR's hand row of the same step, at that row's
+  // scratch lane (left -> the right's columns 254-255, right -> the left's
+  // 0-1), while its own hand row store skips its own scratch lane: stage 1's
+  // level-KA rows arrive patched (published by the same barrier)
+  // (as an offset from this lane's own hand-row address, in an SGPR: a
+  // VGPR base spills the pipeline)
+  const uint32_t nb_delta = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+      static_cast<int>(lds_addr(nhand) - lds_addr(hand)) + (right ? 0 : 16)));
+  // entries of a slot, K levels each: [right's w][left's w][right's x][left's
+  // x]; a strip stores its w at xw, its x at xw + 2K, and reads at xw + K —
+  // the left reads the right's x, the right the left's w — one base register
+  constexpr uint32_t kLev = K * 8;
+  const uint32_t xw = PAIR ? to_vgpr(xbv + (right ? 0u : kLev)) : 0u;
+  // level PB-1 rows of step s (rows s-D-PB-1 .. s-D-PB+1), read one step
+  // ahead so the ds_reads are in flight across the step barrier
+  d4 r0, r1, r2;
+  auto load_rows = [&](int s) {
+    if constexpr (kIn) {
+      // the DMA of row s (issued at the end of step s-P) has landed once at
+      // most (SPS + DPS)(P - 1) younger memory operations are outstanding
+      wait_vmcnt<(SPS + DPS) * (kP - 1)>();
+      r0 = lds_row(ring + ((s + kRS - 2) % kRS) * kSlotBytes, lane);
+      r1 = lds_row(ring + ((s + kRS - 1) % kRS) * kSlotBytes, lane);
+      r2 = lds_row(ring + (s % kRS) * kSlotBytes, lane);
+      // the neighbour's row s-1 landed before ITS wait at the end of step
+      // s-2, i.e. before the barrier this wave has passed; its slot is
+      // refilled at step s+1 at the earliest
+    } else {
+      // stage 0's level-KA rows of steps s-4 .. s-2 (published by the
+      // barriers of those steps)
+      r0 = lds_row(hand + ((s + kHS - 4) % kHS) * kRowBytes, lane);
+      r1 = lds_row(hand + ((s + kHS - 3) % kHS) * kRowBytes, lane);
+      r2 = lds_row(hand + ((s + kHS - 2) % kHS) * kRowBytes, lane);
+    }
+  };
+  load_rows(0);
+
+  // rows of the walk: level p of step s is row rbase(s) - dir * p
+  const int64_t yanchor = up ? ye - 1 + K : yl;
+  // edge hand-off ring of a pair: slot = the step's position in the
+  // unrolled block (compile-time); a strip writes at its step's slot and
+  // reads at the previous step's slot (written before the barrier it has
+  // passed; rewritten kU steps later)
+  constexpr int kU = unroll_for(NL);
+  auto xoff = [](int slot, int lev) { return static_cast<uint32_t>((slot * 4 * K + lev) * 8); };
+  auto step = [&](auto J, int s) {
+    constexpr int j = decltype(J)::value, jp = (j + kU - 1) % kU;
+    const int64_t rbase = yanchor + dir * (s - D);
+    d4 v = level(r0, r1, r2, rbase - dir * PB);
+    if constexpr (PAIR && PB < PE) {  // level PB+1 reads level PB of step s-1 (W[0][1])
+      lds_load_lane<xoff(jp, PB) + kLev>(xw, W[0][1].x, m_edge);
+      lds_load_lane<xoff(jp, PB) + kLev>(xw, W[0][1].w, m_edge);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<PB + 1, PE + 1>([&](auto Q) {
+      constexpr int p = decltype(Q)::value;  // PB+1 .. PE, bottom-up
+      if constexpr (PAIR) {
+        // the neighbour's level p-1 of step s-1 is in the scratch lane of
+        // W[p-1-PB][1]; this strip's level p-1 of step s (v) goes out
+        lds_wait(W[p - 1 - PB][1].x, W[p - 1 - PB][1].w);
+        lds_store_lane<xoff(j, p - 1)>(xw, v.w, m_edge);
+        lds_store_lane<xoff(j, p - 1) + 2 * kLev>(xw, v.x, m_edge);
+      }
+      const d4 nv = level(W[p - 1 - PB][0], W[p - 1 - PB][1], v, rbase - dir * p);
+      W[p - 1 - PB][0] = W[p - 1 - PB][1];  // rows of steps s-1 and s become s-2 and s-1
+      W[p - 1 - PB][1] = v;
+      v = nv;
+      if constexpr (PAIR && p < PE) {  // for level p+1: the neighbour's level p of step s-1
+        lds_load_lane<xoff(jp, p) + kLev>(xw, W[p - PB][1].x, m_edge);
+        lds_load_lane<xoff(jp, p) + kLev>(xw, W[p - PB][1].w, m_edge);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if constexpr (kOut) {
+      if constexpr (!EXACT) {
+        v.x = __builtin_amdgcn_ldexp(v.x, -2 * K);  // exact power-of-two unscale
+        v.y = __builtin_amdgcn_ldexp(v.y, -2 * K);
+        v.z = __builtin_amdgcn_ldexp(v.z, -2 * K);
+        v.w = __builtin_amdgcn_ldexp(v.w, -2 * K);
+      }
+      store_step(s, v);  // issued every step (warm-up rows are out of range)
+    } else {
+      d2* h = reinterpret_cast<d2*>(hand + (s % kHS) * kRowBytes) + 2 * lane;
+      if constexpr (PAIR) {
+        const uint32_t ha = lds_addr(h), nh = ha + nb_delta;
+        lds_store_row_noscratch(ha, d2{v.x, v.y}, d2{v.z, v.w}, m_edge);
+        lds_store_lane<0>(nh, v.x, m_edge);
+        lds_store_lane<8>(nh, v.w, m_edge);
+      } else {
+        h[0] = d2{v.x, v.y};
+        h[1] = d2{v.z, v.w};
+      }
+    }
+    // the ring slot of row s-2 is free (its ds_reads completed before level
+    // 1 used them): prefetch row s+P into it
+    dma(s + kP, (s + kP) % kRS);
+    // hand-off row written (visible to the workgroup after the barrier),
+    // then the next step's rows requested, then the barrier
+    if constexpr (SYNC) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    load_rows(s + 1);
+    if constexpr (SYNC) asm volatile("s_barrier" ::: "memory");
+  };
+
+  for (int s0 = 0; s0 < nsteps; s0 += kU) {
+    static_for<0, kU>([&](auto J) { step(J, s0 + decltype(J)::value); });
+    // A row band's output wave: once the unrolled block holding step
+    // sig_step is done, the band's rows are written — visible device-wide,
+    // then one arrival (the last raises *signal).  Checked at the block
+    // boundary, not per step: the register allocation of the unrolled body
+    // has no room for a branch per step (tests/test_kernel_resources.py).
+    if constexpr (kOut) {
+      if (static_cast<unsigned>(sig_step - s0) < static_cast<unsigned>(kU)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (lane == 0 && __hip_atomic_fetch_add(a.sig_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                             static_cast<unsigned>(a.sig_total - 1)) {
+          __hip_atomic_store(a.sig_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(a.signal, uint64_t{1}, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  }
+  // no LDS-DMA may land after the workgroup's LDS is released
+  wait_vmcnt<0>();
+}
+
+// A workgroup = nw adjacent strips of one segment row, G waves per strip
+// (adjacent strips share their overlap columns in the CU's L1 / the XCD's
+// L2).  G == 1: every wave is independent (no barrier).  G == 2: one pair of
+// strips (4 waves) whose inner edge is handed over in LDS (run_stage PAIR).
+template <int K, bool EXACT, bool EDGE>
+__device__ __forceinline__ void tb_block(const Args& a, const double* __restrict__ u, double* __restrict__ un,
+                                         int64_t t) {
+  constexpr int G = n_stages(K);
+  extern __shared__ d2 lds_dyn[];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
+  const int sl = wave / G, stage = wave % G;
+  int k = 0;
+  while (k + 1 < a.n && t >= a.tstart[k + 1]) ++k;
+  const int64_t lt = t - a.tstart[k];
+  const int64_t ngroups = (a.nstrip[k] + a.nw - 1) / a.nw;
+  // Dispatch order: (R) the row bands of a band-first pass (Args::rb_rect:
+  // every strip group's segment next to a halo row side), then every
+  // workgroup that can hold Dirichlet-rule waves (~1.5x the VALU per step),
+  // so the launch's tail is made of fast ones: (A) the edge segments, all
+  // strip groups; (B) the interior segments' first and last strip groups;
+  // (C) the rest.
+  const int64_t ry0 = a.r[k][2], ry1 = a.r[k][2] + a.r[k][3];
+  const int64_t e0 = a.e0[k], e1 = a.e1[k];
+  const int64_t nedge = (e0 > 0) + (e1 > 0), nbnd = ngroups < 2 ? ngroups : 2;
+  const int rbs = k == a.rb_rect ? a.rb_s : 0, rbn = k == a.rb_rect ? a.rb_n : 0, rb = rbs + rbn;
+  int64_t gi, m = -1;  // m: interior segment index, -1: edge segment `edge`
+  int edge = 0, dir = 1;
+  bool band = false;
+  if (lt < rb * ngroups) {  // (R): S band = first interior segment, N band = last (walked bottom-up)
+    gi = lt % ngroups;
+    const bool north = lt >= ngroups || !rbs;
+    const int64_t nm = (gi == 0 || gi == ngroups - 1) ? a.nmid_b[k] : a.nmid[k];
+    m = north ? nm - 1 : 0;
+    dir = north ? -1 : 1;
+    band = true;
+  } else if (lt < rb * ngroups + nedge * ngroups) {  // (A)
+    const int64_t l1 = lt - rb * ngroups;
+    edge = (l1 / ngroups == 0 && e0 > 0) ? 0 : 1;
+    gi = l1 % ngroups;
+  } else if (lt < rb * ngroups + nedge * ngroups + (a.nmid_b[k] - rb) * nbnd) {  // (B)
+    const int64_t l2 = lt - rb * ngroups - nedge * ngroups;
+    m = rbs + l2 / nbnd;
+    gi = l2 % nbnd == 0 ? 0 : ngroups - 1;
+  } else {  // (C)
+    const int64_t l3 = lt - rb * ngroups - nedge * ngroups - (a.nmid_b[k] - rb) * nbnd;
+    m = rbs + l3 / (ngroups - 2);
+    gi = 1 + l3 % (ngroups - 2);
+  }
+  const int64_t lmid = (gi == 0 || gi == ngroups - 1) ? a.lmid_b[k] : a.lmid[k];
+  int64_t ys, ye;
+  if (m < 0) {
+    ys = edge == 0 ? ry0 : ry1 - e1;
+    ye = edge == 0 ? ry0 + e0 : ry1;
+  } else {
+    ys = ry0 + e0 + m * lmid;
+    ye = ys + lmid < ry1 - e1 ? ys + lmid : ry1 - e1;
+  }
+  // L + 2K steps (stage 1 of a split strip runs two steps behind: two more)
+  constexpr int kU = unroll_for(G == 1 ? K : stage0_levels(K));
+  // a row band's output wave publishes its arrival at the step that stores
+  // the band's last row (the first sig_rows rows of its walk)
+  const int sig_step = band ? static_cast<int>((G > 1 ? 2 : 0) + 2 * K + a.sig_rows - 1) : -1;
+  static_assert(G == 1 || unroll_for(stage0_levels(K)) == unroll_for(K - stage0_levels(K)), "stages step together");
+  const int nsteps = static_cast<int>((ye - ys + 2 * K + (G > 1 ? 2 : 0) + kU - 1) / kU * kU);
+  const int64_t strip = G > 1 ? gi : gi * a.nw + sl;  // G > 1: the pair; sl = its left / right strip
+  if (strip >= a.nstrip[k]) {  // no strip for this wave
+    if constexpr (G > 1) {
+      for (int s = 0; s < nsteps; ++s) step_barrier();  // the workgroup's per-step barriers
+    }
+    return;
+  }
+  constexpr int64_t wout = strip_out(K);
+  const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
+  int64_t xs = rx0 + strip * wout;
+  if (xs + wout > rx1) xs = rx1 - wout > rx0 ? rx1 - wout : rx0;  // last strip: shifted left to end at rx1
+  const int64_t xe = xs + wout < rx1 ? xs + wout : rx1;
+  const int64_t cf = xs - ring_left(K) + (G > 1 ? sl * kCols : 0);  // the wave's window
+  // the rule path only where a computed cell can be a fixed ring cell
+  const int64_t cx0 = cf, cx1 = cx0 + kCols;
+  const bool rule = (cx0 < a.dom[0] && !(a.mask & 1)) || (cx1 > a.dom[0] + a.dom[1] && !(a.mask & 2)) ||
+                    (ys - K < a.dom[2] && !(a.mask & 4)) || (ye + K > a.dom[2] + a.dom[3] && !(a.mask & 8));
+  char* base = reinterpret_cast<char*>(lds_dyn);
+  char* ring = base + sl * strip_lds(G);
+  char* hand = ring + kRS * kSlotBytes;
+  // the other strip of a pair, and the pair's edge hand-off
+  const char* nring = base + (1 - sl) * strip_lds(G);
+  const char* nhand = nring + kRS * kSlotBytes;
+  const uint32_t xbv = G > 1 ? to_vgpr(lds_addr(base + kPair * strip_lds(G))) : 0u;
+  // one instantiation per (stage, rule path, direction); the direction is
+  // bottom-up only for the N row bands
+  // (always_inline: outlined, a stage becomes a call whose ABI spills the
+  // pipeline's registers)
+  auto go = [&](auto pb, auto pe, auto sync, auto rule_c, auto up_c, int sstep) __attribute__((always_inline)) {
+    run_stage<K, decltype(pb)::value, decltype(pe)::value, EXACT, EDGE, decltype(rule_c)::value,
+              decltype(sync)::value, decltype(up_c)::value, (G > 1)>(
+        a, u, un, ring, hand, nring, nhand, xbv, sl == 1, lane, cf, xs, xe, ys, ye, nsteps, sstep);
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  auto stage_go = [&](auto pb, auto pe, auto sync, int sstep) __attribute__((always_inline)) {
+    if (dir < 0) {
+      if (rule) go(pb, pe, sync, T{}, T{}, sstep);
+      else go(pb, pe, sync, F{}, T{}, sstep);
+    } else {
+      if (rule) go(pb, pe, sync, T{}, F{}, sstep);
+      else go(pb, pe, sync, F{}, F{}, sstep);
+    }
+  };
+  using C1 = std::integral_constant<int, 1>;
+  using CK = std::integral_constant<int, K>;
+  if constexpr (G == 1) {
+    stage_go(C1{}, CK{}, F{}, sig_step);
+  } else {
+    constexpr int KA = stage0_levels(K);
+    if (stage == 0) {
+      // a launch of one round has no later workgroups to fill the SIMDs
+      // while a strip's stage 1 waits on its stage 0: favour the producer
+      // (profiles/r02_tb.md 9.4)
+      if (a.prio) __builtin_amdgcn_s_setprio(2);
+      stage_go(C1{}, std::integral_constant<int, KA>{}, T{}, -1);
+    } else {
+      stage_go(std::integral_constant<int, KA + 1>{}, CK{}, T{}, sig_step);
+    }
+  }
+}
+
+template <int K, bool EXACT, bool EDGE>
+__global__ __launch_bounds__(kMaxThreads) __attribute__((amdgpu_waves_per_eu(2)))
+void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__ un, int64_t nblocks) {
+  const int64_t ns = a.sig_wgs, nd = a.sig_dispatch;
+  const int64_t b = blockIdx.x;
+  // signalling workgroups (and row bands) first, in dispatch order over all
+  // XCDs; the rest XCD-contiguous
+  const int64_t t = b < nd ? b : nd + xcd_swizzle(b - nd, nblocks - nd);
+  tb_block<K, EXACT, EDGE>(a, u, un, t);
+  if (t < ns) {
+    // every wave's stores written back past its XCD's L2, then one arrival
+    // per workgroup (vector atomics on uncached memory)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(a.sig_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+            static_cast<unsigned>(a.sig_total - 1)) {
+      __hip_atomic_store(a.sig_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(a.signal, uint64_t{1}, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace tb
+}  // namespace gmt
+
+namespace {
+
+using namespace gmt;
+using namespace gmt::tb;
+
+// Segment plan (rows per strip).  Every segment pays a 2K-step pipeline
+// warm-up, so interior segments should be long; but a wave whose segment
+// touches a Dirichlet row runs the rule path (~1.5x the VALU per step) for
+// the whole segment, and the launch ends with its slowest round.  Measured
+// (profiles/r02_tb4.md, K = 20, 32768^2): all-halo sides 4.41M MLUPS at 384
+// rows and 4.61M at 1024-2048; with Dirichlet sides 3.78M at 384, falling
+// to 2.38M at 4096.  So: short edge segments (max(64, K) rows) where the
+// rect touches a Dirichlet row, and interior segments whose length L
+// minimises rounds(L) x (L + 2K), rounds = ceil(workgroups / resident
+// workgroups), over L in [128, 2048].
+struct SegPlan {
+  int64_t e0[kMaxRect], e1[kMaxRect], nmid[kMaxRect], lmid[kMaxRect], nmid_b[kMaxRect], lmid_b[kMaxRect];
+};
+
+// Signalling rects (k < sig_rects: the boundary bands of a pass whose halo
+// exchange overlaps the rest of it) get short segments, max(128, L/3) rows
+// and no edge split: their workgroups must finish early in the launch.
+// A row-band rect (rb_rect, gmt_tb_opts.signal_rows) keeps at least `rb`
+// interior segments per strip group, each at least rb_min rows long, so its
+// S and N bands are separate segments that finish early.
+template <int K>
+SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t resident_wgs, int sig_rects, int rb_rect = -1,
+                      int rb = 0, int64_t rb_min = 0) {
+  SegPlan p{};
+  const int64_t edge = std::max<int64_t>(64, K);
+  auto fill = [&](int64_t L0, int64_t* wgs) {
+    int64_t w = 0;
+    for (int k = 0; k < a.n; ++k) {
+      int64_t L = L0;
+      const int64_t ny = a.r[k][3], ry0 = a.r[k][2], ry1 = ry0 + ny;
+      if (k < sig_rects) {
+        const int64_t lb = std::min<int64_t>(std::max<int64_t>(128, L / 3), lmax);
+        p.e0[k] = p.e1[k] = 0;
+        p.nmid[k] = p.nmid_b[k] = (ny + lb - 1) / lb;
+        p.lmid[k] = p.lmid_b[k] = (ny + p.nmid[k] - 1) / p.nmid[k];
+        w += (a.nstrip[k] + a.nw - 1) / a.nw * p.nmid[k];
+        continue;
+      }
+      const bool top = seg_rows == 0 && ry0 - K < a.dom[2] && !(a.mask & 4);
+      const bool bot = seg_rows == 0 && ry1 + K > a.dom[2] + a.dom[3] && !(a.mask & 8);
+      p.e0[k] = p.e1[k] = 0;
+      if (ny > 2 * edge + 64) {  // room for edges and an interior
+        p.e0[k] = top ? edge : 0;
+        p.e1[k] = bot ? edge : 0;
+      }
+      const int64_t mid = ny - p.e0[k] - p.e1[k];
+      if (k == rb_rect && rb > 0) L = std::min<int64_t>(L, std::max<int64_t>(rb_min, mid / rb));
+      p.nmid[k] = (mid + L - 1) / L;
+      p.lmid[k] = (mid + p.nmid[k] - 1) / p.nmid[k];  // balanced lengths
+      // strip groups that can reach a Dirichlet column run the rule path
+      // (~2x the VALU per step): half-length segments, so they finish with
+      // the others instead of ending the launch
+      const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
+      const bool xrule = seg_rows == 0 && ((rx0 - ring_left(K) < a.dom[0] && !(a.mask & 1)) ||
+                                           (rx1 + ring_left(K) > a.dom[0] + a.dom[1] && !(a.mask & 2)));
+      int64_t lb = xrule ? std::max<int64_t>(64, p.lmid[k] / 2) : p.lmid[k];
+      if (k == rb_rect && rb > 0) lb = std::min<int64_t>(lb, std::max<int64_t>(rb_min, mid / rb));
+      p.nmid_b[k] = (mid + lb - 1) / lb;
+      p.lmid_b[k] = (mid + p.nmid_b[k] - 1) / p.nmid_b[k];
+      const int64_t groups = (a.nstrip[k] + a.nw - 1) / a.nw, nbnd = groups < 2 ? groups : 2;
+      w += groups * ((p.e0[k] > 0) + (p.e1[k] > 0)) + nbnd * p.nmid_b[k] + (groups - nbnd) * p.nmid[k];
+    }
+    *wgs = w;
+  };
+  int64_t wgs = 0;
+  if (seg_rows > 0) {
+    fill(std::min<int64_t>(seg_rows, lmax), &wgs);
+    return p;
+  }
+  int64_t best_l = 128;
+  double best = 1e300;
+  for (int64_t L = 128; L <= std::min<int64_t>(2048, lmax); L += 32) {
+    fill(L, &wgs);
+    const double rounds = static_cast<double>((wgs + resident_wgs - 1) / resident_wgs);
+    // a segment runs L + 2K (+2 with two stages) steps, rounded up to the unroll
+    constexpr int64_t u = unroll_for(n_stages(K) == 1 ? K : stage0_levels(K));
+    const double cost = rounds * static_cast<double>((L + 2 * K + 2 * (n_stages(K) > 1) + u - 1) / u * u);
+    if (cost < best) {
+      best = cost;
+      best_l = L;
+    }
+  }
+  fill(std::min<int64_t>(best_l, lmax), &wgs);
+  return p;
+}
+
+// Fills the kernel arguments and the launch shape; info (optional) gets
+// {workgroups, resident workgroups, threads per workgroup, rows per interior
+// segment and interior segments of the first rect, VGPRs per lane}.
+template <int K, bool EXACT, bool EDGE>
+int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int64_t* dom, int mask, const double* u,
+              double* un, int64_t ld, int64_t nrows, hipStream_t s, int64_t* info = nullptr) {
+  constexpr int G = n_stages(K);
+  constexpr int kMaxStrips = kMaxThreads / kWave / G;
+  Args a{};
+  // one-stage: 4 lone strips per workgroup; two-stage: one pair
+  a.nw = G > 1 ? 1 : std::min(o.wg_waves > 0 ? o.wg_waves : 4, kMaxStrips);
+  a.ld = ld;
+  a.last_row = nrows - 1;
+  a.mask = mask;
+  a.quarter = 0.25;
+  for (int j = 0; j < 4; ++j) a.dom[j] = dom[j];
+  constexpr int64_t wout = strip_out(K);
+  int64_t maxh = 0;
+  for (int k = 0; k < n_rect; ++k) {
+    const int64_t* r = rects + 4 * k;
+    if (r[1] <= 0 || r[3] <= 0) continue;
+    for (int j = 0; j < 4; ++j) a.r[a.n][j] = r[j];
+    a.nstrip[a.n] = (r[1] + wout - 1) / wout;
+    maxh = std::max(maxh, r[3]);
+    ++a.n;
+  }
+  if (a.n == 0) return 0;
+  // all strips of a rect narrower than nw strips: fewer strips per workgroup
+  int64_t maxs = 0;
+  for (int k = 0; k < a.n; ++k) maxs = std::max(maxs, a.nstrip[k]);
+  if (a.nw > maxs) a.nw = static_cast<int>(maxs);
+  const int threads = G > 1 ? kPair * G * kWave : a.nw * kWave;
+  // the kernel addresses a segment's rows through 32-bit buffer offsets:
+  // (L + 3K + 2 unroll + prefetch) rows of ld doubles must stay below 2^31
+  const int64_t lmax = std::min<int64_t>(1 << 20, (int64_t(1) << 31) / (ld * 8) - 3 * K - 2 * unroll_for(K) - kP);
+  if (lmax < 1) return static_cast<int>(hipErrorInvalidValue);
+  (void)maxh;
+  const size_t smem = static_cast<size_t>(a.nw * unit_lds<K>());
+  if (smem > 65536) {  // above the default dynamic-LDS limit (gfx950 has 160 KB per CU)
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem));
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  // resident workgroups on the device for this shape (registers, LDS);
+  // queried once per device, kernel and strips-per-workgroup (an idempotent
+  // cache: a process driving several devices keeps one entry per device)
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> resident[kMaxDev][kMaxThreads / kWave + 1] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::atomic<int>* slot = dev >= 0 && dev < kMaxDev ? &resident[dev][a.nw] : nullptr;
+  int per_cu = slot ? slot->load(std::memory_order_relaxed) : 0;
+  if (per_cu <= 0) {
+    int occ = 0, cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE>),
+                                                     threads, smem) != hipSuccess || occ < 1)
+      occ = 1;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    per_cu = occ * cus;
+    if (slot) slot->store(per_cu, std::memory_order_relaxed);
+  }
+  const int sig_rects = o.signal_rects;  // non-empty rects (checked): the same indices after the compaction
+  // row bands: the first rect after the signalling ones (checked non-empty)
+  const int rbk = o.signal_rows > 0 ? sig_rects : -1;
+  const int rbs = rbk >= 0 && (mask & 4) ? 1 : 0, rbn = rbk >= 0 && (mask & 8) ? 1 : 0;
+  const int64_t rb_min = std::max<int64_t>(32, o.signal_rows);
+  if (rbk >= 0 && (rbk >= a.n || rbs + rbn == 0 || a.r[rbk][3] < (rbs + rbn) * rb_min))
+    return static_cast<int>(hipErrorInvalidValue);
+  const SegPlan sp = plan_segments<K>(a, o.seg_rows, lmax, per_cu, sig_rects, rbk, rbs + rbn, rb_min);
+  a.tstart[0] = 0;
+  for (int k = 0; k < a.n; ++k) {
+    a.e0[k] = sp.e0[k];
+    a.e1[k] = sp.e1[k];
+    a.nmid[k] = sp.nmid[k];
+    a.lmid[k] = sp.lmid[k];
+    a.nmid_b[k] = sp.nmid_b[k];
+    a.lmid_b[k] = sp.lmid_b[k];
+    const int64_t groups = (a.nstrip[k] + a.nw - 1) / a.nw, nbnd = groups < 2 ? groups : 2;
+    a.tstart[k + 1] = a.tstart[k] + groups * ((sp.e0[k] > 0) + (sp.e1[k] > 0)) + nbnd * sp.nmid_b[k] +
+                      (groups - nbnd) * sp.nmid[k];
+  }
+  for (int k = a.n + 1; k <= kMaxRect; ++k) a.tstart[k] = a.tstart[a.n];
+  const int64_t nb = a.tstart[a.n];
+  a.sig_wgs = a.tstart[sig_rects];
+  a.rb_rect = -1;
+  a.sig_total = a.sig_wgs;
+  a.sig_dispatch = a.sig_wgs;
+  if (rbk >= 0) {
+    // the band segments exist separately: halo row sides have no edge
+    // segments, and the planner kept >= rbs + rbn interior segments of >= rb_min rows
+    const int rb = rbs + rbn;
+    if ((rbs && sp.e0[rbk] > 0) || (rbn && sp.e1[rbk] > 0) || sp.nmid[rbk] < rb || sp.nmid_b[rbk] < rb ||
+        (sp.nmid[rbk] > 1 && sp.lmid[rbk] < o.signal_rows) || (sp.nmid_b[rbk] > 1 && sp.lmid_b[rbk] < o.signal_rows))
+      return static_cast<int>(hipErrorInvalidValue);
+    a.rb_rect = rbk;
+    a.rb_s = rbs;
+    a.rb_n = rbn;
+    a.sig_rows = o.signal_rows;
+    const int64_t groups = (a.nstrip[rbk] + a.nw - 1) / a.nw;
+    a.sig_total += rb * a.nstrip[rbk] * (G > 1 ? kPair : 1);  // one arrival per output wave of every band
+    a.sig_dispatch += rb * groups;       // rect rbk's band tiles follow the signalling rects
+  }
+  a.prio = nb <= per_cu ? 1 : 0;
+  a.sig_count = o.signal_count;
+  a.signal = o.signal;
+  if (info) {
+    hipFuncAttributes fa{};
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE>));
+    const int64_t v[6] = {nb, per_cu, threads, a.lmid[0], a.nmid[0], fa.numRegs};
+    for (int j = 0; j < 6; ++j) info[j] = v[j];
+    return 0;
+  }
+  jacobi5tb_kernel<K, EXACT, EDGE><<<grid_1d(nb), threads, smem, s>>>(a, u, un, nb);
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // namespace
+
+namespace gmt {
+namespace tb {
+
+template <int K>
+int dispatch_k(const gmt_tb_opts& o, bool exact, int n_rect, const int64_t* rects, const int64_t* dom, int mask,
+               const double* u, double* un, int64_t ld, int64_t nrows, hipStream_t s, int64_t* info) {
+  // a rect narrower than a strip whose width is odd ends inside a lane pair:
+  // that lane stores column 0 or 2 alone (wider rects end on a lane
+  // boundary: their last strip is shifted to end at the rect's edge)
+  bool edge = false;
+  for (int k = 0; k < n_rect; ++k)
+    if (rects[4 * k + 1] > 0 && rects[4 * k + 3] > 0 && rects[4 * k + 1] < strip_out(K) && rects[4 * k + 1] % 2 == 1)
+      edge = true;
+  if (edge)
+    return exact ? launch_tb<K, true, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
+                 : launch_tb<K, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
+  return exact ? launch_tb<K, true, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
+               : launch_tb<K, false, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
+}
+
+}  // namespace tb
+}  // namespace gmt

@@ -6,6 +6,8 @@
 #   scripts/build_variant.sh p4 's/constexpr int kP = 6;/constexpr int kP = 4;/'
 #   scripts/build_variant.sh head git:HEAD     (jacobi5tb.hpp as committed at HEAD)
 #   scripts/build_variant.sh b2 file:build/var_src/jacobi5tb_b2.hpp   (a whole edited copy)
+#   scripts/build_variant.sh pair file:csrc/bench/jacobi5tb_pair.hpp   (the paired-strip candidate)
+#   scripts/build_variant.sh x cur             (the working tree's kernel sources as they are)
 set -e
 cd "$(dirname "$0")/.."
 name=$1; expr=$2
@@ -15,9 +17,10 @@ cp csrc/kernels/*.hpp csrc/kernels/jacobi5tb*.hip $D/src/
 case "$expr" in
   git:*) git show "${expr#git:}:csrc/kernels/jacobi5tb.hpp" > $D/src/jacobi5tb.hpp ;;
   file:*) cp "${expr#file:}" $D/src/jacobi5tb.hpp ;;
+  cur) ;;
   *) sed -i "$expr" $D/src/jacobi5tb.hpp ;;
 esac
-cmp -s csrc/kernels/jacobi5tb.hpp $D/src/jacobi5tb.hpp && { echo "sed changed nothing"; exit 1; }
+[ "$expr" != cur ] && cmp -s csrc/kernels/jacobi5tb.hpp $D/src/jacobi5tb.hpp && { echo "sed changed nothing"; exit 1; }
 ls $D/src/jacobi5tb*.hip | xargs -P 8 -I{} sh -c '/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Icsrc/include -munsafe-fp-atomics -c {} -o '$D'/obj/$(basename {} .hip).o'
 others=$(ls build/obj/kernels/*.o | grep -v jacobi5tb)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/libgmt.so $D/obj/*.o $others build/obj/runtime/rt_hip.o \
