@@ -508,8 +508,11 @@ struct SegPlan {
 };
 
 // Signalling rects (k < sig_rects: the boundary bands of a pass whose halo
-// exchange overlaps the rest of it) get short segments, max(128, L/3) rows
-// and no edge split: their workgroups must finish early in the launch.
+// exchange overlaps the rest of it) get segments of max(128, 3L/4) rows and
+// no edge split: their workgroups are dispatched first and end a quarter of
+// a segment before the rest of their round, which is when the exchange runs
+// (L/3 cost 1.5-5 % more on the 1-GPU shares: more workgroups, more 2K-step
+// warm-ups; profiles/r03_band_lb).
 // A row-band rect (rb_rect, gmt_tb_opts.signal_rows) keeps at least `rb`
 // interior segments per strip group, each at least rb_min rows long, so its
 // S and N bands are separate segments that finish early.
@@ -524,7 +527,7 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
       int64_t L = L0;
       const int64_t ny = a.r[k][3], ry0 = a.r[k][2], ry1 = ry0 + ny;
       if (k < sig_rects) {
-        const int64_t lb = std::min<int64_t>(std::max<int64_t>(128, L / 3), lmax);
+        const int64_t lb = std::min<int64_t>(std::max<int64_t>(128, L - L / 4), lmax);
         p.e0[k] = p.e1[k] = 0;
         p.nmid[k] = p.nmid_b[k] = (ny + lb - 1) / lb;
         p.lmid[k] = p.lmid_b[k] = (ny + p.nmid[k] - 1) / p.nmid[k];

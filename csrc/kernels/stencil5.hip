@@ -11,13 +11,15 @@
 // dim 0 (taps along the contiguous axis): stencil5_pt<0>, one output pair
 // per thread, the overlapping loads served by L1 (6.34 TB/s effective).
 //
-// dim 1 (taps along the strided axis): stencil5_d1_dma.  One wave owns a
-// strip of 128 * CPL columns and walks down a segment of L output rows with
-// a 5-row register window; input rows arrive by buffer->LDS DMA into a ring
-// of P + 1 slots, P rows ahead (the jacobi5tb.hip memory pipeline).  The
-// round-1 register-window kernel (now in csrc/bench/variant_bench.hip) issued
-// its unrolled loads in bursts and drained them to vmcnt(0..3) every 8 rows:
-// 85% of wave cycles waiting (rocprofv3 --pmc, profiles/r02_pmc/), 4.92 TB/s.
+// dim 1 (taps along the strided axis): stencil5_d1_win (even widths): 16
+// waves side by side per workgroup walk 256-row segments with a register
+// window, column groups fastest so the chip sweeps the array row band by row
+// band (5.60-5.64 TB/s at the reference's shape, profiles/r03_d1_walk.txt);
+// odd widths: stencil5_d1_dma, the round-2 LDS-DMA pipeline (5.46 TB/s on
+// the same box).  The round-1 register-window kernel (now in
+// csrc/bench/variant_bench.hip) issued its unrolled loads in bursts and
+// drained them to vmcnt(0..3) every 8 rows: 85% of wave cycles waiting
+// (rocprofv3 --pmc, profiles/r02_pmc/), 4.92 TB/s.
 #include "common.hpp"
 #include "gmt/kernels.h"
 #include "stencil5_d1.hpp"
@@ -126,6 +128,16 @@ extern "C" int gmt_stencil5_2d(int dim, int64_t nx_out, int64_t ny_out, const do
   hipStream_t s = static_cast<hipStream_t>(stream);
   const Coef5 cf = make_coef(coef5);
   const bool vec_ok = aligned16(in) && aligned16(out) && (ld_in % 2 == 0) && (ld_out % 2 == 0);
+  if (dim == 1 && vec_ok && nx_out % 2 == 0) {
+    constexpr int kNWw = 16, kPw = 4;
+    const int64_t L = std::min<int64_t>(256, ny_out);
+    const int64_t ng = (nx_out + 128 * kNWw - 1) / (128 * kNWw), nseg = (ny_out + L - 1) / L;
+    d1::Args c{};
+    for (int k = 0; k < 5; ++k) c.c[k] = cf.c[k] * scale;
+    d1::stencil5_d1_win<kNWw, kPw><<<grid_1d(ng * nseg), kNWw * kWave, 0, s>>>(nx_out, ny_out, ld_in, ld_out, L,
+                                                                               ng, c, in, out);
+    GMT_RET_LAUNCH();
+  }
   if (dim == 1 && vec_ok) {
     // segment rows: the 32-bit buffer offsets must reach (L + 4 + P + U) rows
     // of the wider pitch; 128 rows amortise the 4-row input halo to 3 %

@@ -133,5 +133,53 @@ __global__ __launch_bounds__(kNW * kWave) void stencil5_d1_dma(Args a, const dou
   wait_vmcnt<0>();  // no DMA may land after the workgroup's LDS is released
 }
 
+// Register-window walk (the production dim-1 kernel since round 3): a
+// workgroup = NW waves side by side, 128 columns each (one 16-B chunk per
+// lane), so each input row is read as NW KiB contiguous per workgroup;
+// column groups are fastest in blockIdx and not XCD-swizzled, so the
+// resident workgroups walk down the same few rows of the whole width at
+// once (a near-linear sweep of the array).  A ring of 5 + P rows in
+// registers, P rows of plain 16-B nontemporal loads in flight.  Measured at
+// the reference's dim-1 shape (524288 x 1028 -> 1024, csrc/bench/d1_walk.hip,
+// profiles/r03_d1_walk.txt): 5.60-5.64 TB/s for NW = 16, P = 4, L = 128-512,
+// against 5.46 TB/s for the DMA pipeline above on the same box.
+// Requires an even nx and 16-B aligned rows (ld_in, ld_out even).
+template <int NW, int P>
+__global__ __launch_bounds__(NW * kWave) void stencil5_d1_win(int64_t nx, int64_t ny_out, int64_t ld_in,
+                                                               int64_t ld_out, int64_t L, int64_t ngroups, Args c,
+                                                               const double* __restrict__ in,
+                                                               double* __restrict__ out) {
+  constexpr int R = 5 + P;  // ring: rows o .. o+4 in use, o+5 .. o+4+P in flight
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int64_t g = blockIdx.x % ngroups, seg = blockIdx.x / ngroups;
+  const int64_t x = (g * NW + wave) * 128 + 2 * lane;
+  const int64_t y0 = seg * L;
+  const int64_t L1 = std::min<int64_t>(L, ny_out - y0);
+  if ((g * NW + wave) * 128 >= nx || L1 <= 0) return;
+  const bool valid = x < nx;  // nx even: x + 1 < nx too
+  const int64_t xl = valid ? x : nx - 2;  // loads of an idle lane stay inside the row
+  const d2* src = reinterpret_cast<const d2*>(in + y0 * ld_in + xl);
+  d2* dst = reinterpret_cast<d2*>(out + y0 * ld_out + xl);
+  const int64_t li = ld_in / 2, lo = ld_out / 2;
+  const double c0 = c.c[0], c1 = c.c[1], c2 = c.c[2], c3 = c.c[3], c4 = c.c[4];
+  const int64_t nin = L1 + 4;  // input rows of the segment
+  d2 B[R];
+  auto load = [&](int64_t r, int slot) {
+    B[slot] = __builtin_nontemporal_load(src + (r < nin ? r : nin - 1) * li);  // past the end: unused
+  };
+  static_for<0, 4 + P>([&](auto I) { load(decltype(I)::value, decltype(I)::value); });
+  for (int64_t o0 = 0; o0 < L1; o0 += R) {
+    static_for<0, R>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      const int64_t o = o0 + j;
+      load(o + 4 + P, (j + 4 + P) % R);
+      if (o < L1 && valid)
+        __builtin_nontemporal_store(c0 * B[j % R] + c1 * B[(j + 1) % R] + c2 * B[(j + 2) % R] +
+                                        c3 * B[(j + 3) % R] + c4 * B[(j + 4) % R],
+                                    dst + o * lo);
+    });
+  }
+}
+
 }  // namespace d1
 }  // namespace gmt

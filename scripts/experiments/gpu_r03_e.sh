@@ -13,7 +13,7 @@ M=/opt/conda/bin/mpirun
 : > $OUT/mpihost.txt
 for n in 8192 16384; do
   for mode in "--no-overlap" "--overlap" "--overlap=auto"; do
-    timeout -k 10 200 $M -np 2 --oversubscribe $R/build/bin/mpi_jacobi2d $n 100 --tblock --tsteps=20 --warmup=20 \
+    timeout -k 10 200 $M -np 2 $R/build/bin/mpi_jacobi2d $n 100 --tblock --tsteps=20 --warmup=20 \
       --transport=mpi-host $mode > $OUT/j.log 2>&1 || { cat $OUT/j.log; exit 1; }
     echo "n=$n [$mode] $(grep -E 'TIME step|overlap' $OUT/j.log | tr '\n' ' ')" | tee -a $OUT/mpihost.txt
   done
