@@ -150,32 +150,37 @@ double JacobiSolver::measure_max_abs() {
 
 // One timed pass of every size the planner may use, on this rank's share
 // with its real neighbours (a serial pass includes its exchange), max over
-// ranks: the job's pass takes as long as its slowest rank.
+// ranks: the job's pass takes as long as its slowest rank.  The clock falls
+// by about a quarter over the first few ms of sustained passes
+// (profiles/r03_shares.md), so every pass type is launched once first (code
+// object, occupancy query, clock settling), then the sizes are timed in two
+// round-robin sweeps and each keeps its faster one: no size is measured only
+// cold or only hot.
 void JacobiSolver::calibrate_costs() {
   if (ks_ < 2) return;
   std::vector<int> ks;
   for (int K = 1; K <= ks_; ++K)
     if (K == 1 || gmt_jacobi5tb_supported(K)) ks.push_back(K);
   Buffer<double> d(ks.size(), GMT_SPACE_DEVICE);
-  std::vector<double> host(ks.size(), 0.0);
-  constexpr int kPasses = 2;
-  for (size_t i = 0; i < ks.size(); ++i) {
-    const int K = ks[i];
-    auto one = [&] {
-      if (K == 1) {
-        step();
-      } else {
-        enqueue_block(parity_, K);
-        parity_ ^= 1;
-      }
-    };
-    one();  // first launch of this pass type (code object, occupancy query)
-    synchronize();
-    const double t0 = wtime();
-    for (int r = 0; r < kPasses; ++r) one();
-    synchronize();
-    host[i] = (wtime() - t0) / kPasses * 1e3;
-  }
+  std::vector<double> host(ks.size(), 1e300);
+  constexpr int kPasses = 2, kSweeps = 2;
+  auto one = [&](int K) {
+    if (K == 1) {
+      step();
+    } else {
+      enqueue_block(parity_, K);
+      parity_ ^= 1;
+    }
+  };
+  for (int K : ks) one(K);
+  synchronize();
+  for (int sweep = 0; sweep < kSweeps; ++sweep)
+    for (size_t i = 0; i < ks.size(); ++i) {
+      const double t0 = wtime();
+      for (int r = 0; r < kPasses; ++r) one(ks[i]);
+      synchronize();
+      host[i] = std::min(host[i], (wtime() - t0) / kPasses * 1e3);
+    }
   GMT_CHECK("calib H2D", gmt_rt_memcpy(d.data(), host.data(), host.size() * sizeof(double)));
   t_.allreduce_max(d.data(), host.size(), s_);
   GMT_CHECK("calib D2H", gmt_rt_memcpy_async(host.data(), d.data(), host.size() * sizeof(double), s_));
@@ -195,19 +200,25 @@ void JacobiSolver::autotune_overlap() {
   if (ks_ < 2 || !halo_[0]->active()) return;  // nothing to hide
   Buffer<double> t(2, GMT_SPACE_DEVICE);
   double host[2] = {0.0, 0.0};
-  constexpr int kPasses = 3;
+  constexpr int kPasses = 2;
+  // first use of each mode's streams, untimed; then the modes in the order
+  // A B B A, so the clock's fall over sustained passes (profiles/
+  // r03_shares.md) does not favour the mode timed first
   for (int mode = 0; mode < 2; ++mode) {
     cfg_.overlap = mode == 0;
-    enqueue_block(parity_, ks_);  // warm-up (first use of the mode's streams)
+    enqueue_block(parity_, ks_);
     parity_ ^= 1;
-    synchronize();
+  }
+  synchronize();
+  for (int mode : {0, 1, 1, 0}) {
+    cfg_.overlap = mode == 0;
     const double t0 = wtime();
     for (int i = 0; i < kPasses; ++i) {
       enqueue_block(parity_, ks_);
       parity_ ^= 1;
     }
     synchronize();
-    host[mode] = (wtime() - t0) / kPasses;
+    host[mode] += (wtime() - t0) / (2 * kPasses);
   }
   // one decision for every rank: the mode with the smaller summed time
   GMT_CHECK("tune H2D", gmt_rt_memcpy(t.data(), host, sizeof(host)));
