@@ -81,6 +81,8 @@ def test_bench_oversubscribed_ipc(n, extra, name):
         assert "py2 x px2" in rec["config"]["parallelism"]
     if "on" in extra:
         assert rec["config"]["parallelism"].endswith("overlap")
+        # the swapped process grid is timed too (2x1 -> 1x2), same engine path
+        assert rec["stencil_alt_dims"] == "1x2" and rec["stencil_alt_dims_MLUPS"] > 0
 
 
 def test_bench_ipc_peer_hang_fails_the_job():
