@@ -180,7 +180,13 @@ __device__ __forceinline__ void lds_load_lane(uint32_t addr, double& v, uint64_t
       : "s"(lane_mask), "v"(addr), "n"(OFF));
 }
 // every LDS op of this wave complete; `v` is tied so its uses stay after it
-__device__ __forceinline__ void lds_wait(double& a, double& b) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b)); }
+// at most N LDS ops of this wave outstanding (LDS ops complete in order)
+template <int N>
+__device__ __forceinline__ void lds_wait(double& a, double& b) {
+  static_assert(N >= 0 && N < 16, "lgkmcnt");
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N));
+}
+
 // a uniform value in a VGPR the compiler cannot rematerialise (an LDS base
 // address used by many asm operands: no v_mov per use)
 __device__ __forceinline__ uint32_t to_vgpr(uint32_t x) {
@@ -446,18 +452,26 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   auto step = [&](auto J, int s) {
     constexpr int j = decltype(J)::value, jp = (j + kU - 1) % kU;
     const int64_t rbase = yanchor + dir * (s - D);
-    d4 v = level(r0, r1, r2, rbase - dir * PB);
-    if constexpr (PAIR && PB < PE) {  // level PB+1 reads level PB of step s-1 (W[0][1])
-      lds_load_lane<xoff(jp, PB) + kLev>(xw, W[0][1].x, m_edge);
-      lds_load_lane<xoff(jp, PB) + kLev>(xw, W[0][1].w, m_edge);
+    if constexpr (PAIR) {
+      // every level's neighbour column of step s-1, into the scratch lane of
+      // W[k][1] (level PB + k of step s-1, read by level PB + k + 1), all
+      // issued at the step start so each is in flight for a level or more
+      static_for<0, NL - 1>([&](auto Kc) {
+        constexpr int k = decltype(Kc)::value;
+        lds_load_lane<xoff(jp, PB + k) + kLev>(xw, W[k][1].x, m_edge);
+        lds_load_lane<xoff(jp, PB + k) + kLev>(xw, W[k][1].w, m_edge);
+      });
     }
+    d4 v = level(r0, r1, r2, rbase - dir * PB);
     __builtin_amdgcn_sched_barrier(0);
     static_for<PB + 1, PE + 1>([&](auto Q) {
       constexpr int p = decltype(Q)::value;  // PB+1 .. PE, bottom-up
       if constexpr (PAIR) {
         // the neighbour's level p-1 of step s-1 is in the scratch lane of
         // W[p-1-PB][1]; this strip's level p-1 of step s (v) goes out
-        lds_wait(W[p - 1 - PB][1].x, W[p - 1 - PB][1].w);
+        // younger than level p-1's loads: the later levels' loads and the
+        // stores of the levels before: 2 (NL - 2) ops, whatever p is
+        lds_wait<(2 * (NL - 2) < 15 ? 2 * (NL - 2) : 15)>(W[p - 1 - PB][1].x, W[p - 1 - PB][1].w);
         lds_store_lane<xoff(j, p - 1)>(xw, v.w, m_edge);
         lds_store_lane<xoff(j, p - 1) + 2 * kLev>(xw, v.x, m_edge);
       }
@@ -465,10 +479,6 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
       W[p - 1 - PB][0] = W[p - 1 - PB][1];  // rows of steps s-1 and s become s-2 and s-1
       W[p - 1 - PB][1] = v;
       v = nv;
-      if constexpr (PAIR && p < PE) {  // for level p+1: the neighbour's level p of step s-1
-        lds_load_lane<xoff(jp, p) + kLev>(xw, W[p - PB][1].x, m_edge);
-        lds_load_lane<xoff(jp, p) + kLev>(xw, W[p - PB][1].w, m_edge);
-      }
       __builtin_amdgcn_sched_barrier(0);
     });
     if constexpr (kOut) {

@@ -114,8 +114,49 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
     Span2D<double> f(buf_[b].data() + (xo_ - g_), nx_ + 2 * g_, ny_ + 2 * g_, ld_);
     halo_[b] = std::make_unique<Halo2D>(t_, f, g_, g_, nb_, false, GMT_SPACE_DEVICE, ks_ > 1);
   }
+  if (ks_ > 1 && halo_[0]->active() && (c.overlap || c.overlap_auto)) split_cus();
   if (c.overlap_auto) autotune_overlap();
   if (c.graph) capture_graphs();
+}
+
+// Band-first passes run the pass and the exchange on disjoint compute units.
+// A fused pass keeps every CU's wave slots full (2 waves per SIMD, one round
+// of resident workgroups on the shares), so exchange kernels on a stream of
+// their own — pack, RCCL or staging copies, unpack, 256-thread workgroups —
+// could only start as whole CUs drained, i.e. at the end of the pass
+// (profiles/r03_shares.md).  GMT_COMM_CUS = 8, 16 or 24 CUs (the same
+// number from every XCD) are reserved for the exchange while band-first
+// passes run; serial passes keep every CU.  Off by default: measured slower
+// on one GPU (profiles/r03_shares.md, "reserved CUs").
+void JacobiSolver::split_cus() {
+  int cus = 0;
+  if (gmt_rt_device_cu_count(&cus) != 0 || cus < 16) return;
+  const char* e = std::getenv("GMT_COMM_CUS");
+  const int n = e ? std::atoi(e) : 0;
+  if (n <= 0 || n > 24 || n % 8 || cus != 256) return;  // MI355X: 8 XCDs x 32 CUs
+  const int words = (cus + 31) / 32;
+  std::vector<uint32_t> comm(words, 0u), comp(words, 0u);
+  // the same number of CUs from every XCD (8 of them, 32 CUs each), whether
+  // the runtime numbers CUs XCD by XCD or round-robin over the XCDs: CU
+  // 33 x + 8 y is on XCD x either way (x < 8, 8 y + 7 < 32)
+  for (int i = 0; i < n; ++i) {
+    const int cu = ((i % 8) * 33 + (i / 8) * 8) % cus;
+    comm[cu / 32] |= 1u << (cu % 32);
+  }
+  for (int cu = 0; cu < cus; ++cu)
+    if (!(comm[cu / 32] >> (cu % 32) & 1u)) comp[cu / 32] |= 1u << (cu % 32);
+  gmt_stream_t cs = nullptr, sb = nullptr;
+  if (gmt_rt_stream_create_cumask(&cs, words, comm.data()) != 0) return;
+  if (gmt_rt_stream_create_cumask(&sb, words, comp.data()) != 0) {
+    gmt_rt_stream_destroy(cs);
+    return;
+  }
+  GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));
+  gmt_rt_stream_destroy(cs_);
+  cs_ = cs;
+  sb_ = sb;
+  comm_cus_ = n;
+  GMT_CHECK("event", gmt_rt_event_create(&ev_band_, 0));
 }
 
 void JacobiSolver::init_field() {
@@ -234,13 +275,16 @@ void JacobiSolver::autotune_overlap() {
 JacobiSolver::~JacobiSolver() {
   if (s_) gmt_rt_stream_synchronize(s_);
   if (cs_) gmt_rt_stream_synchronize(cs_);
+  if (sb_) gmt_rt_stream_synchronize(sb_);
   for (auto& g : graph_) gmt_rt_graph_destroy(g);
   for (auto& g : graph2_) gmt_rt_graph_destroy(g);
   gmt_rt_event_destroy(ev_start_);
   gmt_rt_event_destroy(ev_halo_);
+  if (ev_band_) gmt_rt_event_destroy(ev_band_);
   halo_[0].reset();
   halo_[1].reset();
   gmt_rt_stream_destroy(cs_);
+  if (sb_) gmt_rt_stream_destroy(sb_);
   gmt_rt_stream_destroy(s_);
 }
 
@@ -288,7 +332,8 @@ int JacobiSolver::halo_mask() const {
          (nb_.north >= 0 ? 8 : 0);
 }
 
-void JacobiSolver::xk_launch(int K, int n, const int64_t* rects, int parity, int sig_rects, int sig_rows) {
+void JacobiSolver::xk_launch(int K, int n, const int64_t* rects, int parity, int sig_rects, int sig_rows,
+                             gmt_stream_t st) {
   const double* u = buf_[parity].data();
   double* un = buf_[parity ^ 1].data();
   const int64_t dom[4] = {xo_, nx_, yo_, ny_};
@@ -296,8 +341,8 @@ void JacobiSolver::xk_launch(int K, int n, const int64_t* rects, int parity, int
   unsigned* count = reinterpret_cast<unsigned*>(sig_.data());
   const bool sig = sig_rects > 0 || sig_rows > 0;
   gmt_tb_opts o{K,   cfg_.wg_waves, cfg_.seg_rows, exact_ ? 1 : 0, sig_rects, sig ? count : nullptr,
-                sig ? sig_.data() + 1 : nullptr, sig_rows};
-  GMT_CHECK("jacobi tb", gmt_jacobi5tb(&o, n, rects, dom, mask, u, un, ld_, ny_ + 2 * g_, s_));
+                sig ? sig_.data() + 1 : nullptr, sig_rows, st == sb_ && sb_ ? comm_cus_ : 0};
+  GMT_CHECK("jacobi tb", gmt_jacobi5tb(&o, n, rects, dom, mask, u, un, ld_, ny_ + 2 * g_, st ? st : s_));
 }
 
 // Output rects of a band-first pass.  W/E halo sides: full-height bands one
@@ -364,7 +409,14 @@ void JacobiSolver::enqueue_block(int parity, int K) {
   // pass), and its wait kernel is enqueued after it
   GMT_CHECK("event", gmt_rt_event_record(ev_start_, s_));
   GMT_CHECK("wait", gmt_rt_stream_wait_event(cs_, ev_start_));
-  xk_launch(K, nb + 1, rects, parity, nb, rows);
+  if (sb_) {  // the pass on the compute CUs, joined back into s_ below
+    GMT_CHECK("wait", gmt_rt_stream_wait_event(sb_, ev_start_));
+    xk_launch(K, nb + 1, rects, parity, nb, rows, sb_);
+    GMT_CHECK("event", gmt_rt_event_record(ev_band_, sb_));
+    GMT_CHECK("wait", gmt_rt_stream_wait_event(s_, ev_band_));
+  } else {
+    xk_launch(K, nb + 1, rects, parity, nb, rows);
+  }
   GMT_CHECK("signal wait", gmt_signal_wait(sig_.data() + 1, sig_.data() + 2,
                                            reinterpret_cast<unsigned*>(sig_.data() + 3), cs_));
   Halo2D& hn = *halo_[parity ^ 1];
@@ -552,6 +604,7 @@ void JacobiSolver::step() {
 void JacobiSolver::synchronize() {
   GMT_CHECK("sync", gmt_rt_stream_synchronize(s_));
   GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));
+  if (sb_) GMT_CHECK("sync", gmt_rt_stream_synchronize(sb_));
   uint64_t err = 0;
   GMT_CHECK("signal D2H", gmt_rt_memcpy(&err, sig_.data() + 3, sizeof(err)));
   if (err != 0) {
@@ -585,12 +638,15 @@ double JacobiSolver::residual() {
 void JacobiSolver::exchange_only() {
   Halo2D& h = *halo_[parity_];
   // the exchange packs the current field and writes its ghost ring: order it
-  // after every pass already enqueued on the compute stream
+  // after every pass already enqueued on the compute stream (on the compute
+  // stream itself when the comm stream is held to a few CUs: this is the
+  // blocking exchange bench.py times, and it has the GPU to itself)
+  gmt_stream_t st = sb_ ? s_ : cs_;
   GMT_CHECK("event", gmt_rt_event_record(ev_start_, s_));
-  GMT_CHECK("wait", gmt_rt_stream_wait_event(cs_, ev_start_));
-  h.start(cs_);
-  h.finish(cs_);
-  GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));
+  GMT_CHECK("wait", gmt_rt_stream_wait_event(st, ev_start_));
+  h.start(st);
+  h.finish(st);
+  GMT_CHECK("sync", gmt_rt_stream_synchronize(st));
   fresh_[parity_] = true;
 }
 

@@ -217,6 +217,11 @@ int gmt_rt_stream_create(gmt_stream_t* s, int) {
   *s = reinterpret_cast<gmt_stream_t>(new char[1]);
   return kOk;
 }
+int gmt_rt_stream_create_cumask(gmt_stream_t* s, int, const uint32_t*) { return gmt_rt_stream_create(s, 0); }
+int gmt_rt_device_cu_count(int* n) {
+  *n = 1;
+  return kOk;
+}
 int gmt_rt_stream_destroy(gmt_stream_t s) {
   delete[] reinterpret_cast<char*>(s);
   return kOk;

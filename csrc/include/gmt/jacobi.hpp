@@ -130,7 +130,8 @@ class JacobiSolver {
   void enqueue_step(int parity);
   void enqueue_block(int parity, int k);  // k <= ks_ fused sweeps
   // one fused k-sweep launch on `n` output rects (gmt_jacobi5tb)
-  void xk_launch(int k, int n, const int64_t* rects, int parity, int sig_rects, int sig_rows);
+  void xk_launch(int k, int n, const int64_t* rects, int parity, int sig_rects, int sig_rows,
+                 gmt_stream_t st = nullptr);
   bool band_rects(int k, int64_t* rects, int* n_bands, int* sig_rows) const;
   bool band_mode(int k) const;  // the fused k-sweep pass runs band-first (overlap)
   void exchange_now(int parity);  // blocking-order halo exchange of buf_[parity] on the compute stream
@@ -142,6 +143,7 @@ class JacobiSolver {
   void calibrate_costs();
   double measure_max_abs();
   int halo_mask() const;
+  void split_cus();
 
   comm::Transport& t_;
   JacobiConfig cfg_;
@@ -157,7 +159,13 @@ class JacobiSolver {
   Buffer<uint64_t> sig_;  // band-first completion signal (GMT_SPACE_FLAGS)
   bool fresh_[2] = {false, false};  // buf_[b]'s ghost ring holds the neighbours' current values
   gmt_stream_t s_ = nullptr, cs_ = nullptr;
-  gmt_event_t ev_start_ = nullptr, ev_halo_ = nullptr;
+  // band-first passes on split compute units (split_cus): the pass on sb_
+  // (all but a few CUs), the exchange on cs_ (those few), so the exchange's
+  // kernels start the moment the bands signal instead of waiting for the
+  // pass's resident workgroups to retire
+  gmt_stream_t sb_ = nullptr;
+  int comm_cus_ = 0;
+  gmt_event_t ev_start_ = nullptr, ev_halo_ = nullptr, ev_band_ = nullptr;
   gmt_graph_t graph_[2] = {nullptr, nullptr};   // single sweep, per parity
   gmt_graph_t graph2_[2] = {nullptr, nullptr};  // fused ks_-sweep block, per parity
   int parity_ = 0;  // buf_[parity_] holds the current u

@@ -155,6 +155,10 @@ typedef struct gmt_tb_opts {
      are ready long before the rect is.  No extra workgroups (the band
      rects of signal_rects each cost a pipeline warm-up and launch slots). */
   int signal_rows;
+  /* Compute units the launch's stream may not use (a CU-masked stream, see
+     gmt_rt_stream_create_cumask): the segment planner sizes the launch for
+     the resident workgroups of the remaining ones (0 = every CU). */
+  int reserved_cus;
 } gmt_tb_opts;
 int gmt_jacobi5tb_supported(int sweeps);
 /* Largest sweep count whose kernel runs without scratch: GMT_TB_MAX_SWEEPS

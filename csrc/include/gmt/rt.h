@@ -98,6 +98,12 @@ int gmt_rt_mem_prefetch_async(const void* p, size_t bytes, int device, gmt_strea
 
 /* ---- streams / events / graphs */
 int gmt_rt_stream_create(gmt_stream_t* s, int high_priority);
+/* A stream whose kernels run only on the compute units whose bits are set
+   in mask[0..n_words) (bit i of word w = CU 32 w + i; hipExtStreamCreateWithCUMask).
+   The host backend ignores the mask. */
+int gmt_rt_stream_create_cumask(gmt_stream_t* s, int n_words, const uint32_t* mask);
+/* compute units of the current device */
+int gmt_rt_device_cu_count(int* n);
 int gmt_rt_stream_destroy(gmt_stream_t s);
 int gmt_rt_stream_synchronize(gmt_stream_t s);
 int gmt_rt_stream_wait_event(gmt_stream_t s, gmt_event_t e);

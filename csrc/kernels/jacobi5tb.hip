@@ -108,7 +108,7 @@ int jacobi5tb_run(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, con
   const int K = o.sweeps;
   if (!gmt_jacobi5tb_supported(K)) return static_cast<int>(hipErrorInvalidValue);
   if (n_rect < 0 || n_rect > kMaxRect) return static_cast<int>(hipErrorInvalidValue);
-  if (o.wg_waves < 0 || o.wg_waves > kMaxThreads / kWave || o.seg_rows < 0 || o.signal_rects < 0 ||
+  if (o.wg_waves < 0 || o.wg_waves > kMaxThreads / kWave || o.seg_rows < 0 || o.signal_rects < 0 || o.reserved_cus < 0 ||
       o.signal_rects > n_rect || ((o.signal_rects > 0 || o.signal_rows > 0) && (!o.signal_count || !o.signal)) ||
       o.signal_rows < 0 || (o.signal_rows > 0 && o.signal_rects >= n_rect))
     return static_cast<int>(hipErrorInvalidValue);

@@ -641,6 +641,12 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     per_cu = occ * cus;
     if (slot) slot->store(per_cu, std::memory_order_relaxed);
   }
+  // a CU-masked stream: the resident workgroups of the CUs it may use
+  if (o.reserved_cus > 0) {
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (o.reserved_cus < cus) per_cu = static_cast<int>(static_cast<int64_t>(per_cu) * (cus - o.reserved_cus) / cus);
+  }
   const int sig_rects = o.signal_rects;  // non-empty rects (checked): the same indices after the compaction
   // row bands: the first rect after the signalling ones (checked non-empty)
   const int rbk = o.signal_rows > 0 ? sig_rects : -1;

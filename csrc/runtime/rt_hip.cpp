@@ -167,6 +167,18 @@ int gmt_rt_stream_create(gmt_stream_t* s, int high_priority) {
   *s = reinterpret_cast<gmt_stream_t>(h);
   RT_RET(e);
 }
+int gmt_rt_stream_create_cumask(gmt_stream_t* s, int n_words, const uint32_t* mask) {
+  hipStream_t h = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&h, static_cast<uint32_t>(n_words), mask);
+  *s = reinterpret_cast<gmt_stream_t>(h);
+  RT_RET(e);
+}
+int gmt_rt_device_cu_count(int* n) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(n, hipDeviceAttributeMultiprocessorCount, dev);
+  RT_RET(e);
+}
 int gmt_rt_stream_destroy(gmt_stream_t s) { RT_RET(s ? hipStreamDestroy(S(s)) : hipSuccess); }
 int gmt_rt_stream_synchronize(gmt_stream_t s) { RT_RET(hipStreamSynchronize(S(s))); }
 int gmt_rt_stream_wait_event(gmt_stream_t s, gmt_event_t e) {

@@ -53,6 +53,8 @@ class TbOpts(ctypes.Structure):
         ("signal_rects", c_int),
         ("signal_count", c_vp),
         ("signal", c_vp),
+        ("signal_rows", c_int),
+        ("reserved_cus", c_int),
     ]
 
 _SIGS = {
