@@ -95,12 +95,13 @@ def test_engine_dirichlet_repeated_runs(env, tblock):
     assert float(np.abs(got - ref).max()) < 1e-13
 
 
-def _app(args, np_=None, timeout=120):
+def _app(args, np_=None, timeout=120, env=None):
     exe = os.path.join(BIN, args[0])
     if not os.path.exists(exe):
         pytest.fail(f"{exe} not built (run make all / __graft_entry__.build())")
     cmd = [exe, *args[1:]] if np_ is None else [MPIRUN, "-np", str(np_), exe, *args[1:]]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd="/tmp")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd="/tmp",
+                       env=None if env is None else dict(os.environ, **env))
     assert p.returncode == 0, f"{' '.join(cmd)} rc={p.returncode}\n{p.stdout[-3000:]}\n{p.stderr[-3000:]}"
     return p.stdout
 
@@ -143,6 +144,17 @@ def test_app_jacobi_band_first(np_, transport, extra):
     nx = 3000 * (3 if "--dims=1x3" in extra else 1)  # 3 x 432-column W/E bands per rank at K = 20
     out = _app(["mpi_jacobi2d", f"--ny=400", f"--nx={nx}", "0", "45", "--check", "--tblock", "--tsteps=20",
                 "--warmup=20", f"--transport={transport}", *extra], np_=np_)
+    assert "overlap=1 (band-first)" in out, out
+    m = re.search(r"check\s*: max\|diff\| vs serial = ([0-9.eE+-]+) OK", out)
+    assert m and float(m.group(1)) == 0.0, out
+
+
+@pytest.mark.parametrize("cus", ["8", "16"])
+def test_app_jacobi_band_first_reserved_cus(cus):
+    """Opt-in CU partition (GMT_COMM_CUS): band-first passes on a CU-masked
+    stream, the exchange on the reserved CUs; still bitwise."""
+    out = _app(["mpi_jacobi2d", "--ny=900", "--nx=3000", "0", "45", "--check", "--tblock", "--tsteps=20",
+                "--warmup=20", "--periodic", "--transport=rccl"], env={"GMT_COMM_CUS": cus})
     assert "overlap=1 (band-first)" in out, out
     m = re.search(r"check\s*: max\|diff\| vs serial = ([0-9.eE+-]+) OK", out)
     assert m and float(m.group(1)) == 0.0, out
