@@ -120,9 +120,12 @@ __global__ __launch_bounds__(kBlock) void ipc_exchange_kernel(Args a) {
       for (int64_t o = lo + threadIdx.x; o < hi; o += kBlock) dst[o] = src[o];
     }
   }
-  __threadfence_system();
+  // every wave's copies complete (the barrier waits for them), then ONE
+  // system-scope release for the workgroup: the L2 writeback it implies
+  // covers every wave's stores, four of them cost four writebacks
   __syncthreads();
   if (threadIdx.x == 0) {
+    __threadfence_system();
     // each role signals on its own: a rank's "ready" must not wait for its
     // own receives (those wait for the peers' "ready")
     if (last_arrival(a.counter + (send ? 0 : 1), static_cast<unsigned>(nrb))) {
