@@ -55,9 +55,6 @@ struct Args {
   uint64_t timeout_ticks;  // device wall-clock ticks per wait
 };
 
-__device__ __forceinline__ uint64_t load_sys(const uint64_t* p) {
-  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
 // the last of `total` arrivals on *c (thread 0 of each workgroup) resets it
 __device__ __forceinline__ bool last_arrival(unsigned* c, unsigned total) {
@@ -70,17 +67,20 @@ __device__ __forceinline__ bool last_arrival(unsigned* c, unsigned total) {
 // record `code` in *err (a plain system-scope store: any non-zero is an error).
 // Once an exchange of the plan has failed, later ones do not wait again (the
 // host aborts at its next synchronisation; queued exchanges drain quickly).
+// (relaxed polls of the uncached flag, one system-scope acquire after the
+// flag is seen: an acquire per poll would invalidate the caches every time)
 __device__ __forceinline__ void bounded_wait(const uint64_t* flag, uint64_t want, uint64_t ticks, unsigned* err,
                                              unsigned code) {
   if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
   const uint64_t t0 = wall_clock64();
-  while (load_sys(flag) < want) {
-    __builtin_amdgcn_s_sleep(4);
+  while (__hip_atomic_load(const_cast<uint64_t*>(flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+    __builtin_amdgcn_s_sleep(1);
     if (wall_clock64() - t0 > ticks) {
       __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
   }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the peer's data is read after this
 }
 
 __global__ __launch_bounds__(kBlock) void ipc_exchange_kernel(Args a) {
@@ -131,7 +131,9 @@ __global__ __launch_bounds__(kBlock) void ipc_exchange_kernel(Args a) {
     if (last_arrival(a.counter + (send ? 0 : 1), static_cast<unsigned>(nrb))) {
       for (int j = k0; j < k1; ++j) {
         uint64_t* sig = a.chan[j].signal;
-        if (sig) __hip_atomic_store(sig, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // relaxed: the workgroup's system-scope release fence above (and the
+        // other workgroups' before their arrivals) already published the data
+        if (sig) __hip_atomic_store(sig, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
     if (last_arrival(a.counter + 2, static_cast<unsigned>(a.sb + a.rb)))
