@@ -407,6 +407,7 @@ void JacobiSolver::enqueue_block(int parity, int K) {
   }
   // the comm stream forks before the launch (so it never waits for the whole
   // pass), and its wait kernel is enqueued after it
+  band_ran_ = true;
   GMT_CHECK("event", gmt_rt_event_record(ev_start_, s_));
   GMT_CHECK("wait", gmt_rt_stream_wait_event(cs_, ev_start_));
   if (sb_) {  // the pass on the compute CUs, joined back into s_ below
@@ -438,6 +439,7 @@ void JacobiSolver::step_block() {
     // a band-first graph starts from a current halo (it was captured so)
     const bool band = band_mode(ks_);
     if (band && !fresh_[parity_]) exchange_now(parity_);
+    band_ran_ = band_ran_ || band;
     GMT_CHECK("graph launch", gmt_rt_graph_launch(graph2_[parity_], s_));
     fresh_[parity_ ^ 1] = band;
   } else {
@@ -603,14 +605,21 @@ void JacobiSolver::step() {
 
 void JacobiSolver::synchronize() {
   GMT_CHECK("sync", gmt_rt_stream_synchronize(s_));
-  GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));
-  if (sb_) GMT_CHECK("sync", gmt_rt_stream_synchronize(sb_));
-  uint64_t err = 0;
-  GMT_CHECK("signal D2H", gmt_rt_memcpy(&err, sig_.data() + 3, sizeof(err)));
-  if (err != 0) {
-    std::printf("JacobiSolver: a band-first pass timed out waiting for its boundary bands (error %llu)\n",
-                static_cast<unsigned long long>(err));
-    abort_job(EXIT_FAILURE);
+  // band-first passes fork to the side streams and join back into s_ (and
+  // graph replays of them run on s_), so s_ covers them; the side streams
+  // are synchronised and the band signal's error word read only after an
+  // eager band-first pass (serial passes use neither)
+  if (band_ran_) {
+    GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));
+    if (sb_) GMT_CHECK("sync", gmt_rt_stream_synchronize(sb_));
+    uint64_t err = 0;
+    GMT_CHECK("signal D2H", gmt_rt_memcpy(&err, sig_.data() + 3, sizeof(err)));
+    if (err != 0) {
+      std::printf("JacobiSolver: a band-first pass timed out waiting for its boundary bands (error %llu)\n",
+                  static_cast<unsigned long long>(err));
+      abort_job(EXIT_FAILURE);
+    }
+    band_ran_ = false;
   }
   // a halo exchange that timed out (IPC) left stale ghost cells: fail loudly
   for (auto& h : halo_)

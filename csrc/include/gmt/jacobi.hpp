@@ -165,6 +165,10 @@ class JacobiSolver {
   // pass's resident workgroups to retire
   gmt_stream_t sb_ = nullptr;
   int comm_cus_ = 0;
+  // a band-first pass was enqueued since the last synchronize(): only then
+  // do the side streams and the band signal's error word need a look (a
+  // D2H read and two stream syncs are ~2% of an N = 8 pass)
+  bool band_ran_ = false;
   gmt_event_t ev_start_ = nullptr, ev_halo_ = nullptr, ev_band_ = nullptr;
   gmt_graph_t graph_[2] = {nullptr, nullptr};   // single sweep, per parity
   gmt_graph_t graph2_[2] = {nullptr, nullptr};  // fused ks_-sweep block, per parity
