@@ -87,6 +87,23 @@ def test_bench_two_ranks_torchrun_cpu(transport):
     assert rec["stencil_alt_dims"] == f"{px}x{py}" and rec["stencil_alt_dims_MLUPS"] > 0
 
 
+def test_bench_eight_ranks_driver_shape_cpu():
+    """The driver's N = 8 launch shape (one node, 8 ranks, strong scaling) on
+    gloo: the 4x2 grid is timed and bitwise-gated, the swapped 2x4 grid that
+    BASELINE names is timed too, and every BASELINE key is in the one line."""
+    port = str(free_port())
+    rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "8",
+                "--device", "cpu", "--size", "512", "--steps", "20", "--warmup", "5",
+                "--daxpy-n", "20000", "--ref-n-local", "32", "--ref-n-other", "300",
+                "--ref-iters", "4", "--small-size", "128"], GMT_TRANSPORT="rccl")
+    _check(rec, 8, 20, 5, points=512 * 512)
+    _baseline_keys(rec, 128)
+    assert rec["config"]["parallelism"].startswith("spatial2d py4 x px2")
+    assert rec["stencil_alt_dims"] == "2x4" and rec["stencil_alt_dims_MLUPS"] > 0
+    assert rec["ref_halo_dim0_rel_err"] < 1e-6 and rec["ref_halo_dim1_rel_err"] < 1e-6
+
+
 def test_bench_two_ranks_weak_scaling_cpu():
     """--scaling weak: size x size per rank, the global domain grows with N."""
     port = str(free_port())
