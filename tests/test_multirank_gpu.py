@@ -54,6 +54,8 @@ def _need_gpu():
 @pytest.mark.parametrize("n,extra,name", [
     (2, ["--overlap", "on"], "n2_overlap_on"),
     (4, ["--dims", "2x2"], "n4_dims2x2"),
+    # the driver's N = 8 launch: default 4x2 grid, BASELINE's 2x4 timed too
+    (8, [], "n8_driver_shape"),
 ])
 def test_bench_oversubscribed_ipc(n, extra, name):
     p = _torchrun(n, ["--size", "8192", "--steps", "20", "--warmup", "5", "--daxpy-n", str(1 << 24),
@@ -83,6 +85,9 @@ def test_bench_oversubscribed_ipc(n, extra, name):
         assert rec["config"]["parallelism"].endswith("overlap")
         # the swapped process grid is timed too (2x1 -> 1x2), same engine path
         assert rec["stencil_alt_dims"] == "1x2" and rec["stencil_alt_dims_MLUPS"] > 0
+    if n == 8:
+        assert "py4 x px2" in rec["config"]["parallelism"]
+        assert rec["stencil_alt_dims"] == "2x4" and rec["stencil_alt_dims_MLUPS"] > 0
 
 
 def test_bench_ipc_peer_hang_fails_the_job():
