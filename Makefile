@@ -40,7 +40,7 @@ MPI_LIBS  := $(MPI_HOME)/lib/libmpi.so -Wl,-rpath,$(MPI_HOME)/lib -static-libstd
 
 KERNEL_SRCS := $(wildcard csrc/kernels/*.hip)
 KERNEL_OBJS := $(patsubst csrc/kernels/%.hip,$(OBJ)/kernels/%.o,$(KERNEL_SRCS))
-KERNEL_HDRS := $(wildcard csrc/kernels/*.hpp) csrc/include/gmt/kernels.h
+KERNEL_HDRS := $(wildcard csrc/kernels/*.hpp) csrc/include/gmt/kernels.h csrc/include/gmt/tb_geom.h
 RT_OBJ      := $(OBJ)/runtime/rt_hip.o
 CCL_OBJ     := $(OBJ)/runtime/ccl_rccl.o
 HOST_OBJS   := $(OBJ)/host/kernels_host.o $(OBJ)/host/rt_host.o
@@ -80,7 +80,7 @@ $(LIB_CCL): $(CCL_OBJ) $(LIB)
 	$(CXX) -shared -fPIC -o $@ $(CCL_OBJ) -Wl,-soname,libgmt_ccl.so \
 	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lrccl -lamdhip64
 
-$(OBJ)/host/%.o: csrc/host/%.cpp csrc/include/gmt/rt.h csrc/include/gmt/kernels.h csrc/include/gmt/ccl.h
+$(OBJ)/host/%.o: csrc/host/%.cpp csrc/include/gmt/rt.h csrc/include/gmt/kernels.h csrc/include/gmt/ccl.h csrc/include/gmt/tb_geom.h
 	@mkdir -p $(dir $@)
 	$(CXX) $(HOSTFLAGS) -c $< -o $@
 

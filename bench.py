@@ -57,9 +57,18 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 DEFAULT_TSTEPS = 20  # max fused sweeps per memory pass / halo exchange; the engine plans the mix (profiles/r02_tb.md)
 
 from gpu_mpi_tests_amd import ops  # noqa: E402
-from gpu_mpi_tests_amd.engine import MAX_TSTEPS  # noqa: E402
+from gpu_mpi_tests_amd.engine import MAX_TSTEPS, watchdog_timeout  # noqa: E402
 from gpu_mpi_tests_amd.parallel import dist as gdist  # noqa: E402
 from gpu_mpi_tests_amd.parallel.decomp import choose_dims  # noqa: E402
+
+
+def mark(env, phase):
+    """Progress mark for the engine's hang watchdog (armed by the first engine
+    call; GMT_TIMEOUT seconds without a mark end the job with status 124 and a
+    line naming the rank and this phase)."""
+    from gpu_mpi_tests_amd.engine import watchdog_kick
+
+    watchdog_kick(f"bench.py: {phase}", "cuda" if env.is_gpu else "cpu")
 
 
 def _sync(env):
@@ -345,7 +354,12 @@ def main(argv=None):
                     help="reference halo benchmark: extent of the other axis (default 512Ki: 8 MiB faces)")
     ap.add_argument("--ref-iters", type=int, default=100, help="reference halo benchmark: timed exchanges")
     ap.add_argument("--device", type=str, default=None, help="cuda|cpu (default: cuda if available)")
+    ap.add_argument("--timeout", type=float, default=300.0,
+                    help="hang watchdog: seconds without progress before the job fails naming the rank and "
+                         "phase (GMT_TIMEOUT overrides; 0 = off)")
     args = ap.parse_args(argv)
+    # read by the engine library when its first entry point arms the watchdog
+    os.environ.setdefault("GMT_TIMEOUT", str(args.timeout))
 
     env = gdist.init(device=args.device)
     if args.gpus != env.world_size and env.rank == 0:
@@ -363,6 +377,7 @@ def main(argv=None):
     tsteps = (args.tsteps or DEFAULT_TSTEPS) if args.tblock == "on" else 1
     extras = {}
     if not args.skip_check:
+        mark(env, "correctness gate")
         diff = check_engine(env, dims or gdims, tsteps, graph, args.init, args.seed)
         extras["check_max_diff"] = diff
         extras.update(peer_status(env, dims or gdims))
@@ -372,6 +387,7 @@ def main(argv=None):
                       file=sys.stderr)
             gdist.shutdown()
             sys.exit(3)
+    mark(env, "headline stencil run")
     solver, dt, info = bench_native(env, shape, args.steps, args.warmup, overlap, dims, graph,
                                     tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows,
                                     args.init, args.seed, not args.no_calibrate)
@@ -380,6 +396,7 @@ def main(argv=None):
     ms_per_step = dt / args.steps * 1e3
     if not args.skip_extras:
         iters = max(20, min(args.steps, 200))
+        mark(env, "halo latency")
         if env.world_size > 1:
             extras["halo_exchange_us"] = round(halo_latency(env, solver, iters) * 1e6, 2)
             extras["halo_exchange_kind"] = (f"{info['transport']}, {info['tsteps']}-wide faces + corners "
@@ -400,6 +417,7 @@ def main(argv=None):
         # swapped, so both rates are on record (profiles/r03_shares.md)
         hp, hx = info["dims"]
         if env.world_size > 1 and hp != hx and args.scaling == "strong":
+            mark(env, "swapped process grid run")
             eng3, dt3, info3 = bench_native(env, shape, args.steps, args.warmup, overlap, (hx, hp), graph,
                                             tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows,
                                             args.init, args.seed, not args.no_calibrate)
@@ -410,6 +428,7 @@ def main(argv=None):
             if env.is_gpu:
                 torch.cuda.empty_cache()
         if args.small_size:
+            mark(env, "small-domain stencil run")
             s2 = (args.small_size, args.small_size)
             steps2 = max(100, 4 * args.steps)
             eng2, dt2, info2 = bench_native(env, s2, steps2, max(args.warmup, 10), overlap, dims, graph,
@@ -420,12 +439,15 @@ def main(argv=None):
             extras[f"stencil_{args.small_size}_ms_per_step"] = round(dt2 / steps2 * 1e3, 5)
             extras[f"stencil_{args.small_size}_pass_plan"] = f"{steps2} steps: {info2['pass_plan']}"
         if env.world_size > 1:
+            mark(env, "reference halo benchmark")
             extras.update(ref_halo(env, args.ref_n_local, args.ref_n_other, args.ref_iters))
+        mark(env, "daxpy")
         gbps, ddt = bench_daxpy(env, args.daxpy_n, iters=20)
         extras["daxpy_GBps"] = round(gbps, 1)
         extras["daxpy_GBps_per_gpu"] = round(gbps / env.world_size, 1)
         extras["daxpy_n"] = args.daxpy_n
         extras["daxpy_ms"] = round(ddt * 1e3, 4)
+        mark(env, "daxpy all-reduce")
         extras.update(daxpy_allreduce(env, args.daxpy_n, iters=20))
         if not extras["daxpy_allsum_rel_err"] <= 1e-9:
             if env.rank == 0:
@@ -437,6 +459,8 @@ def main(argv=None):
     else:
         solver.close()
     py, px = info["dims"] if info.get("dims") else gdims
+    mark(env, "report")
+    extras["watchdog_timeout_s"] = watchdog_timeout("cuda" if env.is_gpu else "cpu")
     if env.rank == 0:
         rec = {
             "metric": "2D 5-pt Jacobi stencil MLUPS (fp64)",

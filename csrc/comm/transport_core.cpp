@@ -1,5 +1,7 @@
 // MPI-free transports: rccl (bootstrapped from a distributed unique id) and
 // local (single process).  See gmt/transport.hpp.
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -47,7 +49,14 @@ class RcclTransport : public Transport {
                   gmt_rt_backend_name());
       abort_job(EXIT_FAILURE);
     }
-    GMT_CCL_CHECK("comm init", gmt_ccl_comm_init(&cc_, size_, &id, rank_));
+    const int e = gmt_ccl_comm_init(&cc_, size_, &id, rank_);
+    if (e != 0) {
+      char host[256] = "?";
+      gethostname(host, sizeof(host) - 1);
+      std::fprintf(stderr, "GMT: rank %d of %d (host %s): RCCL communicator init failed: %s (%d)\n", rank_, size_,
+                   host, gmt_ccl_error_string(e), e);
+      abort_job(e == GMT_CCL_TIMEOUT ? 124 : EXIT_FAILURE);
+    }
   }
   ~RcclTransport() override { gmt_ccl_comm_destroy(cc_); }
   Kind kind() const override { return Kind::Rccl; }

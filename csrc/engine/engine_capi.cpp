@@ -1,4 +1,5 @@
 // C ABI of the native Jacobi engine (gmt/engine.h) for the Python package.
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -6,10 +7,13 @@
 #include <memory>
 #include <vector>
 
+#include <unistd.h>
+
 #include "gmt/control.hpp"
 #include "gmt/engine.h"
 #include "gmt/jacobi.hpp"
 #include "gmt/kernels.h"
+#include "gmt/watchdog.hpp"
 
 namespace {
 struct Handle {
@@ -21,6 +25,29 @@ struct Handle {
 }  // namespace
 
 namespace gmt {
+namespace {
+// The engine runs inside a Python process: a job-wide abort (a failed check,
+// the watchdog firing from its own thread while the main thread is blocked
+// in a collective) must end the process at once, not run exit handlers that
+// wait on the hung device or communicator; the launcher then tears the other
+// ranks down.
+[[noreturn]] void engine_abort(int code) {
+  std::fflush(stdout);
+  std::fflush(stderr);
+  _exit(code);
+}
+}  // namespace
+
+// Arms the hang watchdog (gmt/watchdog.hpp) for an engine entry point: a
+// no-op unless GMT_TIMEOUT is set (bench.py sets a default), idempotent.
+void engine_watchdog(int rank, const char* phase) {
+  if (!abort_hook()) abort_hook() = &engine_abort;
+  int dev = -1;
+  (void)gmt_rt_get_device(&dev);
+  watchdog_start(rank, dev);
+  watchdog_kick(phase);
+}
+
 // Transport of an engine handle (also used by deriv_bench.cpp); nullptr when
 // the request is invalid.
 std::unique_ptr<comm::Transport> engine_transport(int rank, int world, int transport, const void* id) {
@@ -28,13 +55,20 @@ std::unique_ptr<comm::Transport> engine_transport(int rank, int world, int trans
   if (transport == GMT_ENGINE_RCCL) {
     gmt_ccl_id cid;
     std::memcpy(&cid, id, sizeof(cid));
-    return comm::make_rccl_transport(rank, world, cid);
+    engine_watchdog(rank, "engine: rccl communicator init");
+    auto t = comm::make_rccl_transport(rank, world, cid);
+    watchdog_kick("engine: rccl communicator ready");
+    return t;
   }
   if (transport == GMT_ENGINE_IPC) {
     if (!id) return nullptr;
-    return comm::make_ipc_transport(comm::make_socket_control(rank, world, static_cast<const char*>(id)));
+    engine_watchdog(rank, "engine: ipc control plane connect");
+    auto t = comm::make_ipc_transport(comm::make_socket_control(rank, world, static_cast<const char*>(id)));
+    watchdog_kick("engine: ipc transport ready");
+    return t;
   }
   if (world != 1) return nullptr;
+  engine_watchdog(rank, "engine: local transport");
   return comm::make_local_transport();
 }
 }  // namespace gmt
@@ -73,6 +107,19 @@ int gmt_engine_comm_allreduce_sum(void* h, double* buf, int64_t n, void* stream)
 const char* gmt_engine_comm_name(void* h) { return static_cast<gmt::comm::Transport*>(h)->name(); }
 void gmt_engine_comm_destroy(void* h) { delete static_cast<gmt::comm::Transport*>(h); }
 
+void gmt_engine_watchdog_kick(const char* phase) {
+  // the phase string is kept by pointer: Python passes a bytes object that
+  // may be freed, so copy it into a small ring of static slots
+  static char slots[8][96];
+  static std::atomic<unsigned> next{0};
+  char* d = slots[next.fetch_add(1) % 8];
+  std::snprintf(d, sizeof(slots[0]), "%s", phase ? phase : "python");
+  gmt::watchdog_kick(d);
+}
+double gmt_engine_watchdog_timeout(void) {
+  return gmt::watchdog_state().armed.load() ? gmt::watchdog_state().timeout : 0.0;
+}
+
 void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank, int world,
                                int transport, const void* ccl_id, const gmt_engine_opts* opts) {
   gmt_engine_opts o{};
@@ -87,6 +134,7 @@ void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank,
     delete h;
     return nullptr;
   }
+  gmt::watchdog_kick("engine: jacobi setup");
   gmt::JacobiConfig c;
   c.ny_global = ny;
   c.nx_global = nx;
@@ -107,6 +155,7 @@ void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank,
   h->py = py;
   h->px = px;
   h->s = std::make_unique<gmt::JacobiSolver>(*h->t, c);
+  gmt::watchdog_kick("engine: jacobi ready");
   return h;
 }
 
@@ -119,15 +168,18 @@ void gmt_engine_jacobi_destroy(void* p) {
 }
 
 int gmt_engine_jacobi_run(void* p, int steps) {
+  gmt::watchdog_kick("engine: jacobi run (enqueue)");
   static_cast<Handle*>(p)->s->run(steps);
   return 0;
 }
 int gmt_engine_jacobi_sync(void* p) {
+  gmt::watchdog_kick("engine: jacobi synchronize (waiting for the device)");
   static_cast<Handle*>(p)->s->synchronize();
   return 0;
 }
 double gmt_engine_jacobi_residual(void* p) { return static_cast<Handle*>(p)->s->residual(); }
 int gmt_engine_jacobi_exchange(void* p) {
+  gmt::watchdog_kick("engine: halo exchange");
   static_cast<Handle*>(p)->s->exchange_only();
   return 0;
 }

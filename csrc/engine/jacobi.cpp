@@ -35,6 +35,7 @@ void choose_dims(int world, int64_t ny, int64_t nx, int* py, int* px) {
 
 JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), cfg_(c) {
   const int rank = t.rank(), world = t.size();
+  watchdog_kick("jacobi: setup");
   if (c.py * c.px != world) {
     std::printf("JacobiSolver: process grid %dx%d != world size %d\n", c.py, c.px, world);
     abort_job(EXIT_FAILURE);
@@ -101,6 +102,7 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   // max|u| * 4^K stays finite (and no level value is subnormal).  Every
   // Jacobi sweep averages, so the initial field's max|u| — measured here on
   // the device, max over ranks — bounds every later field.
+  watchdog_kick("jacobi: max|u| all-reduce");
   umax_ = measure_max_abs();
   exact_ = c.exact == 1 || !(umax_ * std::ldexp(1.0, 2 * ks_) < 1e300);
   // exact passes stop at the largest K whose kernel fits the register file
@@ -115,8 +117,10 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
     halo_[b] = std::make_unique<Halo2D>(t_, f, g_, g_, nb_, false, GMT_SPACE_DEVICE, ks_ > 1);
   }
   if (ks_ > 1 && halo_[0]->active() && (c.overlap || c.overlap_auto)) split_cus();
+  watchdog_kick("jacobi: halo plans ready");
   if (c.overlap_auto) autotune_overlap();
   if (c.graph) capture_graphs();
+  watchdog_kick("jacobi: ready");
 }
 
 // Band-first passes run the pass and the exchange on disjoint compute units.
@@ -199,6 +203,7 @@ double JacobiSolver::measure_max_abs() {
 // cold or only hot.
 void JacobiSolver::calibrate_costs() {
   if (ks_ < 2) return;
+  watchdog_kick("jacobi: pass-cost calibration");
   std::vector<int> ks;
   for (int K = 1; K <= ks_; ++K)
     if (K == 1 || gmt_jacobi5tb_supported(K)) ks.push_back(K);
@@ -239,6 +244,7 @@ void JacobiSolver::calibrate_costs() {
 
 void JacobiSolver::autotune_overlap() {
   if (ks_ < 2 || !halo_[0]->active()) return;  // nothing to hide
+  watchdog_kick("jacobi: overlap autotune");
   Buffer<double> t(2, GMT_SPACE_DEVICE);
   double host[2] = {0.0, 0.0};
   constexpr int kPasses = 2;

@@ -30,6 +30,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <random>
@@ -44,11 +45,17 @@ enum : int {
   kOk = 0,
   kErrSys = 9002,       // socket / system call failure
   kErrArg = 9003,       // invalid argument
-  kErrTimeout = 9004,   // a peer did not connect / progress
+  kErrTimeout = GMT_CCL_TIMEOUT,  // a peer did not connect / progress
   kErrMismatch = 9005,  // message sizes of a send/recv pair differ
 };
 
 constexpr int kTimeoutMs = 120000;
+// communicator set-up deadline: GMT_CCL_INIT_TIMEOUT seconds (default 120)
+int init_timeout_ms() {
+  const char* e = std::getenv("GMT_CCL_INIT_TIMEOUT");
+  const double s = e ? std::atof(e) : 0.0;
+  return s > 0.0 ? static_cast<int>(s * 1000.0) : kTimeoutMs;
+}
 
 struct Op {
   bool send;
@@ -283,7 +290,7 @@ int gmt_ccl_comm_init(gmt_ccl_comm_t* out, int nranks, const gmt_ccl_id* id, int
         break;
       }
       ::close(f);
-      if (now_ms() - t0 > kTimeoutMs) {
+      if (now_ms() - t0 > init_timeout_ms()) {
         if (lfd >= 0) ::close(lfd);
         return bail(kErrTimeout, "comm_init: lower rank never listened");
       }
@@ -295,7 +302,7 @@ int gmt_ccl_comm_init(gmt_ccl_comm_t* out, int nranks, const gmt_ccl_id* id, int
   // accept every higher rank
   for (int k = rank + 1; k < nranks; ++k) {
     pollfd pf{lfd, POLLIN, 0};
-    if (::poll(&pf, 1, kTimeoutMs) <= 0) {
+    if (::poll(&pf, 1, init_timeout_ms()) <= 0) {
       ::close(lfd);
       return bail(kErrTimeout, "comm_init: higher rank never connected");
     }

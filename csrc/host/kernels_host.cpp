@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "gmt/kernels.h"
+#include "gmt/tb_geom.h"
 
 extern "C" {
 
@@ -259,10 +260,9 @@ int gmt_jacobi5tb(const gmt_tb_opts* o, int n_rect, const int64_t* rects, const 
 
 int64_t gmt_jacobi5tb_group_cols(int sweeps, int wg_waves) {
   if (!gmt_jacobi5tb_supported(sweeps)) return 0;
-  // the GPU kernel's strip geometry: 256 - 2 * ceil4(K) columns per strip
-  const int G = sweeps <= 10 ? 1 : 2, cap = 8 / G;
-  const int nw = std::min(wg_waves > 0 ? wg_waves : (G == 1 ? 4 : 1), cap);
-  return static_cast<int64_t>(nw) * (256 - 2 * ((sweeps + 3) / 4 * 4));
+  // the GPU kernel's strip geometry (gmt/tb_geom.h)
+  const int nw = std::min(wg_waves > 0 ? wg_waves : gmt::tb::tb_default_strips(sweeps), gmt::tb::tb_max_strips(sweeps));
+  return static_cast<int64_t>(nw) * gmt::tb::tb_strip_out(sweeps);
 }
 
 // in-order CPU streams: the signal was raised before this call runs

@@ -25,6 +25,9 @@ extern "C" {
 #endif
 
 #define GMT_CCL_UNAVAILABLE 9001
+/* gmt_ccl_comm_init gave up: not every rank joined within
+ * GMT_CCL_INIT_TIMEOUT seconds (default 300 with RCCL, 120 emulated) */
+#define GMT_CCL_TIMEOUT 9004
 
 typedef struct gmt_ccl_comm_s* gmt_ccl_comm_t;
 typedef struct gmt_ccl_id {

@@ -77,6 +77,12 @@ void* gmt_engine_comm_create(int rank, int world, int transport, const void* id)
 int gmt_engine_comm_allreduce_sum(void* h, double* buf, int64_t n, void* stream);
 const char* gmt_engine_comm_name(void* h);
 void gmt_engine_comm_destroy(void* h);
+/* Hang watchdog (gmt/watchdog.hpp): armed by the first engine entry point
+ * when GMT_TIMEOUT=<seconds> is set; the process exits with status 124 and a
+ * "GMT WATCHDOG: rank R ... last phase '<phase>'" line when no phase mark
+ * arrives for that long.  A caller marks progress of its own phases here. */
+void gmt_engine_watchdog_kick(const char* phase);
+double gmt_engine_watchdog_timeout(void); /* 0 when not armed */
 
 /* The reference's halo-exchange benchmark (mpi_stencil2d_gt test_deriv for
  * dim 0 and dim 1, then test_sum), n_local x n_other per rank, 2 ghosts,

@@ -161,9 +161,8 @@ extern "C" int gmt_jacobi5tb(const gmt_tb_opts* opts, int n_rect, const int64_t*
 
 extern "C" int64_t gmt_jacobi5tb_group_cols(int sweeps, int wg_waves) {
   if (!gmt_jacobi5tb_supported(sweeps)) return 0;
-  const int G = n_stages(sweeps), cap = kMaxThreads / kWave / G;
-  const int nw = std::min(wg_waves > 0 ? wg_waves : (G == 1 ? 4 : 1), cap);
-  return static_cast<int64_t>(nw) * strip_out(sweeps);
+  const int nw = std::min(wg_waves > 0 ? wg_waves : tb_default_strips(sweeps), tb_max_strips(sweeps));
+  return static_cast<int64_t>(nw) * tb_strip_out(sweeps);
 }
 
 extern "C" int gmt_jacobi5tb_plan(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, const int64_t* dom,

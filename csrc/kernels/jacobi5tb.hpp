@@ -11,35 +11,58 @@
 
 #include "common.hpp"
 #include "gmt/kernels.h"
+#include "gmt/tb_geom.h"
 
 namespace gmt {
 namespace tb {
 
 constexpr int kMaxRect = 8;
 constexpr int kMaxThreads = 512;              // 8 waves: 2 per SIMD
-constexpr int kNC = 4;                        // columns per lane
-constexpr int kCols = kNC * kWave;            // 256 columns per strip
-constexpr uint32_t kRowBytes = kCols * 8;     // one row of a strip: 2 KB
-constexpr uint32_t kSlotBytes = kRowBytes;    // DMA ring slot: two full-wave 16-B DMAs
 constexpr uint32_t kDrop = 0x80000000u;       // buffer offset past num_records: no-op access
-constexpr int kP = 6;                         // input rows in flight
-constexpr int kRS = kP + 2;                   // DMA ring: rows s-2..s in use, s+1..s+P-1 in flight
-constexpr int kHS = 6;                        // hand-off ring (2 stages): rows of steps s-4..s
-constexpr int kMaxK1 = 10;                    // largest single-wave K
-static_assert(kHS >= 5, "hand ring: rows of steps s-4..s");
 
-constexpr int ring_left(int K) { return (K + kNC - 1) / kNC * kNC; }
-constexpr int strip_out(int K) { return kCols - 2 * ring_left(K); }
-constexpr int n_stages(int K) { return K <= kMaxK1 ? 1 : 2; }
-constexpr int stage0_levels(int K) { return (K + 1) / 2; }
 // Unroll of the step loop: the register cycle of the pipeline.  A level's
 // new row is live while its step-(s-2) row is still being read, so a step
-// frees one d4 at the top level and the rows move up one register slot per
+// frees one row at the top level and the rows move up one register slot per
 // step: a value's register passes through the two slots of each of the
 // NL - 1 stored levels plus the spare, 2(NL - 1) + 1 steps.  Unrolling by
 // exactly that lets the allocator keep every row in place (no copies at the
-// back edge) at 16 VGPRs per level; ring slots are then computed per step.
+// back edge).
 constexpr int unroll_for(int NL) { return NL > 1 ? 2 * (NL - 1) + 1 : 2; }
+
+// Per-K shape (gmt/tb_geom.h).  Narrow strips re-read their three level-0
+// rows from LDS every step (the round-2/3 kernel); wide strips slide them
+// (SLIDE: one new row per step, read in the middle of the step into the
+// registers of the row level PB no longer needs), which makes the ring and
+// hand-off slots compile-time constants of the unrolled step (RS = U, HS = 3
+// divide U).
+template <int K>
+struct Cfg {
+  static constexpr int NC = tb_nc(K);           // columns per lane
+  static constexpr int S = tb_stages(K);        // waves (stages) per strip
+  static constexpr bool SLIDE = tb_wide(K);
+  static constexpr int COLS = NC * kWave;
+  static constexpr uint32_t ROW = COLS * 8;     // bytes of one strip row
+  static constexpr int NDMA = NC / 2;           // 1-KB full-wave DMAs per row
+  static constexpr int KL = tb_left(K);
+  static constexpr int WOUT = tb_strip_out(K);
+  static constexpr int NL = K / S;              // levels per stage
+  static constexpr int U = unroll_for(NL);
+  static constexpr int P = SLIDE ? 7 : 6;       // input rows in flight
+  static constexpr int RS = SLIDE ? U : P + 2;  // DMA ring slots
+  static constexpr int HS = SLIDE ? 3 : 6;      // hand-off ring slots
+  static constexpr int LAG = 2 * (S - 1);       // the output stage's step lag
+  static_assert(K % S == 0, "equal stages");
+  static_assert(NC % 2 == 0 && KL % 2 == 0, "column pairs");
+  static_assert(!SLIDE || (U % 3 == 0 && U % RS == 0 && U % HS == 0 && RS >= P + 2), "compile-time slots");
+  static_assert(SLIDE || HS >= 5, "hand ring: rows of steps s-4..s");
+};
+
+// LDS per strip: the DMA ring, plus S - 1 hand-off rings
+template <int K>
+__host__ __device__ constexpr int64_t strip_lds() {
+  using C = Cfg<K>;
+  return static_cast<int64_t>(C::RS) * C::ROW + static_cast<int64_t>(C::S - 1) * C::HS * C::ROW;
+}
 
 struct Args {
   int64_t r[kMaxRect][4];        // output rects: x0, nx, y0, ny (absolute)
@@ -78,8 +101,10 @@ struct Args {
   int64_t sig_rows, sig_total, sig_dispatch;
 };
 
-struct d4 {
-  double x, y, z, w;
+// NC doubles of one strip row held by a lane (its columns c0 .. c0+NC-1)
+template <int NC>
+struct dv {
+  double c[NC];
 };
 
 template <int I, int N, class F>
@@ -98,11 +123,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double* p, uint
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(p), 0, bytes, 0x00020000);
 }
 
-// LDS per strip: the DMA ring, plus the hand-off ring with 2 stages
-__host__ __device__ constexpr int64_t strip_lds(int stages) {
-  return static_cast<int64_t>(kRS) * kSlotBytes + (stages > 1 ? kHS * kRowBytes : 0);
-}
-
 // s_waitcnt vmcnt(n) only (expcnt / lgkmcnt left at their maxima), as a
 // compiler barrier for memory: the LDS-DMA'd rows are read by ds_read after
 // it, and the compiler does not track LDS-DMA -> ds_read dependencies
@@ -117,10 +137,35 @@ __device__ __forceinline__ void wait_vmcnt() {
 // barrier, so s_barrier needs no vmcnt(0)).
 __device__ __forceinline__ void step_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-__device__ __forceinline__ d4 lds_row(const char* slot, int lane) {
-  const d2* p = reinterpret_cast<const d2*>(slot) + 2 * lane;
-  const d2 a = p[0], b = p[1];
-  return d4{a.x, a.y, b.x, b.y};
+// a lane's NC columns of an LDS row (NC / 2 ds_read_b128)
+template <int NC>
+__device__ __forceinline__ dv<NC> lds_row(const char* slot, int lane) {
+  const d2* p = reinterpret_cast<const d2*>(slot) + (NC / 2) * lane;
+  dv<NC> r;
+  static_for<0, NC / 2>([&](auto Q) {
+    constexpr int q = decltype(Q)::value;
+    const d2 a = p[q];
+    r.c[2 * q] = a.x;
+    r.c[2 * q + 1] = a.y;
+  });
+  return r;
+}
+
+template <int NC>
+__device__ __forceinline__ void lds_put(char* slot, int lane, const dv<NC>& v) {
+  d2* p = reinterpret_cast<d2*>(slot) + (NC / 2) * lane;
+  static_for<0, NC / 2>([&](auto Q) {
+    constexpr int q = decltype(Q)::value;
+    p[q] = d2{v.c[2 * q], v.c[2 * q + 1]};
+  });
+}
+
+template <int NC>
+__device__ __forceinline__ dv<NC> dv_zero() {
+  dv<NC> r;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) r.c[j] = 0.0;
+  return r;
 }
 
 __device__ __forceinline__ u4 pack2(double a, double b) {
@@ -131,25 +176,43 @@ __device__ __forceinline__ u2 pack1(double a) {
   return u2{static_cast<unsigned>(__double2loint(a)), static_cast<unsigned>(__double2hiint(a))};
 }
 
-// One wave = one stage of one strip: levels PB..PE of the K-level pipeline.
-// PB == 1: level 0 comes from the DMA ring; otherwise from the hand-off ring
-// (rows written by stage 0 two to four steps earlier; this stage runs two
-// steps behind, D = 2, so it can read them before the step barrier).  PE == K: level K is stored to `un`; otherwise level
-// PE goes to the hand-off ring.  Strip output columns [xs, xe), rows [ys, ye).
-// UP walks the segment bottom-up (a row band at the segment's top edge is
-// then output first; a compile-time direction: a runtime one costs the
-// unrolled body its register allocation, tests/test_kernel_resources.py);
-// sig_step >= 0: once that step's row is stored, this (output) wave
-// publishes a row-band arrival (Args::rb_rect).
-template <int K, int PB, int PE, bool EXACT, bool EDGE, bool RULE, bool SYNC, bool UP>
+// One wave = stage J of one strip: levels PB..PE of the K-level pipeline
+// (PB = J NL + 1, PE = (J + 1) NL).  Stage 0 takes level 0 from the DMA
+// ring; stage J > 0 from hand-off ring J - 1 (rows written by stage J - 1;
+// every stage runs two steps behind the previous one, D = 2J, so it can
+// request them before the step barrier).  The last stage stores level K to
+// `un`; the others write level PE to hand-off ring J.  Strip output columns
+// [xs, xe), rows [ys, ye).  UP walks the segment bottom-up (a row band at the
+// segment's top edge is then output first; a compile-time direction: a
+// runtime one costs the unrolled body its register allocation,
+// tests/test_kernel_resources.py); sig_step >= 0: once that step's row is
+// stored, this (output) wave publishes a row-band arrival (Args::rb_rect).
+template <int K, int J, bool EXACT, bool EDGE, bool RULE, bool UP>
 __device__ __forceinline__ void run_stage(const Args& a, const double* __restrict__ u, double* __restrict__ un,
-                                          char* ring, char* hand, int lane, int64_t xs, int64_t xe, int64_t ys,
-                                          int64_t ye, int nsteps, int sig_step) {
-  constexpr bool kIn = PB == 1;
-  constexpr bool kOut = PE == K;
-  constexpr int D = kIn ? 0 : 2;                  // step lag behind stage 0
-  constexpr int SPS = kOut ? (EDGE ? 4 : 2) : 0;  // global stores per step
-  constexpr int DPS = kIn ? 2 : 0;                // DMAs per step
+                                          char* ring, int lane, int64_t xs, int64_t xe, int64_t ys, int64_t ye,
+                                          int nsteps, int sig_step) {
+  using C = Cfg<K>;
+  constexpr int NC = C::NC;
+  constexpr int PB = J * C::NL + 1, PE = (J + 1) * C::NL;
+  constexpr bool kIn = J == 0;
+  constexpr bool kOut = J == C::S - 1;
+  constexpr bool SYNC = C::S > 1;
+  constexpr bool SLIDE = C::SLIDE;
+  constexpr int kP = C::P, kRS = C::RS, kHS = C::HS;
+  constexpr uint32_t kRow = C::ROW;
+  constexpr int D = 2 * J;                           // step lag behind stage 0
+  constexpr int SPS = kOut ? (EDGE ? NC : NC / 2) : 0;  // global stores per step
+  // DMAs per step.  Narrow strips: stage 0 loads the whole row.  Wide strips:
+  // stage q < NDMA loads the row's q-th 1-KB piece (an LDS-DMA costs ~60
+  // issue cycles: three on one wave made stage 0 the pole of every step
+  // barrier, profiles/r04_wide.md) and waits for it before the barrier that
+  // publishes the row to stage 0.
+  constexpr bool kDma = SLIDE ? J < C::NDMA : kIn;
+  constexpr int DPS = kDma ? (SLIDE ? 1 : C::NDMA) : 0;
+  static_assert(!SLIDE || (C::S > C::NDMA && SPS * DPS == 0), "wide strips: the output stage loads nothing");
+  // hand-off rings: read ring J - 1, write ring J
+  char* const hand_rd = ring + kRS * kRow + (J > 0 ? J - 1 : 0) * kHS * kRow;
+  char* const hand_wr = ring + kRS * kRow + J * kHS * kRow;
   // every kernel argument the loop needs, as values: the asm memory clobbers
   // below would otherwise force a reload of the kernarg segment per use
   const int64_t ld = a.ld;
@@ -157,9 +220,9 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   const double quarter = a.quarter;
   const int64_t dx0 = a.dom[0], dx1 = a.dom[0] + a.dom[1];
   const int64_t dy0 = a.dom[2], dy1 = a.dom[2] + a.dom[3];
-  const int64_t cf = xs - ring_left(K);  // first column of the strip window
-  const int64_t c0 = cf + kNC * lane;    // this lane: columns c0 .. c0+3
-  const int64_t yl = ys - K;             // the window's first row
+  const int64_t cf = xs - C::KL;        // first column of the strip window
+  const int64_t c0 = cf + NC * lane;    // this lane: columns c0 .. c0+NC-1
+  const int64_t yl = ys - K;            // the window's first row
   const int L = static_cast<int>(ye - ys);
   const uint32_t ld8 = static_cast<uint32_t>(ld) * 8u;
   // row offsets of step s in the window / in the output: base + s * step
@@ -171,40 +234,53 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   const uint32_t dbase = up ? static_cast<uint32_t>(L + 2 * K - 1) * ld8 : 0u;
   const uint32_t sbase = up ? static_cast<uint32_t>(L - 1) * ld8 : 0u;
 
-  //  loads: rows [yl, min(yl + L + 2K, last_row + 1)), 2048 contiguous bytes
-  //  from column cf (a column outside the row wraps into the neighbouring
-  //  row or is zero-filled: garbage outside every output cone)
+  //  loads: rows [yl, min(yl + L + 2K, last_row + 1)), COLS * 8 contiguous
+  //  bytes from column cf (a column outside the row wraps into the
+  //  neighbouring row or is zero-filled: garbage outside every output cone)
   const int64_t nrow_in = std::min<int64_t>(L + 2 * K, a.last_row + 1 - yl);
   const __amdgpu_buffer_rsrc_t lrs = row_rsrc(u + yl * ld, static_cast<uint32_t>(nrow_in) * ld8);
   const uint32_t loff = static_cast<uint32_t>(cf) * 8u + static_cast<uint32_t>(lane) * 16u;
   auto dma = [&](int s, int slot) {
-    if constexpr (kIn) {
-      char* dst = ring + slot * kSlotBytes;
+    if constexpr (kDma) {
+      char* dst = ring + slot * kRow;
       const uint32_t o = dbase + static_cast<uint32_t>(s) * rstep;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst, 16, loff + o, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + 1024, 16, loff + 1024u + o, 0, 0, 0);
+      if constexpr (SLIDE) {
+        constexpr uint32_t q = J;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + q * 1024u, 16, loff + q * 1024u + o, 0, 0, 0);
+      } else {
+        static_for<0, C::NDMA>([&](auto Q) {
+          constexpr uint32_t q = decltype(Q)::value;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + q * 1024u, 16, loff + q * 1024u + o, 0, 0, 0);
+        });
+      }
     }
   };
-  //  stores: rows [ys, ye) from column xs.  The left output edge is a lane
-  //  boundary (KL = 0 mod 4): 16-B stores of columns 0-1 and 2-3 where both
-  //  are inside, and (EDGE: a rect of the launch ends inside a lane at an odd
-  //  column) 8-B stores of column 0 or 2 alone.  Lanes with nothing to store
+  //  stores: rows [ys, ye) from column xs.  The left output edge is a column
+  //  pair boundary (KL even): 16-B stores of the lane's column pairs where
+  //  both are inside, and (EDGE: a rect of the launch ends at an odd column)
+  //  8-B stores of a pair's first column alone.  Lanes with nothing to store
   //  get an offset past any row (dropped).
   const __amdgpu_buffer_rsrc_t srs = row_rsrc(un + ys * ld + xs, static_cast<uint32_t>(L) * ld8);
-  const bool in0 = c0 >= xs && c0 < xe, in1 = c0 + 1 >= xs && c0 + 1 < xe;
-  const bool in2 = c0 + 2 >= xs && c0 + 2 < xe, in3 = c0 + 3 >= xs && c0 + 3 < xe;
-  const uint32_t sta = (in0 && in1) ? static_cast<uint32_t>(c0 - xs) * 8u : kDrop;
-  const uint32_t stb = (in2 && in3) ? static_cast<uint32_t>(c0 + 2 - xs) * 8u : kDrop;
-  const uint32_t stc = (in0 && !in1) ? static_cast<uint32_t>(c0 - xs) * 8u : kDrop;
-  const uint32_t std_ = (in2 && !in3) ? static_cast<uint32_t>(c0 + 2 - xs) * 8u : kDrop;
-  auto store_step = [&](int s, const d4& v) {  // level K of step s = output row s - D - 2K of the walk
+  uint32_t stp[NC / 2], sts[NC / 2];
+#pragma unroll
+  for (int q = 0; q < NC / 2; ++q) {
+    const int64_t ca = c0 + 2 * q;
+    const bool ina = ca >= xs && ca < xe, inb = ca + 1 >= xs && ca + 1 < xe;
+    stp[q] = (ina && inb) ? static_cast<uint32_t>(ca - xs) * 8u : kDrop;
+    sts[q] = (ina && !inb) ? static_cast<uint32_t>(ca - xs) * 8u : kDrop;
+  }
+  auto store_step = [&](int s, const dv<NC>& v) {  // level K of step s = output row s - D - 2K of the walk
     if constexpr (kOut) {
       const uint32_t ro = sbase + static_cast<uint32_t>(s - D - 2 * K) * rstep;  // warm-up rows: out of range
-      __builtin_amdgcn_raw_buffer_store_b128(pack2(v.x, v.y), srs, sta + ro, 0, 2 /* nt */);
-      __builtin_amdgcn_raw_buffer_store_b128(pack2(v.z, v.w), srs, stb + ro, 0, 2);
+      static_for<0, NC / 2>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        __builtin_amdgcn_raw_buffer_store_b128(pack2(v.c[2 * q], v.c[2 * q + 1]), srs, stp[q] + ro, 0, 2 /* nt */);
+      });
       if constexpr (EDGE) {
-        __builtin_amdgcn_raw_buffer_store_b64(pack1(v.x), srs, stc + ro, 0, 2);
-        __builtin_amdgcn_raw_buffer_store_b64(pack1(v.z), srs, std_ + ro, 0, 2);
+        static_for<0, NC / 2>([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          __builtin_amdgcn_raw_buffer_store_b64(pack1(v.c[2 * q]), srs, sts[q] + ro, 0, 2);
+        });
       }
     }
   };
@@ -213,85 +289,130 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   // ghost ring is fixed keeps its value at every level
   const bool gw = mask & 1, ge = mask & 2, gs = mask & 4, gn = mask & 8;
   auto kept_col = [&](int64_t c) { return (c < dx0 && !gw) || (c >= dx1 && !ge); };
-  const bool kx0 = kept_col(c0), kx1 = kept_col(c0 + 1), kx2 = kept_col(c0 + 2), kx3 = kept_col(c0 + 3);
+  bool kx[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) kx[j] = kept_col(c0 + j);
 
-  auto level = [&](const d4& up_, const d4& c, const d4& dn, int64_t row) -> d4 {
+  auto level = [&](const dv<NC>& up_, const dv<NC>& c, const dv<NC>& dn, int64_t row) -> dv<NC> {
 #pragma clang fp contract(off)
-    const double w = dpp_from_lower(c.w), e = dpp_from_upper(c.x);
-    d4 v;
-    if constexpr (EXACT) {
-      v.x = quarter * ((w + c.y) + (up_.x + dn.x));
-      v.y = quarter * ((c.x + c.z) + (up_.y + dn.y));
-      v.z = quarter * ((c.y + c.w) + (up_.z + dn.z));
-      v.w = quarter * ((c.z + e) + (up_.w + dn.w));
-    } else {
-      v.x = (w + c.y) + (up_.x + dn.x);
-      v.y = (c.x + c.z) + (up_.y + dn.y);
-      v.z = (c.y + c.w) + (up_.z + dn.z);
-      v.w = (c.z + e) + (up_.w + dn.w);
-    }
+    const double w = dpp_from_lower(c.c[NC - 1]), e = dpp_from_upper(c.c[0]);
+    dv<NC> v;
+    static_for<0, NC>([&](auto Q) {
+#pragma clang fp contract(off)
+      constexpr int j = decltype(Q)::value;
+      double l, r;
+      if constexpr (j == 0) l = w;
+      else l = c.c[j - 1];
+      if constexpr (j == NC - 1) r = e;
+      else r = c.c[j + 1];
+      if constexpr (EXACT) v.c[j] = quarter * ((l + r) + (up_.c[j] + dn.c[j]));
+      else v.c[j] = (l + r) + (up_.c[j] + dn.c[j]);
+    });
     if constexpr (RULE) {
       const bool rk = (row < dy0 && !gs) || (row >= dy1 && !gn);
       const double f = EXACT ? 1.0 : 4.0;  // a kept cell: V_p = 4 V_{p-1}
-      v.x = (rk || kx0) ? c.x * f : v.x;
-      v.y = (rk || kx1) ? c.y * f : v.y;
-      v.z = (rk || kx2) ? c.z * f : v.z;
-      v.w = (rk || kx3) ? c.w * f : v.w;
+#pragma unroll
+      for (int j = 0; j < NC; ++j) v.c[j] = (rk || kx[j]) ? c.c[j] * f : v.c[j];
     }
     return v;
   };
 
   constexpr int NL = PE - PB + 1;
   // W[p - PB][0 / 1]: level p (PB..PE-1) of the rows of steps s-2 / s-1
-  d4 W[NL > 1 ? NL - 1 : 1][2];
+  dv<NC> W[NL > 1 ? NL - 1 : 1][2];
 #pragma unroll
   for (int p = 0; p < (NL > 1 ? NL - 1 : 1); ++p)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) W[p][j] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int j = 0; j < 2; ++j) W[p][j] = dv_zero<NC>();
 
   // prologue: rows 0..P-1 in flight, each preceded by the (dropped) stores a
-  // steady-state step issues, so every wait below counts the same
-  // (SPS + DPS)(P - 1) younger memory operations
-  if constexpr (kIn) {
+  // steady-state step issues, so every wait below counts the same younger
+  // memory operations
+  if constexpr (SLIDE) {
+    // wide strips: every loading stage issues its piece of rows 0..P-1 and
+    // waits for rows 0 and 1; one extra barrier publishes them (every wave of
+    // the workgroup takes it, idle ones included)
+    if constexpr (kDma) {
+      static_for<0, kP>([&](auto I) { dma(decltype(I)::value, decltype(I)::value); });
+      wait_vmcnt<DPS * (kP - 2)>();
+    }
+    step_barrier();
+  } else if constexpr (kIn) {
     // (each dummy store gets its own out-of-range row so the compiler cannot
     // merge identical stores)
     static_for<0, kP>([&](auto I) {
-      store_step(decltype(I)::value - kP, d4{0.0, 0.0, 0.0, 0.0});
+      store_step(decltype(I)::value - kP, dv_zero<NC>());
       dma(decltype(I)::value, decltype(I)::value);
     });
   }
 
-  // level PB-1 rows of step s (rows s-D-PB-1 .. s-D-PB+1), read one step
-  // ahead so the ds_reads are in flight across the step barrier
-  d4 r0, r1, r2;
-  auto load_rows = [&](int s) {
+  // level PB-1 input rows.  Narrow strips: r0, r1, r2 = the rows of step s,
+  // read one step ahead so the ds_reads are in flight across the step
+  // barrier.  Wide strips (SLIDE): R[i % 3] holds input row i; the row step s
+  // adds is read in the middle of step s - 1.
+  //   stage 0: input row i = DMA'd window row i, step s uses rows s-2, s-1, s;
+  //   stage J > 0: input row i = the row stage J-1 wrote at its step i, step
+  //   s uses rows s-4, s-3, s-2 (published by the barriers of those steps).
+  constexpr int RD = kIn ? 0 : 2;  // step s's newest input row is s - RD
+  dv<NC> r0, r1, r2;
+  dv<NC> R[3];
+  auto load_rows = [&](int s) {  // narrow strips: the three rows of step s
     if constexpr (kIn) {
       // the DMA of row s (issued at the end of step s-P) has landed once at
       // most (SPS + DPS)(P - 1) younger memory operations are outstanding
       wait_vmcnt<(SPS + DPS) * (kP - 1)>();
-      r0 = lds_row(ring + ((s + kRS - 2) % kRS) * kSlotBytes, lane);
-      r1 = lds_row(ring + ((s + kRS - 1) % kRS) * kSlotBytes, lane);
-      r2 = lds_row(ring + (s % kRS) * kSlotBytes, lane);
+      r0 = lds_row<NC>(ring + ((s + kRS - 2) % kRS) * kRow, lane);
+      r1 = lds_row<NC>(ring + ((s + kRS - 1) % kRS) * kRow, lane);
+      r2 = lds_row<NC>(ring + (s % kRS) * kRow, lane);
     } else {
-      // stage 0's level-KA rows of steps s-4 .. s-2 (published by the
-      // barriers of those steps)
-      r0 = lds_row(hand + ((s + kHS - 4) % kHS) * kRowBytes, lane);
-      r1 = lds_row(hand + ((s + kHS - 3) % kHS) * kRowBytes, lane);
-      r2 = lds_row(hand + ((s + kHS - 2) % kHS) * kRowBytes, lane);
+      r0 = lds_row<NC>(hand_rd + ((s + kHS - 4) % kHS) * kRow, lane);
+      r1 = lds_row<NC>(hand_rd + ((s + kHS - 3) % kHS) * kRow, lane);
+      r2 = lds_row<NC>(hand_rd + ((s + kHS - 2) % kHS) * kRow, lane);
     }
   };
-  load_rows(0);
+  // wide strips: input row i (i = s0 + j, s0 a multiple of U: every slot
+  // index is a constant of the unrolled step)
+  auto load_one = [&](auto Jc) {  // the newest input row of step s0 + Jc + 1
+    constexpr int i = decltype(Jc)::value + 1 - RD;  // its index mod U (+ a multiple of U)
+    constexpr int im = ((i % 3) + 3) % 3;
+    if constexpr (kIn) {
+      // row s+1: every piece landed before the barrier that ended step s-1
+      R[im] = lds_row<NC>(ring + (((i % kRS) + kRS) % kRS) * kRow, lane);
+    } else {
+      R[im] = lds_row<NC>(hand_rd + (((i % kHS) + kHS) % kHS) * kRow, lane);
+    }
+  };
+  if constexpr (SLIDE) {
+    // rows -RD-2, -RD-1 (warm-up: never in an output cone) and -RD
+    static_for<0, 3>([&](auto Q) {
+      constexpr int i = decltype(Q)::value - 2 - RD;
+      constexpr int im = ((i % 3) + 3) % 3;
+      if constexpr (kIn) R[im] = lds_row<NC>(ring + (((i % kRS) + kRS) % kRS) * kRow, lane);
+      else R[im] = lds_row<NC>(hand_rd + (((i % kHS) + kHS) % kHS) * kRow, lane);
+    });
+  } else {
+    load_rows(0);
+  }
 
   // rows of the walk: level p of step s is row rbase(s) - dir * p
   const int64_t yanchor = up ? ye - 1 + K : yl;
-  auto step = [&](auto J, int s) {
-    (void)J;
+  auto step = [&](auto Jc, int s) {
+    constexpr int j = decltype(Jc)::value;
     const int64_t rbase = yanchor + dir * (s - D);
-    d4 v = level(r0, r1, r2, rbase - dir * PB);
+    dv<NC> v;
+    if constexpr (SLIDE) {
+      constexpr int i2 = j - RD;  // newest input row (mod U)
+      constexpr int m0 = (((i2 - 2) % 3) + 3) % 3, m1 = (((i2 - 1) % 3) + 3) % 3, m2 = ((i2 % 3) + 3) % 3;
+      v = level(R[m0], R[m1], R[m2], rbase - dir * PB);
+      __builtin_amdgcn_sched_barrier(0);
+      load_one(Jc);  // into R[m0], free now
+    } else {
+      v = level(r0, r1, r2, rbase - dir * PB);
+    }
     __builtin_amdgcn_sched_barrier(0);
     static_for<PB + 1, PE + 1>([&](auto Q) {
       constexpr int p = decltype(Q)::value;  // PB+1 .. PE, bottom-up
-      const d4 nv = level(W[p - 1 - PB][0], W[p - 1 - PB][1], v, rbase - dir * p);
+      const dv<NC> nv = level(W[p - 1 - PB][0], W[p - 1 - PB][1], v, rbase - dir * p);
       W[p - 1 - PB][0] = W[p - 1 - PB][1];  // rows of steps s-1 and s become s-2 and s-1
       W[p - 1 - PB][1] = v;
       v = nv;
@@ -299,30 +420,35 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
     });
     if constexpr (kOut) {
       if constexpr (!EXACT) {
-        v.x = __builtin_amdgcn_ldexp(v.x, -2 * K);  // exact power-of-two unscale
-        v.y = __builtin_amdgcn_ldexp(v.y, -2 * K);
-        v.z = __builtin_amdgcn_ldexp(v.z, -2 * K);
-        v.w = __builtin_amdgcn_ldexp(v.w, -2 * K);
+#pragma unroll
+        for (int q = 0; q < NC; ++q) v.c[q] = __builtin_amdgcn_ldexp(v.c[q], -2 * K);  // exact power-of-two unscale
       }
       store_step(s, v);  // issued every step (warm-up rows are out of range)
     } else {
-      d2* h = reinterpret_cast<d2*>(hand + (s % kHS) * kRowBytes) + 2 * lane;
-      h[0] = d2{v.x, v.y};
-      h[1] = d2{v.z, v.w};
+      const int slot = SLIDE ? j % kHS : s % kHS;
+      lds_put<NC>(hand_wr + slot * kRow, lane, v);
     }
-    // the ring slot of row s-2 is free (its ds_reads completed before level
-    // 1 used them): prefetch row s+P into it
-    dma(s + kP, (s + kP) % kRS);
-    // hand-off row written (visible to the workgroup after the barrier),
-    // then the next step's rows requested, then the barrier
-    if constexpr (SYNC) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    load_rows(s + 1);
-    if constexpr (SYNC) asm volatile("s_barrier" ::: "memory");
+    // the ring slot of row s-2 (narrow) / s+P-RS (wide) is free: prefetch row
+    // s+P into it
+    dma(s + kP, SLIDE ? (j + kP) % kRS : (s + kP) % kRS);
+    if constexpr (SLIDE) {
+      // this wave's piece of row s+2 (issued at step s+2-P) has landed once
+      // at most P-2 younger DMAs are outstanding: then the barrier publishes
+      // it to stage 0, which reads row s+2 in the middle of step s+1
+      if constexpr (kDma) wait_vmcnt<DPS * (kP - 2)>();
+      step_barrier();
+    } else {
+      // hand-off row written (visible to the workgroup after the barrier),
+      // then the next step's rows requested, then the barrier
+      if constexpr (SYNC) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      load_rows(s + 1);
+      if constexpr (SYNC) asm volatile("s_barrier" ::: "memory");
+    }
   };
 
-  constexpr int kU = unroll_for(NL);
+  constexpr int kU = C::U;
   for (int s0 = 0; s0 < nsteps; s0 += kU) {
-    static_for<0, kU>([&](auto J) { step(J, s0 + decltype(J)::value); });
+    static_for<0, kU>([&](auto Jc) { step(Jc, s0 + decltype(Jc)::value); });
     // A row band's output wave: once the unrolled block holding step
     // sig_step is done, the band's rows are written — visible device-wide,
     // then one arrival (the last raises *signal).  Checked at the block
@@ -344,17 +470,21 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   wait_vmcnt<0>();
 }
 
-// A workgroup = nw adjacent strips of one segment row, G waves per strip
+// A workgroup = nw adjacent strips of one segment row, S waves per strip
 // (adjacent strips share their overlap columns in the CU's L1 / the XCD's
-// L2).  G == 1: every wave is independent (no barrier).
+// L2).  S == 1: every wave is independent (no barrier).
 template <int K, bool EXACT, bool EDGE>
 __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict__ u, double* __restrict__ un,
                                          int64_t t) {
-  constexpr int G = n_stages(K);
+  using C = Cfg<K>;
+  constexpr int G = C::S;
   extern __shared__ d2 lds_dyn[];
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
-  const int sl = wave / G, stage = wave % G;
+  // wide strips, two per workgroup: the second strip's stages are rotated by
+  // half, so the two waves a SIMD hosts (waves w and w + 4) are stages j and
+  // j + 2 — a loading stage next to a light one
+  const int sl = wave / G, stage = C::SLIDE ? (wave % G + (sl & 1) * (G / 2)) % G : wave % G;
   int k = 0;
   while (k + 1 < a.n && t >= a.tstart[k + 1]) ++k;
   const int64_t lt = t - a.tstart[k];
@@ -401,64 +531,62 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
     ys = ry0 + e0 + m * lmid;
     ye = ys + lmid < ry1 - e1 ? ys + lmid : ry1 - e1;
   }
-  // L + 2K steps (stage 1 of a split strip runs two steps behind: two more)
-  constexpr int kU = unroll_for(G == 1 ? K : stage0_levels(K));
+  // L + 2K steps (the output stage of a split strip runs LAG steps behind)
+  constexpr int kU = C::U;
   // a row band's output wave publishes its arrival at the step that stores
   // the band's last row (the first sig_rows rows of its walk)
-  const int sig_step = band ? static_cast<int>((G > 1 ? 2 : 0) + 2 * K + a.sig_rows - 1) : -1;
-  static_assert(G == 1 || unroll_for(stage0_levels(K)) == unroll_for(K - stage0_levels(K)), "stages step together");
-  const int nsteps = static_cast<int>((ye - ys + 2 * K + (G > 1 ? 2 : 0) + kU - 1) / kU * kU);
+  const int sig_step = band ? static_cast<int>(C::LAG + 2 * K + a.sig_rows - 1) : -1;
+  const int nsteps = static_cast<int>((ye - ys + 2 * K + C::LAG + kU - 1) / kU * kU);
   const int64_t strip = gi * a.nw + sl;
   if (strip >= a.nstrip[k]) {  // no strip for this wave
     if constexpr (G > 1) {
-      for (int s = 0; s < nsteps; ++s) step_barrier();  // the workgroup's per-step barriers
+      // the workgroup's per-step barriers (wide strips: and the prologue's)
+      for (int s = 0; s < nsteps + (C::SLIDE ? 1 : 0); ++s) step_barrier();
     }
     return;
   }
-  constexpr int64_t wout = strip_out(K);
+  constexpr int64_t wout = C::WOUT;
   const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
   int64_t xs = rx0 + strip * wout;
   if (xs + wout > rx1) xs = rx1 - wout > rx0 ? rx1 - wout : rx0;  // last strip: shifted left to end at rx1
   const int64_t xe = xs + wout < rx1 ? xs + wout : rx1;
   // the rule path only where a computed cell can be a fixed ring cell
-  const int64_t cx0 = xs - ring_left(K), cx1 = cx0 + kCols;
+  const int64_t cx0 = xs - C::KL, cx1 = cx0 + C::COLS;
   const bool rule = (cx0 < a.dom[0] && !(a.mask & 1)) || (cx1 > a.dom[0] + a.dom[1] && !(a.mask & 2)) ||
                     (ys - K < a.dom[2] && !(a.mask & 4)) || (ye + K > a.dom[2] + a.dom[3] && !(a.mask & 8));
-  char* ring = reinterpret_cast<char*>(lds_dyn) + sl * strip_lds(G);
-  char* hand = ring + kRS * kSlotBytes;
+  char* ring = reinterpret_cast<char*>(lds_dyn) + sl * strip_lds<K>();
   // one instantiation per (stage, rule path, direction); the direction is
   // bottom-up only for the N row bands
-  auto go = [&](auto pb, auto pe, auto sync, auto rule_c, auto up_c, int sstep) {
-    run_stage<K, decltype(pb)::value, decltype(pe)::value, EXACT, EDGE, decltype(rule_c)::value,
-              decltype(sync)::value, decltype(up_c)::value>(a, u, un, ring, hand, lane, xs, xe, ys, ye, nsteps,
-                                                            sstep);
+  auto go = [&](auto jc, auto rule_c, auto up_c, int sstep) {
+    run_stage<K, decltype(jc)::value, EXACT, EDGE, decltype(rule_c)::value, decltype(up_c)::value>(
+        a, u, un, ring, lane, xs, xe, ys, ye, nsteps, sstep);
   };
   using T = std::true_type;
   using F = std::false_type;
-  auto stage_go = [&](auto pb, auto pe, auto sync, int sstep) {
+  auto stage_go = [&](auto jc, int sstep) {
     if (dir < 0) {
-      if (rule) go(pb, pe, sync, T{}, T{}, sstep);
-      else go(pb, pe, sync, F{}, T{}, sstep);
+      if (rule) go(jc, T{}, T{}, sstep);
+      else go(jc, F{}, T{}, sstep);
     } else {
-      if (rule) go(pb, pe, sync, T{}, F{}, sstep);
-      else go(pb, pe, sync, F{}, F{}, sstep);
+      if (rule) go(jc, T{}, F{}, sstep);
+      else go(jc, F{}, F{}, sstep);
     }
   };
-  using C1 = std::integral_constant<int, 1>;
-  using CK = std::integral_constant<int, K>;
   if constexpr (G == 1) {
-    stage_go(C1{}, CK{}, F{}, sig_step);
+    stage_go(std::integral_constant<int, 0>{}, sig_step);
   } else {
-    constexpr int KA = stage0_levels(K);
-    if (stage == 0) {
-      // a launch of one round has no later workgroups to fill the SIMDs
-      // while a strip's stage 1 waits on its stage 0: favour the producer
-      // (profiles/r02_tb.md 9.4)
-      if (a.prio) __builtin_amdgcn_s_setprio(2);
-      stage_go(C1{}, std::integral_constant<int, KA>{}, T{}, -1);
-    } else {
-      stage_go(std::integral_constant<int, KA + 1>{}, CK{}, T{}, sig_step);
-    }
+    static_for<0, G>([&](auto Jc) {
+      constexpr int j = decltype(Jc)::value;
+      if (stage == j) {
+        if constexpr (j == 0) {
+          // a launch of one round has no later workgroups to fill the SIMDs
+          // while a strip's later stages wait on its stage 0: favour the
+          // producer (profiles/r02_tb.md 9.4)
+          if (a.prio) __builtin_amdgcn_s_setprio(2);
+        }
+        stage_go(Jc, j == G - 1 ? sig_step : -1);
+      }
+    });
   }
 }
 
@@ -487,7 +615,6 @@ void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__
 
 }  // namespace tb
 }  // namespace gmt
-
 namespace {
 
 using namespace gmt;
@@ -549,8 +676,8 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
       // (~2x the VALU per step): half-length segments, so they finish with
       // the others instead of ending the launch
       const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
-      const bool xrule = seg_rows == 0 && ((rx0 - ring_left(K) < a.dom[0] && !(a.mask & 1)) ||
-                                           (rx1 + ring_left(K) > a.dom[0] + a.dom[1] && !(a.mask & 2)));
+      const bool xrule = seg_rows == 0 && ((rx0 - Cfg<K>::KL < a.dom[0] && !(a.mask & 1)) ||
+                                           (rx1 + Cfg<K>::KL > a.dom[0] + a.dom[1] && !(a.mask & 2)));
       int64_t lb = xrule ? std::max<int64_t>(64, p.lmid[k] / 2) : p.lmid[k];
       if (k == rb_rect && rb > 0) lb = std::min<int64_t>(lb, std::max<int64_t>(rb_min, mid / rb));
       p.nmid_b[k] = (mid + lb - 1) / lb;
@@ -571,8 +698,8 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
     fill(L, &wgs);
     const double rounds = static_cast<double>((wgs + resident_wgs - 1) / resident_wgs);
     // a segment runs L + 2K (+2 with two stages) steps, rounded up to the unroll
-    constexpr int64_t u = unroll_for(n_stages(K) == 1 ? K : stage0_levels(K));
-    const double cost = rounds * static_cast<double>((L + 2 * K + 2 * (n_stages(K) > 1) + u - 1) / u * u);
+    constexpr int64_t u = Cfg<K>::U;
+    const double cost = rounds * static_cast<double>((L + 2 * K + Cfg<K>::LAG + u - 1) / u * u);
     if (cost < best) {
       best = cost;
       best_l = L;
@@ -588,16 +715,17 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
 template <int K, bool EXACT, bool EDGE>
 int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int64_t* dom, int mask, const double* u,
               double* un, int64_t ld, int64_t nrows, hipStream_t s, int64_t* info = nullptr) {
-  constexpr int G = n_stages(K);
-  constexpr int kMaxStrips = kMaxThreads / kWave / G;
+  using C = Cfg<K>;
+  constexpr int G = C::S;
+  constexpr int kMaxStrips = tb_max_strips(K);
   Args a{};
-  a.nw = std::min(o.wg_waves > 0 ? o.wg_waves : (G == 1 ? 4 : 1), kMaxStrips);  // two-stage: one strip (profiles/r02_tb4/launch_shapes.txt)
+  a.nw = std::min(o.wg_waves > 0 ? o.wg_waves : tb_default_strips(K), kMaxStrips);  // multi-stage: one strip (profiles/r02_tb4/launch_shapes.txt)
   a.ld = ld;
   a.last_row = nrows - 1;
   a.mask = mask;
   a.quarter = 0.25;
   for (int j = 0; j < 4; ++j) a.dom[j] = dom[j];
-  constexpr int64_t wout = strip_out(K);
+  constexpr int64_t wout = C::WOUT;
   int64_t maxh = 0;
   for (int k = 0; k < n_rect; ++k) {
     const int64_t* r = rects + 4 * k;
@@ -614,10 +742,10 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   if (a.nw > maxs) a.nw = static_cast<int>(maxs);
   // the kernel addresses a segment's rows through 32-bit buffer offsets:
   // (L + 3K + 2 unroll + prefetch) rows of ld doubles must stay below 2^31
-  const int64_t lmax = std::min<int64_t>(1 << 20, (int64_t(1) << 31) / (ld * 8) - 3 * K - 2 * unroll_for(K) - kP);
+  const int64_t lmax = std::min<int64_t>(1 << 20, (int64_t(1) << 31) / (ld * 8) - 3 * K - C::LAG - 2 * C::U - C::P);
   if (lmax < 1) return static_cast<int>(hipErrorInvalidValue);
   (void)maxh;
-  const size_t smem = static_cast<size_t>(a.nw * strip_lds(G));
+  const size_t smem = static_cast<size_t>(a.nw * strip_lds<K>());
   if (smem > 65536) {  // above the default dynamic-LDS limit (gfx950 has 160 KB per CU)
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem));
@@ -715,7 +843,7 @@ int dispatch_k(const gmt_tb_opts& o, bool exact, int n_rect, const int64_t* rect
   // boundary: their last strip is shifted to end at the rect's edge)
   bool edge = false;
   for (int k = 0; k < n_rect; ++k)
-    if (rects[4 * k + 1] > 0 && rects[4 * k + 3] > 0 && rects[4 * k + 1] < strip_out(K) && rects[4 * k + 1] % 2 == 1)
+    if (rects[4 * k + 1] > 0 && rects[4 * k + 3] > 0 && rects[4 * k + 1] < tb_strip_out(K) && rects[4 * k + 1] % 2 == 1)
       edge = true;
   if (edge)
     return exact ? launch_tb<K, true, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)

@@ -8,7 +8,13 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <mutex>
+#include <thread>
 
 #include "gmt/ccl.h"
 
@@ -23,6 +29,7 @@ int gmt_ccl_available(void) { return 1; }
 int gmt_ccl_emulated(void) { return 0; }
 const char* gmt_ccl_error_string(int err) {
   if (err == GMT_CCL_UNAVAILABLE) return "RCCL not available in this build";
+  if (err == GMT_CCL_TIMEOUT) return "communicator init timed out (a rank never joined; GMT_CCL_INIT_TIMEOUT)";
   return ncclGetErrorString(static_cast<ncclResult_t>(err));
 }
 int gmt_ccl_version(int* v) { return static_cast<int>(ncclGetVersion(v)); }
@@ -36,13 +43,43 @@ int gmt_ccl_get_unique_id(gmt_ccl_id* id) {
   return static_cast<int>(r);
 }
 
+// ncclCommInitRank blocks until every rank has joined.  It runs on a helper
+// thread (bound to the caller's device) and the caller waits for it against
+// a deadline, GMT_CCL_INIT_TIMEOUT seconds (default 300): a rank that never
+// joins makes every other rank return GMT_CCL_TIMEOUT instead of hanging the
+// job (the caller names itself and aborts; the stuck init thread is left
+// behind, the process is about to exit).  A non-blocking communicator would
+// give the same deadline but makes every later call asynchronous, including
+// the grouped exchanges captured into hipGraphs.
 int gmt_ccl_comm_init(gmt_ccl_comm_t* comm, int nranks, const gmt_ccl_id* id, int rank) {
+  *comm = nullptr;
   ncclUniqueId u;
   std::memcpy(&u, id->internal, sizeof(u));
-  ncclComm_t c = nullptr;
-  ncclResult_t r = ncclCommInitRank(&c, nranks, u, rank);
-  *comm = reinterpret_cast<gmt_ccl_comm_t>(c);
-  return static_cast<int>(r);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  const char* e = std::getenv("GMT_CCL_INIT_TIMEOUT");
+  const double limit = e && std::atof(e) > 0.0 ? std::atof(e) : 300.0;
+  struct State {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false;
+    ncclComm_t c = nullptr;
+    ncclResult_t r = ncclSuccess;
+  };
+  auto st = std::make_shared<State>();
+  std::thread([st, u, nranks, rank, dev] {
+    ncclComm_t c = nullptr;
+    ncclResult_t r = hipSetDevice(dev) == hipSuccess ? ncclCommInitRank(&c, nranks, u, rank) : ncclUnhandledCudaError;
+    std::lock_guard<std::mutex> g(st->m);
+    st->c = c;
+    st->r = r;
+    st->done = true;
+    st->cv.notify_all();
+  }).detach();
+  std::unique_lock<std::mutex> lk(st->m);
+  if (!st->cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return st->done; })) return GMT_CCL_TIMEOUT;
+  *comm = reinterpret_cast<gmt_ccl_comm_t>(st->c);
+  return static_cast<int>(st->r);
 }
 int gmt_ccl_comm_destroy(gmt_ccl_comm_t comm) {
   return comm ? static_cast<int>(ncclCommDestroy(C(comm))) : 0;

@@ -107,6 +107,10 @@ def load(device: str = "cuda") -> ctypes.CDLL:
     lib.gmt_engine_backend.restype = ctypes.c_char_p
     lib.gmt_engine_deriv_bench.argtypes = [i64, i64, c_int, c_int, c_int, c_int, c_int, vp, vp]
     lib.gmt_engine_deriv_bench.restype = c_int
+    lib.gmt_engine_watchdog_kick.argtypes = [ctypes.c_char_p]
+    lib.gmt_engine_watchdog_kick.restype = None
+    lib.gmt_engine_watchdog_timeout.argtypes = []
+    lib.gmt_engine_watchdog_timeout.restype = ctypes.c_double
     # from libgmt (a dependency of the engine library: found through its handle)
     lib.gmt_jacobi5tb_group_cols.argtypes = [c_int, c_int]
     lib.gmt_jacobi5tb_group_cols.restype = i64
@@ -116,6 +120,19 @@ def load(device: str = "cuda") -> ctypes.CDLL:
                           "(another libgmt.so is already loaded in this process)")
     _libs[kind] = lib
     return lib
+
+
+def watchdog_kick(phase: str, device: str = "cpu") -> None:
+    """Marks progress for the engine's hang watchdog (GMT_TIMEOUT seconds of
+    no progress end the process with status 124 and a line naming the rank
+    and the last phase; gmt/watchdog.hpp).  A no-op until an engine entry
+    point has armed it."""
+    load(device).gmt_engine_watchdog_kick(phase.encode()[:95])
+
+
+def watchdog_timeout(device: str = "cpu") -> float:
+    """The armed watchdog's timeout in seconds (0: not armed)."""
+    return float(load(device).gmt_engine_watchdog_timeout())
 
 
 def group_cols(sweeps: int, wg_waves: int = 0, device: str = "cpu") -> int:
@@ -162,13 +179,26 @@ def _broadcast_id(lib, env, kind: int) -> bytes:
 
 def resolve_transport(env, transport: str = "auto") -> str:
     """auto -> rccl with one rank per GPU, ipc when ranks share a GPU; local
-    for one rank.  GMT_TRANSPORT overrides auto (rccl|ipc)."""
+    for one rank.  GMT_ENGINE_TRANSPORT (rccl|ipc) overrides auto; so does
+    GMT_TRANSPORT, the native apps' variable, when it names a transport the
+    engine has (its other values — mpi-host, mpi-direct — are the apps' own
+    and are ignored here with a warning)."""
     if transport not in ("auto", "local", "rccl", "ipc"):
         raise ValueError(f"transport must be auto, local, rccl or ipc, got {transport!r}")
     if transport == "auto":
-        transport = os.environ.get("GMT_TRANSPORT", "auto").strip().lower() or "auto"
-        if transport not in ("auto", "rccl", "ipc"):
-            raise ValueError(f"GMT_TRANSPORT must be rccl or ipc, got {transport!r}")
+        eng = os.environ.get("GMT_ENGINE_TRANSPORT", "").strip().lower()
+        if eng:
+            if eng not in ("auto", "rccl", "ipc"):
+                raise ValueError(f"GMT_ENGINE_TRANSPORT must be auto, rccl or ipc, got {eng!r}")
+            transport = eng
+        else:
+            app = os.environ.get("GMT_TRANSPORT", "").strip().lower()
+            if app in ("rccl", "ipc"):
+                transport = app
+            elif app not in ("", "auto"):
+                import warnings
+                warnings.warn(f"GMT_TRANSPORT={app!r} is a native-app transport the engine does not have; "
+                              "the engine picks its own (set GMT_ENGINE_TRANSPORT to choose)", stacklevel=2)
     if transport == "auto":
         if env.world_size == 1:
             return "local"

@@ -1,4 +1,2 @@
-"""Cross-cutting helpers: roctx tracing (trace), timers/statistics (timer), JSON reports (report)."""
-from .report import json_line, write_jsonl  # noqa: F401
-from .timer import Stats, Timer  # noqa: F401
+"""Cross-cutting helpers: roctx tracing (trace)."""
 from .trace import profiler_start, profiler_stop, range_ctx  # noqa: F401

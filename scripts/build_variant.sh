@@ -4,9 +4,8 @@
 # libgmt.so into build/var/NAME/ (run a binary against it with
 # LD_LIBRARY_PATH=build/var/NAME: the apps' RUNPATH yields to it).
 #   scripts/build_variant.sh p4 's/constexpr int kP = 6;/constexpr int kP = 4;/'
-#   scripts/build_variant.sh head git:HEAD     (jacobi5tb.hpp as committed at HEAD)
-#   scripts/build_variant.sh b2 file:build/var_src/jacobi5tb_b2.hpp   (a whole edited copy)
-#   scripts/build_variant.sh pair file:csrc/bench/jacobi5tb_pair.hpp   (the paired-strip candidate)
+#   scripts/build_variant.sh head git:HEAD     (jacobi5tb.hpp + .hip as committed at HEAD)
+#   (the rejected round-3 candidates live in git history: git show a32db55:csrc/bench/jacobi5tb_pair.hpp)
 #   scripts/build_variant.sh x cur             (the working tree's kernel sources as they are)
 set -e
 cd "$(dirname "$0")/.."
@@ -15,7 +14,8 @@ D=build/var/$name
 rm -rf $D && mkdir -p $D/src $D/obj
 cp csrc/kernels/*.hpp csrc/kernels/jacobi5tb*.hip $D/src/
 case "$expr" in
-  git:*) git show "${expr#git:}:csrc/kernels/jacobi5tb.hpp" > $D/src/jacobi5tb.hpp ;;
+  git:*) git show "${expr#git:}:csrc/kernels/jacobi5tb.hpp" > $D/src/jacobi5tb.hpp
+         git show "${expr#git:}:csrc/kernels/jacobi5tb.hip" > $D/src/jacobi5tb.hip ;;
   file:*) cp "${expr#file:}" $D/src/jacobi5tb.hpp ;;
   cur) ;;
   *) sed -i "$expr" $D/src/jacobi5tb.hpp ;;

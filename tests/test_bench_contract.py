@@ -145,3 +145,43 @@ def test_bench_ipc_peer_hang_fails_the_job_cpu():
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")], p.stdout
     assert "GMT FAULT INJECTION: rank 1" in p.stderr, p.stderr[-4000:]
     assert "timed out waiting for the peer" in p.stdout + p.stderr, (p.stdout + p.stderr)[-4000:]
+
+
+def test_bench_rccl_peer_hang_watchdog_cpu():
+    """A rank that hangs inside the RCCL data plane (emulated on the CPU
+    backend): rank 1 stops forever at its 3rd halo exchange, rank 0 blocks in
+    the grouped send/recv.  The engine's watchdog (armed by bench.py's default
+    GMT_TIMEOUT, here 4 s) ends the job with status 124 and a line naming the
+    rank and its last phase, well before any launcher timeout."""
+    port = str(free_port())
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
+               GMT_TRANSPORT="rccl", GMT_INJECT_HANG="1:2", GMT_TIMEOUT="4")
+    p = subprocess.run(["timeout", "-k", "5", "150", sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port", port, "bench.py",
+                        "--gpus", "2", "--device", "cpu", "--size", "128", "--steps", "6", "--warmup", "1",
+                        "--skip-extras"], capture_output=True, text=True, timeout=180, cwd=ROOT, env=env)
+    assert p.returncode not in (0, 124) or "GMT WATCHDOG" in p.stderr, p.stdout + p.stderr
+    assert p.returncode != 0, p.stdout + p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")], p.stdout
+    assert "GMT FAULT INJECTION: rank 1" in p.stderr, p.stderr[-4000:]
+    assert "GMT WATCHDOG: rank 1" in p.stderr and "last phase" in p.stderr, p.stderr[-4000:]
+
+
+def test_rccl_init_timeout_names_the_rank_cpu():
+    """A communicator whose peers never join: rank 0 of 2 creates the engine's
+    RCCL transport alone.  gmt_ccl_comm_init gives up after
+    GMT_CCL_INIT_TIMEOUT seconds and the engine exits 124 naming the rank and
+    the phase, instead of blocking the job forever."""
+    code = ("import ctypes, sys; sys.path.insert(0, '.');"
+            "from gpu_mpi_tests_amd import engine as e;"
+            "lib = e.load('cpu'); buf = ctypes.create_string_buffer(128);"
+            "assert lib.gmt_engine_unique_id(buf) == 0;"
+            "lib.gmt_engine_comm_create.restype = ctypes.c_void_p;"
+            "lib.gmt_engine_comm_create(0, 2, e.RCCL, buf); print('returned')")
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", GMT_CCL_INIT_TIMEOUT="2")
+    env.pop("GMT_TIMEOUT", None)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60, cwd=ROOT, env=env)
+    assert p.returncode == 124, p.stdout + p.stderr
+    assert "returned" not in p.stdout
+    assert "rank 0 of 2" in p.stderr and "RCCL communicator init failed" in p.stderr, p.stderr
+    assert "never" in p.stderr, p.stderr
