@@ -220,12 +220,14 @@ def ref_halo(env, n_local, n_other, iters):
     median, max over ranks."""
     from gpu_mpi_tests_amd.engine import deriv_bench
 
-    r = deriv_bench(n_local, n_other, n_iter=iters, n_warmup=5, env=env)
+    r = deriv_bench(n_local, n_other, n_iter=iters, n_warmup=5, env=env, check=True)
     out = {"ref_halo_config": f"mpi_stencil2d_gt {n_local}x{n_other} per rank, 1-D slabs, "
                               f"{iters} exchanges, {r['transport']}"}
     for d in (0, 1):
         out[f"ref_halo_dim{d}_us"] = round(gdist.allreduce_max(r[f"dim{d}"]["median_s"], env) * 1e6, 2)
         out[f"ref_halo_dim{d}_err_norm"] = gdist.allreduce_max(r[f"dim{d}"]["err_norm"], env)
+        # every exchange's ghost rows vs the analytic field (gmt/deriv.hpp check)
+        out[f"ref_halo_dim{d}_bad_ghosts"] = int(gdist.allreduce_max(float(r[f"dim{d}"]["bad_ghosts"]), env))
         # scale-free: round-off of x^3 + y^2 at the reference's spacing grows
         # with the extent; a missing or wrong ghost cell gives O(1) and more
         out[f"ref_halo_dim{d}_rel_err"] = gdist.allreduce_max(
@@ -441,6 +443,13 @@ def main(argv=None):
         if env.world_size > 1:
             mark(env, "reference halo benchmark")
             extras.update(ref_halo(env, args.ref_n_local, args.ref_n_other, args.ref_iters))
+            if extras["ref_halo_dim0_bad_ghosts"] or extras["ref_halo_dim1_bad_ghosts"]:
+                if env.rank == 0:
+                    print("bench.py: the reference halo benchmark found wrong ghost cells after an exchange "
+                          f"(dim 0: {extras['ref_halo_dim0_bad_ghosts']}, dim 1: {extras['ref_halo_dim1_bad_ghosts']})",
+                          file=sys.stderr)
+                gdist.shutdown()
+                sys.exit(6)
         mark(env, "daxpy")
         gbps, ddt = bench_daxpy(env, args.daxpy_n, iters=20)
         extras["daxpy_GBps"] = round(gbps, 1)

@@ -104,6 +104,12 @@ inline comm::Kind pick_transport(const DerivConfig& c, const RankBinding& b) {
   return comm::resolve(comm::Kind::Auto, b, c.space == GMT_SPACE_MANAGED);
 }
 
+// --check failed on some rank in some test (the app then exits with status 5)
+inline bool& halo_check_failed() {
+  static bool f = false;
+  return f;
+}
+
 inline DerivResult run_deriv(const DerivConfig& c, const RankBinding& b, MPI_Comm comm,
                              TransportPool& pool) {
   comm::Transport& tr = pool.get(pick_transport(c, b));
@@ -111,7 +117,19 @@ inline DerivResult run_deriv(const DerivConfig& c, const RankBinding& b, MPI_Com
   DumpFn dump = [&](const char* what, const double* f, size_t nr, size_t nc, size_t r0, size_t n) {
     dump_rows(comm, rank, ws, what, f, nr, nc, r0, n);
   };
-  return run_deriv_on(c, tr, rank, ws, dump);
+  DerivResult r = run_deriv_on(c, tr, rank, ws, dump);
+  if (c.check) {  // per-exchange ghost check: one line per test on rank 0
+    long long bad = r.bad_ghosts < 0 ? 0 : r.bad_ghosts, tot = 0;
+    int n = r.checked_exchanges, nmin = 0;
+    MPI_Allreduce(&bad, &tot, 1, MPI_LONG_LONG, MPI_SUM, comm);
+    MPI_Allreduce(&n, &nmin, 1, MPI_INT, MPI_MIN, comm);
+    if (rank == 0)
+      std::printf("# halo check dim:%d buf:%d (%s): %lld bad ghost cells, %d exchanges checked per rank\n", c.dim,
+                  c.buf ? 1 : 0, r.transport.c_str(), tot, nmin);
+    if (tot != 0) halo_check_failed() = true;
+    r.bad_ghosts = tot;
+  }
+  return r;
 }
 
 inline SumResult run_sum(int dim, int space, size_t n_local, size_t n_other, int n_iter,

@@ -27,6 +27,8 @@
 //   --dim=0|1 --mem=device|managed --buf=0|1   run one slice of the test matrix
 //   --iters=N --warmup=W  (positional n_iter still wins when given; warmup default 5)
 //   --timeout=S           hang watchdog (gmt/watchdog.hpp)
+//   --check               compare the ghost rows with the analytic field after EVERY
+//                         exchange (GMT_CORRUPT_GHOST=R:K injects a bad cell); exit 5 on a mismatch
 #include <mpi.h>
 
 #include <cstdio>
@@ -132,6 +134,7 @@ int main(int argc, char** argv) {
           c.transport = want;
           c.host_init = cli.flag("host-init");
           c.host_verify = cli.flag("host-verify");
+          c.check = cli.flag("check");
           c.realloc_per_call = alloc_per_call;
           DerivResult r = run_deriv(c, b, MPI_COMM_WORLD, pool);
           report("deriv", dim, c.space, buf, r);
@@ -167,5 +170,5 @@ int main(int argc, char** argv) {
   }
   pool_owner.reset();
   MPI_Finalize();
-  return EXIT_SUCCESS;
+  return halo_check_failed() ? 5 : EXIT_SUCCESS;
 }

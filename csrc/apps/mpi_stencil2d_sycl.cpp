@@ -17,6 +17,9 @@
 // halo copy kernel (gmt_copy2d_batched): print the field and a second
 // buffer, pack ghost-side rows [0, n_bnd) into a buffer, unpack the second
 // buffer into rows [N-n_bnd, N), print again.  No MPI.
+//
+// --check: ghost rows compared with the analytic field after every exchange
+// (gmt/deriv.hpp DerivConfig::check); exit status 5 on a mismatch.
 #include <mpi.h>
 
 #include <cstdio>
@@ -147,6 +150,7 @@ int main(int argc, char** argv) {
     c.transport = comm::parse_kind(cli.get("transport", "auto"));
     c.host_init = cli.flag("host-init");
     c.host_verify = cli.flag("host-verify");
+    c.check = cli.flag("check");
     DerivResult r = run_deriv(c, b, MPI_COMM_WORLD, pool);
     std::printf("%d/%d exchange time %0.8f ms\n", world_rank, world_size,
                 r.total_time / n_iter * 1000);
@@ -164,5 +168,5 @@ int main(int argc, char** argv) {
     }
   }
   MPI_Finalize();
-  return EXIT_SUCCESS;
+  return halo_check_failed() ? 5 : EXIT_SUCCESS;
 }

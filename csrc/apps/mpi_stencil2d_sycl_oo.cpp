@@ -7,6 +7,8 @@
 // "%d: exchange time %0.8f ms" and "%d: [0x%08x] err_norm = %.8f".
 // --debug mirrors the reference's DEBUG build: domain / 1024, one iteration,
 // no warmup, and a rank-serialised dump of the halo rows.
+// --check: ghost rows compared with the analytic field after every exchange
+// (gmt/deriv.hpp DerivConfig::check); exit status 5 on a mismatch.
 #include <mpi.h>
 
 #include <cstdio>
@@ -66,6 +68,7 @@ int main(int argc, char** argv) {
     c.transport = comm::parse_kind(cli.get("transport", "auto"));
     c.host_init = cli.flag("host-init");
     c.host_verify = cli.flag("host-verify");
+    c.check = cli.flag("check");
     c.debug_dump = debug;
     DerivResult r = run_deriv(c, b, MPI_COMM_WORLD, pool);
     std::printf("%d: exchange time %0.8f ms\n", world_rank, r.total_time / (n_iter > 0 ? n_iter : 1) * 1000);
@@ -81,5 +84,5 @@ int main(int argc, char** argv) {
     }
   }
   MPI_Finalize();
-  return EXIT_SUCCESS;
+  return halo_check_failed() ? 5 : EXIT_SUCCESS;
 }

@@ -136,6 +136,29 @@ static double lattice_uniform(int64_t gx, int64_t gy, uint64_t seed) {
   return static_cast<double>(k >> 11) * 0x1.0p-53;
 }
 
+int gmt_poly_check(int64_t nx, int64_t ny, double x0, double dx, double y0, double dy, double offset,
+                   double rtol, const double* z, int64_t ld, unsigned* bad, void*) {
+  if (nx <= 0 || ny <= 0) return 0;
+  if (!bad || !z || ld < nx) return 1;
+  unsigned n = 0;
+  for (int64_t iy = 0; iy < ny; ++iy)
+    for (int64_t ix = 0; ix < nx; ++ix) {
+      const double x = x0 + ix * dx, y = y0 + iy * dy;
+      const double e = (x * x * x + y * y) + offset, v = z[iy * ld + ix];
+      if (!(std::fabs(v - e) <= rtol * (1.0 + std::fabs(e)))) ++n;
+    }
+  __atomic_fetch_add(bad, n, __ATOMIC_RELAXED);
+  return 0;
+}
+
+int gmt_add_scalar(int64_t nx, int64_t ny, double v, double* z, int64_t ld, void*) {
+  if (nx <= 0 || ny <= 0) return 0;
+  if (!z || ld < nx) return 1;
+  for (int64_t iy = 0; iy < ny; ++iy)
+    for (int64_t ix = 0; ix < nx; ++ix) z[iy * ld + ix] += v;
+  return 0;
+}
+
 int gmt_fill_poly(int mode, int64_t nx, int64_t ny, double x0, double dx, double y0, double dy,
                   double* z, int64_t ld, void*) {
   for (int64_t j = 0; j < ny; ++j)

@@ -16,6 +16,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <memory>
 #include <string>
@@ -48,6 +50,13 @@ struct DerivConfig {
   bool host_init = false, host_verify = false;
   bool realloc_per_call = false;  // emulate the gt version's per-call buffers
   bool debug_dump = false;        // rank-serialised halo-row dumps (sycl_oo DEBUG build)
+  // --check: after EVERY exchange, one small kernel compares the ghost rows
+  // the exchange filled with the analytic field; before every exchange the
+  // whole local field is raised by 1.0 (outside the timed region), so a
+  // ghost row left from an earlier exchange (a reused staging slot, a lost
+  // chunk) differs by >= 1 and is counted.  The reference checks only the
+  // last iteration's derivative (mpi_stencil2d_gt.cc:541-570).
+  bool check = false;
 };
 
 struct DerivResult {
@@ -60,7 +69,18 @@ struct DerivResult {
   Stats iters;              // per-exchange seconds
   std::string transport;
   size_t bytes_per_exchange = 0;
+  long long bad_ghosts = -1;  // --check: ghost cells that were wrong after some exchange (-1: not checked)
+  int checked_exchanges = 0;
 };
+
+// GMT_CORRUPT_GHOST=R:K (fault injection for --check): rank R overwrites one
+// ghost cell after its K-th exchange (counting warm-ups from 0)
+inline bool corrupt_ghost_now(int rank, int it) {
+  const char* e = std::getenv("GMT_CORRUPT_GHOST");
+  if (!e) return false;
+  const char* c = std::strchr(e, ':');
+  return std::atoi(e) == rank && c && std::atoi(c + 1) == it;
+}
 
 // `dump(what, row0)` (optional) prints n_bnd rows of the field from every
 // rank (the apps gather them over MPI).
@@ -148,11 +168,43 @@ inline DerivResult run_deriv_on(const DerivConfig& c, comm::Transport& tr, int r
   DerivResult r;
   r.transport = tr.name();
   r.bytes_per_exchange = halo->bytes_sent();
+  // --check: the ghost blocks the exchange fills, in the fill's coordinates
+  struct Ghost {
+    double* p;
+    int64_t nx, ny;
+    double x0, y0;
+  };
+  std::vector<Ghost> ghosts;
+  Buffer<unsigned> bad;
+  if (c.check) {
+    bad = Buffer<unsigned>(1, GMT_SPACE_DEVICE);
+    GMT_CHECK("bad = 0", gmt_rt_memset_async(bad.data(), 0, sizeof(unsigned), s));
+    const double lo_c = start - n_bnd * delta, hi_c = start + c.n_local * delta;
+    if (d0) {
+      if (lo >= 0) ghosts.push_back({&zf(0, 0), static_cast<int64_t>(n_bnd), static_cast<int64_t>(c.n_other), lo_c, 0.0});
+      if (hi >= 0)
+        ghosts.push_back({&zf(n_bnd + c.n_local, 0), static_cast<int64_t>(n_bnd), static_cast<int64_t>(c.n_other), hi_c, 0.0});
+    } else {
+      if (lo >= 0) ghosts.push_back({&zf(0, 0), static_cast<int64_t>(c.n_other), static_cast<int64_t>(n_bnd), 0.0, lo_c});
+      if (hi >= 0)
+        ghosts.push_back({&zf(0, n_bnd + c.n_local), static_cast<int64_t>(c.n_other), static_cast<int64_t>(n_bnd), 0.0, hi_c});
+    }
+  }
   for (int it = 0; it < c.n_warmup + c.n_iter; ++it) {
+    if (c.check) GMT_CHECK("raise", gmt_add_scalar(nrows, ncols, 1.0, z.data(), nrows, s));
+    if (c.check) GMT_CHECK("raise sync", gmt_rt_stream_synchronize(s));
     const double t0 = wtime();
     if (c.realloc_per_call) halo = std::make_unique<Halo2D>(tr, zf, gx, gy, nb, pack_y, buf_space);
     halo->exchange(s);
     const double t1 = wtime();
+    if (c.check) {
+      if (corrupt_ghost_now(rank, it) && !ghosts.empty())
+        GMT_CHECK("corrupt", gmt_add_scalar(1, 1, 0.5, ghosts[0].p, nrows, s));
+      for (const Ghost& g : ghosts)
+        GMT_CHECK("ghost check", gmt_poly_check(g.nx, g.ny, g.x0, delta, g.y0, delta, static_cast<double>(it + 1),
+                                                1e-9, g.p, nrows, bad.data(), s));
+      ++r.checked_exchanges;
+    }
     if (it >= c.n_warmup) {
       r.total_time += t1 - t0;
       r.iters.add(t1 - t0);
@@ -202,6 +254,12 @@ inline DerivResult run_deriv_on(const DerivConfig& c, comm::Transport& tr, int r
     GMT_CHECK("err D2H", gmt_rt_memcpy_async(&acc, ws_buf.data(), sizeof(double), s));
     GMT_CHECK("err sync", gmt_rt_stream_synchronize(s));
     r.err_norm = std::sqrt(acc);
+  }
+  if (c.check) {
+    unsigned h = 0;
+    GMT_CHECK("bad D2H", gmt_rt_memcpy_async(&h, bad.data(), sizeof(h), s));
+    GMT_CHECK("bad sync", gmt_rt_stream_synchronize(s));
+    r.bad_ghosts = h;
   }
   halo.reset();
   gmt_rt_stream_destroy(s);

@@ -87,12 +87,15 @@ double gmt_engine_watchdog_timeout(void); /* 0 when not armed */
 /* The reference's halo-exchange benchmark (mpi_stencil2d_gt test_deriv for
  * dim 0 and dim 1, then test_sum), n_local x n_other per rank, 2 ghosts,
  * non-periodic 1-D slabs, on the RCCL or IPC transport (local for world == 1).
- * out[16]: per dim d (6 values at 6*d): exchange seconds median, mean, min,
+ * out[18]: per dim d (6 values at 6*d): exchange seconds median, mean, min,
  * max, bytes sent per exchange, this rank's err_norm; out[12] = all-reduce
  * (1024 doubles in place) median seconds, out[13] = its max relative error;
- * out[14 + d] = norm of the analytic derivative over this rank's output. */
+ * out[14 + d] = norm of the analytic derivative over this rank's output;
+ * out[16 + d] = ghost cells found wrong after some exchange (check != 0: the
+ * ghost rows are compared with the analytic field after EVERY exchange,
+ * gmt/deriv.hpp; -1 without check). */
 int gmt_engine_deriv_bench(int64_t n_local, int64_t n_other, int n_iter, int n_warmup, int rank,
-                           int world, int transport, const void* ccl_id, double* out);
+                           int world, int transport, const void* ccl_id, double* out, int check);
 
 #ifdef __cplusplus
 }

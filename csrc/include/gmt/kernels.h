@@ -99,6 +99,16 @@ int gmt_abs_max(int64_t nx, int64_t ny, const double* z, int64_t ld, double* out
  *      decomposition-independent random init. */
 int gmt_fill_poly(int mode, int64_t nx, int64_t ny, double x0, double dx, double y0,
                   double dy, double* z, int64_t ld, void* stream);
+/* Per-exchange halo check (the apps' --check): counts the cells of the
+ * nx x ny block z (pitch ld) that differ from x^3 + y^2 + offset at
+ * x = x0 + i*dx, y = y0 + j*dy by more than rtol * (1 + |expected|), adding
+ * the count to *bad (a device counter) — one small launch after each
+ * exchange over the ghost rows it filled.  gmt_add_scalar adds v to every
+ * cell of a block (the per-iteration offset that makes a stale ghost row
+ * visible). */
+int gmt_poly_check(int64_t nx, int64_t ny, double x0, double dx, double y0, double dy, double offset,
+                   double rtol, const double* z, int64_t ld, unsigned* bad, void* stream);
+int gmt_add_scalar(int64_t nx, int64_t ny, double v, double* z, int64_t ld, void* stream);
 
 /* ---- 2-D 5-point Jacobi sweep (the BASELINE "5-pt Jacobi" extension):
  *      for y in [y0, y0+ny), x in [x0, x0+nx) (absolute array coordinates):

@@ -50,7 +50,13 @@ struct Cfg {
   static constexpr int P = SLIDE ? 7 : 6;       // input rows in flight
   static constexpr int RS = SLIDE ? U : P + 2;  // DMA ring slots
   static constexpr int HS = SLIDE ? 3 : 6;      // hand-off ring slots
-  static constexpr int LAG = 2 * (S - 1);       // the output stage's step lag
+  // step lag of each stage behind the previous one: narrow strips 2 (the
+  // hand-off rows of step s are requested before the barrier that ends step
+  // s); wide strips 3 (a writer leaves its newest hand-off row in flight
+  // across the step barrier: waiting for the three ds_write_b128 a wave has
+  // just issued cost every step ~a fifth, profiles/r04_wide.md)
+  static constexpr int DLAG = SLIDE ? 3 : 2;
+  static constexpr int LAG = DLAG * (S - 1);    // the output stage's step lag
   static_assert(K % S == 0, "equal stages");
   static_assert(NC % 2 == 0 && KL % 2 == 0, "column pairs");
   static_assert(!SLIDE || (U % 3 == 0 && U % RS == 0 && U % HS == 0 && RS >= P + 2), "compile-time slots");
@@ -200,7 +206,7 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   constexpr bool SLIDE = C::SLIDE;
   constexpr int kP = C::P, kRS = C::RS, kHS = C::HS;
   constexpr uint32_t kRow = C::ROW;
-  constexpr int D = 2 * J;                           // step lag behind stage 0
+  constexpr int D = C::DLAG * J;                     // step lag behind stage 0
   constexpr int SPS = kOut ? (EDGE ? NC : NC / 2) : 0;  // global stores per step
   // DMAs per step.  Narrow strips: stage 0 loads the whole row.  Wide strips:
   // stage q < NDMA loads the row's q-th 1-KB piece (an LDS-DMA costs ~60
@@ -352,8 +358,10 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   // adds is read in the middle of step s - 1.
   //   stage 0: input row i = DMA'd window row i, step s uses rows s-2, s-1, s;
   //   stage J > 0: input row i = the row stage J-1 wrote at its step i, step
-  //   s uses rows s-4, s-3, s-2 (published by the barriers of those steps).
-  constexpr int RD = kIn ? 0 : 2;  // step s's newest input row is s - RD
+  //   s uses rows s-2-RD .. s-RD (RD = DLAG: row i is complete once the
+  //   writer has waited for it at the end of its step i + 1, and published by
+  //   that step's barrier).
+  constexpr int RD = kIn ? 0 : C::DLAG;  // step s's newest input row is s - RD
   dv<NC> r0, r1, r2;
   dv<NC> R[3];
   auto load_rows = [&](int s) {  // narrow strips: the three rows of step s
@@ -436,7 +444,9 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
       // at most P-2 younger DMAs are outstanding: then the barrier publishes
       // it to stage 0, which reads row s+2 in the middle of step s+1
       if constexpr (kDma) wait_vmcnt<DPS * (kP - 2)>();
-      step_barrier();
+      // every LDS access but this step's hand-off writes (issued last) done
+      if constexpr (kOut) step_barrier();
+      else asm volatile("s_waitcnt lgkmcnt(%0)\n\ts_barrier" ::"n"(NC / 2) : "memory");
     } else {
       // hand-off row written (visible to the workgroup after the barrier),
       // then the next step's rows requested, then the barrier

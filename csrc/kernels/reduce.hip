@@ -279,6 +279,31 @@ __global__ __launch_bounds__(kBlock) void fill_poly_kernel(int mode, int64_t nx,
   z[iy * ld + ix] = v;
 }
 
+__global__ __launch_bounds__(kBlock) void poly_check_kernel(int64_t nx, int64_t ny, double x0, double dx,
+                                                            double y0, double dy, double offset, double rtol,
+                                                            const double* __restrict__ z, int64_t ld,
+                                                            unsigned* __restrict__ bad) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  bool wrong = false;
+  if (i < nx * ny) {
+    const int64_t ix = i % nx, iy = i / nx;
+    const double x = x0 + ix * dx, y = y0 + iy * dy;
+    const double e = (x * x * x + y * y) + offset;
+    const double v = z[iy * ld + ix];
+    wrong = !(fabs(v - e) <= rtol * (1.0 + fabs(e)));  // NaN counts as wrong
+  }
+  // one atomic per wave with a mismatch
+  const unsigned long long m = __ballot(wrong);
+  if (m && (threadIdx.x & (kWave - 1)) == 0) atomicAdd(bad, static_cast<unsigned>(__popcll(m)));
+}
+
+__global__ __launch_bounds__(kBlock) void add_scalar_kernel(int64_t nx, int64_t ny, double v,
+                                                            double* __restrict__ z, int64_t ld) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= nx * ny) return;
+  z[(i / nx) * ld + i % nx] += v;
+}
+
 }  // namespace gmt
 
 extern "C" int64_t gmt_sum_axis_workspace(int keep_dim, int64_t nx, int64_t ny) {
@@ -376,6 +401,26 @@ extern "C" int gmt_fill_poly(int mode, int64_t nx, int64_t ny, double x0, double
   hipStream_t s = static_cast<hipStream_t>(stream);
   fill_poly_kernel<<<grid_1d((nx * ny + kBlock - 1) / kBlock), kBlock, 0, s>>>(
       mode, nx, ny, x0, dx, y0, dy, z, ld);
+  GMT_RET_LAUNCH();
+}
+
+extern "C" int gmt_poly_check(int64_t nx, int64_t ny, double x0, double dx, double y0, double dy, double offset,
+                              double rtol, const double* z, int64_t ld, unsigned* bad, void* stream) {
+  using namespace gmt;
+  if (nx <= 0 || ny <= 0) return 0;
+  if (!bad || !z || ld < nx) return static_cast<int>(hipErrorInvalidValue);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  poly_check_kernel<<<grid_1d((nx * ny + kBlock - 1) / kBlock), kBlock, 0, s>>>(nx, ny, x0, dx, y0, dy, offset,
+                                                                                 rtol, z, ld, bad);
+  GMT_RET_LAUNCH();
+}
+
+extern "C" int gmt_add_scalar(int64_t nx, int64_t ny, double v, double* z, int64_t ld, void* stream) {
+  using namespace gmt;
+  if (nx <= 0 || ny <= 0) return 0;
+  if (!z || ld < nx) return static_cast<int>(hipErrorInvalidValue);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  add_scalar_kernel<<<grid_1d((nx * ny + kBlock - 1) / kBlock), kBlock, 0, s>>>(nx, ny, v, z, ld);
   GMT_RET_LAUNCH();
 }
 

@@ -105,7 +105,7 @@ def load(device: str = "cuda") -> ctypes.CDLL:
     lib.gmt_engine_jacobi_stat.argtypes = [vp, c_int]
     lib.gmt_engine_jacobi_stat.restype = ctypes.c_double
     lib.gmt_engine_backend.restype = ctypes.c_char_p
-    lib.gmt_engine_deriv_bench.argtypes = [i64, i64, c_int, c_int, c_int, c_int, c_int, vp, vp]
+    lib.gmt_engine_deriv_bench.argtypes = [i64, i64, c_int, c_int, c_int, c_int, c_int, vp, vp, c_int]
     lib.gmt_engine_deriv_bench.restype = c_int
     lib.gmt_engine_watchdog_kick.argtypes = [ctypes.c_char_p]
     lib.gmt_engine_watchdog_kick.restype = None
@@ -388,7 +388,8 @@ class NativeJacobi:
 
 
 def deriv_bench(n_local: int = 1024, n_other: int = 512 * 1024, n_iter: int = 100,
-                n_warmup: int = 5, env: "gdist.DistEnv | None" = None, transport: str = "auto") -> dict:
+                n_warmup: int = 5, env: "gdist.DistEnv | None" = None, transport: str = "auto",
+                check: bool = False) -> dict:
     """The reference's main benchmark on the native engine (one rank per GPU,
     RCCL): ``mpi_stencil2d_gt``'s test_deriv for dim 0 and dim 1 (2-deep
     ghost faces of ``n_other`` values per neighbour — 8 MiB at the reference
@@ -396,14 +397,16 @@ def deriv_bench(n_local: int = 1024, n_other: int = 512 * 1024, n_iter: int = 10
     test_sum (in-place all-reduce of 1024 doubles).  Returns this rank's
     per-exchange seconds (median/mean/min/max), bytes sent per exchange,
     err_norm, and the all-reduce median seconds.  Collective: every rank calls it.
-    Transport as NativeJacobi (RCCL, IPC when ranks share a GPU)."""
+    Transport as NativeJacobi (RCCL, IPC when ranks share a GPU).  ``check``: the
+    ghost rows are compared with the analytic field after every exchange
+    (``bad_ghosts`` per dim; the exchanges stay timed alone)."""
     e = env or gdist.get()
     lib = load("cuda" if e.is_gpu else "cpu")
     transport, cid = _transport_args(lib, e, transport)
-    out = (ctypes.c_double * 16)()
+    out = (ctypes.c_double * 18)()
     with _StdoutToStderr():
         err = lib.gmt_engine_deriv_bench(int(n_local), int(n_other), int(n_iter), int(n_warmup), e.rank,
-                                         e.world_size, transport, cid, out)
+                                         e.world_size, transport, cid, out, int(bool(check)))
     if err:
         raise EngineError(f"gmt_engine_deriv_bench failed: {err}")
     v = list(out)
@@ -411,7 +414,7 @@ def deriv_bench(n_local: int = 1024, n_other: int = 512 * 1024, n_iter: int = 10
     for d in (0, 1):
         o = v[6 * d:6 * d + 6]
         res[f"dim{d}"] = dict(median_s=o[0], mean_s=o[1], min_s=o[2], max_s=o[3], bytes=int(o[4]),
-                              err_norm=o[5], exact_norm=v[14 + d])
+                              err_norm=o[5], exact_norm=v[14 + d], bad_ghosts=int(v[16 + d]))
     res["allreduce_median_s"] = v[12]
     res["allreduce_max_rel_err"] = v[13]
     res["transport"] = transport_label({LOCAL: "local", RCCL: "rccl", IPC: "ipc"}[transport], e)

@@ -355,3 +355,30 @@ def test_watchdog_aborts_hung_exchange():
 def test_watchdog_quiet_on_healthy_run():
     p = run_app("mpi_jacobi2d", "50", "20", "--transport=ipc", "--timeout=30", np=2)
     assert "WATCHDOG" not in p.stdout + p.stderr
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+def test_stencil2d_gt_per_exchange_halo_check(np_):
+    """--check: the ghost rows are compared with the analytic field after
+    EVERY exchange (the field is raised by 1 before each one, so a ghost row
+    left from an earlier exchange is wrong by 1); every test of the matrix
+    reports 0 bad cells over all its exchanges."""
+    out = run_app("mpi_stencil2d_gt", "16", "30", "--no-managed", "--tests=deriv", "--n-other=300", "--check",
+                  np=np_).stdout
+    lines = re.findall(r"# halo check dim:(\d) buf:(\d) \(([\w-]+)\): (\d+) bad ghost cells, (\d+) exchanges", out)
+    assert len(lines) == 4, out
+    assert all(int(b) == 0 and int(n) == 35 for _, _, _, b, n in lines), out
+
+
+def test_stencil2d_gt_halo_check_catches_a_corrupt_cell():
+    """Fault injection: rank 1 overwrites one ghost cell after its 7th
+    exchange; the check counts it and the app exits with status 5."""
+    p = run_app("mpi_stencil2d_gt", "16", "30", "--no-managed", "--tests=deriv", "--n-other=300", "--check",
+                "--dim=1", np=3, env={"GMT_CORRUPT_GHOST": "1:7"}, check=False)
+    assert p.returncode == 5, p.stdout + p.stderr
+    assert re.findall(r"# halo check dim:1 buf:\d \([\w-]+\): 1 bad ghost cells", p.stdout), p.stdout
+
+
+def test_stencil2d_sycl_halo_check():
+    out = run_app("mpi_stencil2d_sycl", "64", "1", "40", "--check", np=2).stdout
+    assert re.search(r"# halo check dim:0 buf:1 \(mpi-host\): 0 bad ghost cells, 45 exchanges", out), out

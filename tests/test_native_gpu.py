@@ -240,3 +240,25 @@ def test_engine_overlap_autotune_periodic(env):
         e.close()
     ref = engine.serial_jacobi(300, 517, 31, True)
     assert float(np.abs(got - ref).max()) < 1e-13
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+@pytest.mark.parametrize("transport", ["ipc", "mpi-host"])
+def test_app_halo_check_every_exchange(np_, transport):
+    """200 exchanges between oversubscribed ranks with the ghost rows checked
+    after every one of them (a reused IPC staging slot or a lost host-staged
+    chunk in any iteration would leave a ghost row off by >= 1): 0 bad cells."""
+    out = _app(["mpi_stencil2d_gt", "64", "200", "--no-managed", "--tests=deriv", "--n-other=4096", "--check",
+                f"--transport={transport}"], np_=np_, timeout=240)
+    lines = re.findall(r"# halo check dim:(\d) buf:(\d) \(([\w-]+)\): (\d+) bad ghost cells, (\d+) exchanges", out)
+    assert len(lines) == 4, out
+    assert all(t == transport and int(b) == 0 and int(n) == 205 for _, _, t, b, n in lines), out
+
+
+def test_app_halo_check_catches_injected_corruption():
+    exe = os.path.join(BIN, "mpi_stencil2d_gt")
+    p = subprocess.run([MPIRUN, "-np", "2", exe, "64", "50", "--no-managed", "--tests=deriv", "--dim=0", "--buf=0",
+                        "--n-other=4096", "--check", "--transport=ipc"], capture_output=True, text=True, timeout=120,
+                       cwd="/tmp", env=dict(os.environ, GMT_CORRUPT_GHOST="0:20"))
+    assert p.returncode == 5, p.stdout + p.stderr
+    assert "# halo check dim:0 buf:0 (ipc): 1 bad ghost cells" in p.stdout, p.stdout
