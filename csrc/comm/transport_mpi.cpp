@@ -1,6 +1,7 @@
 // MPI-based transports: mpi-host, mpi-direct, ipc, and the factory that
 // bootstraps rccl over MPI (gmt/comm.hpp, gmt/transport.hpp).
 #include <dlfcn.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <climits>
@@ -146,6 +147,11 @@ class MpiHostExchange : public Exchange {
   MpiHostExchange(MPI_Comm c, size_t chunk, std::vector<Msg> r, std::vector<Msg> s)
       : c_(c), recvs_(std::move(r)), sends_(std::move(s)), kernel_(kernel_staging()) {
     const size_t kChunk = chunk;
+    for (auto& m : sends_)
+      if (m.block.base && !kernel_) {
+        std::printf("mpi-host: a field block message needs kernel staging (GMT_HOST_STAGE=sdma given)\n");
+        abort_job(EXIT_FAILURE);
+      }
     for (int set = 0; set < 2; ++set)
       for (auto& m : recvs_) rstage_[set].emplace_back(m.bytes, GMT_SPACE_PINNED);
     for (auto& m : sends_) sstage_.emplace_back(m.bytes, kernel_ ? GMT_SPACE_PINNED_COHERENT : GMT_SPACE_PINNED);
@@ -154,18 +160,23 @@ class MpiHostExchange : public Exchange {
         schunks_.push_back({i, off, std::min(kChunk, sends_[i].bytes - off)});
         if (sends_[i].bytes == 0) break;
       }
-    for (size_t i = 0; i < recvs_.size(); ++i)
+    for (size_t i = 0; i < recvs_.size(); ++i) {
       for (size_t off = 0; off < recvs_[i].bytes || off == 0; off += kChunk) {
         rchunks_.push_back({i, off, std::min(kChunk, recvs_[i].bytes - off)});
         if (recvs_[i].bytes == 0) break;
       }
+      (recvs_[i].block.base ? any_block_recv_ : any_flat_recv_) = true;
+    }
     if (kernel_ && !schunks_.empty()) {
       const size_t n = schunks_.size();
       std::vector<gmt_stage_chunk> t(n);
       for (size_t k = 0; k < n; ++k) {
         const Chunk& ch = schunks_[k];
-        t[k] = {static_cast<const char*>(sends_[ch.msg].buf) + ch.off, sstage_[ch.msg].data() + ch.off,
-                static_cast<int64_t>(ch.len)};
+        const Msg& m = sends_[ch.msg];
+        // a field block is gathered in place (the pack and the D2H leg in one
+        // pass); a flat buffer is copied
+        t[k] = stage_chunk(m, m.buf ? static_cast<const char*>(m.buf) + ch.off : nullptr,
+                           sstage_[ch.msg].data() + ch.off, ch);
       }
       table_ = Buffer<gmt_stage_chunk>(n, GMT_SPACE_DEVICE);
       GMT_CHECK("stage table", gmt_rt_memcpy(table_.data(), t.data(), n * sizeof(gmt_stage_chunk)));
@@ -178,7 +189,25 @@ class MpiHostExchange : public Exchange {
       events_.resize(schunks_.size(), nullptr);
       for (auto& e : events_) GMT_CHECK("event", gmt_rt_event_create(&e, 0));
     }
+    if (any_block_recv_ && !rchunks_.empty()) {
+      // per staging set: the scatter descriptors of every receive chunk
+      // (field blocks straight out of page-locked memory)
+      const size_t n = rchunks_.size();
+      for (int set = 0; set < 2; ++set) {
+        std::vector<gmt_stage_chunk> t(n);
+        for (size_t k = 0; k < n; ++k) {
+          const Chunk& ch = rchunks_[k];
+          const Msg& m = recvs_[ch.msg];
+          t[k] = stage_chunk(m, rstage_[set][ch.msg].data() + ch.off,
+                             m.buf ? static_cast<char*>(m.buf) + ch.off : nullptr, ch);
+        }
+        rtable_[set] = Buffer<gmt_stage_chunk>(n, GMT_SPACE_DEVICE);
+        GMT_CHECK("scatter table", gmt_rt_memcpy(rtable_[set].data(), t.data(), n * sizeof(gmt_stage_chunk)));
+      }
+    }
     for (auto& e : h2d_done_) GMT_CHECK("event", gmt_rt_event_create(&e, 0));
+    const char* w = std::getenv("GMT_WAIT_TIMEOUT_MS");
+    wait_limit_s_ = (w && std::atof(w) > 0 ? std::atof(w) : 10000.0) / 1e3;
   }
   ~MpiHostExchange() override {
     for (auto& e : events_) gmt_rt_event_destroy(e);
@@ -215,13 +244,26 @@ class MpiHostExchange : public Exchange {
     sreqs.reserve(schunks_.size());
     size_t next = 0, pending = rchunks_.size();
     std::vector<int> idx(rchunks_.size() ? rchunks_.size() : 1);
-    auto land = [&](int n) {
-      for (int q = 0; q < n; ++q) {
-        const Chunk& ch = rchunks_[idx[q]];
-        if (ch.len)
-          GMT_CHECK("stage H2D", gmt_rt_memcpy_async(static_cast<char*>(recvs_[ch.msg].buf) + ch.off,
-                                                     rstage_[cur_][ch.msg].data() + ch.off, ch.len, s));
+    std::vector<size_t> deferred;
+    // a received chunk: a flat message gets its H2D copy; a field block is
+    // scattered from page-locked memory into the ghost cells by one launch
+    // — after every flat copy when the exchange has both (a flat y face
+    // carries the sender's stale corner ghosts; the corner blocks must land
+    // last, gmt/halo.hpp)
+    auto land_one = [&](size_t k) {
+      const Chunk& ch = rchunks_[k];
+      const Msg& m = recvs_[ch.msg];
+      if (!ch.len) return;
+      if (m.block.base) {
+        if (any_flat_recv_) deferred.push_back(k);
+        else GMT_CHECK("stage scatter", gmt_stage_scatter(1, rtable_[cur_].data() + k, kScatterWgs, s));
+        return;
       }
+      GMT_CHECK("stage H2D", gmt_rt_memcpy_async(static_cast<char*>(m.buf) + ch.off,
+                                                 rstage_[cur_][ch.msg].data() + ch.off, ch.len, s));
+    };
+    auto land = [&](int n) {
+      for (int q = 0; q < n; ++q) land_one(static_cast<size_t>(idx[q]));
       pending -= static_cast<size_t>(n);
     };
     auto send = [&](size_t k) {
@@ -235,6 +277,8 @@ class MpiHostExchange : public Exchange {
       return kernel_ ? __atomic_load_n(flags_.data() + k, __ATOMIC_ACQUIRE) >= epoch_
                      : gmt_rt_event_query(events_[k]) == 0;
     };
+    const double t0 = MPI_Wtime();
+    long polls = 0;
     while (next < schunks_.size() || pending > 0) {
       bool progress = false;
       while (next < schunks_.size() && staged(next)) {
@@ -252,14 +296,44 @@ class MpiHostExchange : public Exchange {
       }
       if (progress) continue;
       if (next < schunks_.size()) {  // nothing landed: block on the next D2H chunk
-        if (kernel_) continue;      // poll its flag (and the receives) again
-        GMT_CHECK("stage D2H wait", gmt_rt_event_synchronize(events_[next]));
-        send(next++);
-      } else {  // every chunk is sent: block on the receives
-        int n = 0;
-        GMT_MPI_CHECK(MPI_Waitsome(static_cast<int>(rreqs_.size()), rreqs_.data(), &n, idx.data(),
-                                   MPI_STATUSES_IGNORE));
-        if (n > 0 && n != MPI_UNDEFINED) land(n);
+        if (!kernel_) {
+          GMT_CHECK("stage D2H wait", gmt_rt_event_synchronize(events_[next]));
+          send(next++);
+          continue;
+        }
+        // poll its host flag (and the receives) again: bounded by wall
+        // clock, the stream's error state checked, the core yielded now and
+        // then (ranks share the host's cores with MPI progress)
+        if ((++polls & 1023) == 0) {
+          const int q = gmt_rt_stream_query(s);
+          if (q != 0 && q != 1) {
+            std::printf("mpi-host: the staging stream failed before chunk %zu of %zu was staged: %s\n", next,
+                        schunks_.size(), gmt_rt_error_string(q));
+            abort_job(EXIT_FAILURE);
+          }
+          if (MPI_Wtime() - t0 > wait_limit_s_) {
+            std::printf("mpi-host: chunk %zu of %zu never staged within %.1f s (GMT_WAIT_TIMEOUT_MS)\n", next,
+                        schunks_.size(), wait_limit_s_);
+            abort_job(EXIT_FAILURE);
+          }
+          sched_yield();
+        }
+        continue;
+      }
+      // every chunk is sent: block on the receives
+      int n = 0;
+      GMT_MPI_CHECK(MPI_Waitsome(static_cast<int>(rreqs_.size()), rreqs_.data(), &n, idx.data(),
+                                 MPI_STATUSES_IGNORE));
+      if (n > 0 && n != MPI_UNDEFINED) land(n);
+    }
+    if (!deferred.empty()) {  // the field blocks, after every flat copy
+      std::sort(deferred.begin(), deferred.end());
+      for (size_t a = 0; a < deferred.size();) {  // runs of consecutive chunks: one launch each
+        size_t b = a + 1;
+        while (b < deferred.size() && deferred[b] == deferred[b - 1] + 1) ++b;
+        GMT_CHECK("stage scatter", gmt_stage_scatter(static_cast<int>(b - a), rtable_[cur_].data() + deferred[a],
+                                                     kScatterWgs, s));
+        a = b;
       }
     }
     waitall(sreqs, "mpi-host exchange");
@@ -271,11 +345,26 @@ class MpiHostExchange : public Exchange {
   struct Chunk {
     size_t msg, off, len;
   };
+  // the staging descriptor of chunk ch of message m: flat (rows 0) or the
+  // packed doubles [off/8, (off+len)/8) of the message's field block
+  static gmt_stage_chunk stage_chunk(const Msg& m, const void* src, void* dst, const Chunk& ch) {
+    gmt_stage_chunk t{src, dst, static_cast<int64_t>(ch.len), 0, 0, 0, nullptr};
+    if (m.block.base) {
+      t.rows = static_cast<int64_t>(m.block.rows);
+      t.ld = static_cast<int64_t>(m.block.ld);
+      t.first = static_cast<int64_t>(ch.off / sizeof(double));
+      t.block = m.block.base;
+    }
+    return t;
+  }
   static constexpr int kStageWgs = 32;
+  static constexpr int kScatterWgs = 32;
   MPI_Comm c_;
   std::vector<Msg> recvs_, sends_;
   bool kernel_;
+  bool any_block_recv_ = false, any_flat_recv_ = false;
   Buffer<gmt_stage_chunk> table_;
+  Buffer<gmt_stage_chunk> rtable_[2];
   Buffer<unsigned> counters_;
   Buffer<uint64_t> flags_;  // per send chunk: the exchange (epoch) whose data it holds
   uint64_t epoch_ = 0;
@@ -286,6 +375,7 @@ class MpiHostExchange : public Exchange {
   gmt_event_t h2d_done_[2] = {nullptr, nullptr};
   bool armed_[2] = {false, false};
   int cur_ = 1;
+  double wait_limit_s_ = 10.0;
 };
 
 class MpiHostTransport : public MpiTransport {
@@ -302,6 +392,12 @@ class MpiHostTransport : public MpiTransport {
   }
   Kind kind() const override { return Kind::MpiHost; }
   const char* name() const override { return "mpi-host"; }
+  // GMT_HOST_BLOCKS=0: pack / unpack halo faces through device buffers (the
+  // round-3 five-hop path, for A/B) instead of staging them in place
+  bool takes_blocks() const override {
+    const char* e = std::getenv("GMT_HOST_BLOCKS");
+    return MpiHostExchange::kernel_staging() && !(e && e[0] == '0');
+  }
   std::unique_ptr<Exchange> plan(const std::vector<Msg>& r, const std::vector<Msg>& s) override {
     return std::make_unique<MpiHostExchange>(comm_, chunk_, r, s);
   }

@@ -371,13 +371,35 @@ int gmt_ipc_exchange(const gmt_ipc_plan* p, void*) {
   return 0;
 }
 
+// packed doubles of a strided chunk <-> its contiguous run (stage.hip strided_part)
+static void strided_chunk(const gmt_stage_chunk& c, bool gather) {
+  const int64_t n = c.bytes / 8;
+  double* run = gather ? static_cast<double*>(c.dst) : const_cast<double*>(static_cast<const double*>(c.src));
+  for (int64_t t = 0; t < n; ++t) {
+    const int64_t e = c.first + t, col = e / c.rows, row = e - col * c.rows;
+    double* f = c.block + row + col * c.ld;
+    if (gather) run[t] = *f;
+    else *f = run[t];
+  }
+}
+
 // CPU backend of csrc/kernels/stage.hip: copy, then publish each chunk's flag
 int gmt_stage_copy(int n_chunks, const gmt_stage_chunk* chunks, unsigned*, uint64_t* flags, uint64_t value,
                    int wgs_per_chunk, void*) {
   if (n_chunks < 0 || wgs_per_chunk < 1 || (n_chunks > 0 && (!chunks || !flags))) return 1;
   for (int k = 0; k < n_chunks; ++k) {
-    if (chunks[k].bytes > 0) std::memcpy(chunks[k].dst, chunks[k].src, static_cast<size_t>(chunks[k].bytes));
+    if (chunks[k].rows > 0) strided_chunk(chunks[k], true);
+    else if (chunks[k].bytes > 0) std::memcpy(chunks[k].dst, chunks[k].src, static_cast<size_t>(chunks[k].bytes));
     __atomic_store_n(flags + k, value, __ATOMIC_RELEASE);
+  }
+  return 0;
+}
+
+int gmt_stage_scatter(int n_chunks, const gmt_stage_chunk* chunks, int wgs_per_chunk, void*) {
+  if (n_chunks < 0 || wgs_per_chunk < 1 || (n_chunks > 0 && !chunks)) return 1;
+  for (int k = 0; k < n_chunks; ++k) {
+    if (chunks[k].rows > 0) strided_chunk(chunks[k], false);
+    else if (chunks[k].bytes > 0) std::memcpy(chunks[k].dst, chunks[k].src, static_cast<size_t>(chunks[k].bytes));
   }
   return 0;
 }

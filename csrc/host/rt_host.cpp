@@ -242,6 +242,7 @@ int gmt_rt_event_record(gmt_event_t e, gmt_stream_t) {
 }
 int gmt_rt_event_synchronize(gmt_event_t) { return kOk; }
 int gmt_rt_event_query(gmt_event_t) { return kOk; }
+int gmt_rt_stream_query(gmt_stream_t) { return kOk; }
 int gmt_rt_event_elapsed_ms(float* ms, gmt_event_t a, gmt_event_t b) {
   *ms = static_cast<float>(reinterpret_cast<HostEvent*>(b)->t_ms -
                            reinterpret_cast<HostEvent*>(a)->t_ms);

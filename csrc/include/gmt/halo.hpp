@@ -71,14 +71,28 @@ class Halo2D {
     const bool lo_full = corners_ || (cx && nb.south < 0), hi_full = corners_ || (cx && nb.north < 0);
     const size_t xrow0 = lo_full ? 0 : gy, xrows = ny_ + (lo_full ? gy : 0) + (hi_full ? gy : 0);
     std::vector<comm::Msg> recvs, sends;
-    auto x_face = [&](int peer, size_t send_row, size_t recv_row, int send_tag, int recv_tag) {
-      Face fc;
-      fc.sbuf = Buffer<double>(static_cast<size_t>(gx) * xrows, buf_space);
-      fc.rbuf = Buffer<double>(static_cast<size_t>(gx) * xrows, buf_space);
-      fc.send = f_.sub(send_row, gx, xrow0, xrows);
-      fc.recv = f_.sub(recv_row, gx, xrow0, xrows);
+    // x faces and corner blocks are strided: packed into device buffers by
+    // one fused launch, or handed to a transport that moves blocks in place
+    blocks_ = t_.takes_blocks();
+    auto strided = [&](Face& fc, int peer, int send_tag, int recv_tag) {
+      const size_t n = static_cast<size_t>(gx) * fc.send.ncols;
+      if (blocks_) {
+        sends.push_back({nullptr, n * sizeof(double), peer, send_tag,
+                         {fc.send.data, static_cast<size_t>(gx), fc.send.ncols, fc.send.ld}});
+        recvs.push_back({nullptr, n * sizeof(double), peer, recv_tag,
+                         {fc.recv.data, static_cast<size_t>(gx), fc.recv.ncols, fc.recv.ld}});
+        return;
+      }
+      fc.sbuf = Buffer<double>(n, buf_space);
+      fc.rbuf = Buffer<double>(n, buf_space);
       sends.push_back({fc.sbuf.data(), fc.sbuf.bytes(), peer, send_tag});
       recvs.push_back({fc.rbuf.data(), fc.rbuf.bytes(), peer, recv_tag});
+    };
+    auto x_face = [&](int peer, size_t send_row, size_t recv_row, int send_tag, int recv_tag) {
+      Face fc;
+      fc.send = f_.sub(send_row, gx, xrow0, xrows);
+      fc.recv = f_.sub(recv_row, gx, xrow0, xrows);
+      strided(fc, peer, send_tag, recv_tag);
       xfaces_.push_back(std::move(fc));
     };
     if (gx > 0) {
@@ -91,12 +105,9 @@ class Halo2D {
                         int rtag) {
         if (peer < 0) return;
         Face fc;
-        fc.sbuf = Buffer<double>(static_cast<size_t>(gx) * gy, buf_space);
-        fc.rbuf = Buffer<double>(static_cast<size_t>(gx) * gy, buf_space);
         fc.send = f_.sub(srow, gx, scol, gy);
         fc.recv = f_.sub(rrow, gx, rcol, gy);
-        sends.push_back({fc.sbuf.data(), fc.sbuf.bytes(), peer, stag});
-        recvs.push_back({fc.rbuf.data(), fc.rbuf.bytes(), peer, rtag});
+        strided(fc, peer, stag, rtag);
         xfaces_.push_back(std::move(fc));
       };
       const size_t lo = gx, hi = nx_, glo = 0, ghi = gx + nx_;  // rows (x)
@@ -226,7 +237,7 @@ class Halo2D {
     unpack_x_faces(s);  // x faces and (one-phase mode) the corner blocks
   }
   void pack_x_faces(gmt_stream_t s) {
-    if (xfaces_.empty()) return;
+    if (xfaces_.empty() || blocks_) return;  // blocks: the transport reads the faces in place
     gmt_copy2d_desc d[GMT_MAX_COPY2D];
     int n = 0;
     for (auto& fc : xfaces_)
@@ -235,7 +246,7 @@ class Halo2D {
     GMT_CHECK("halo pack", gmt_copy2d_batched(n, d, sizeof(double), s));
   }
   void unpack_x_faces(gmt_stream_t s) {
-    if (xfaces_.empty()) return;
+    if (xfaces_.empty() || blocks_) return;  // blocks: the transport wrote the ghosts in place
     gmt_copy2d_desc d[GMT_MAX_COPY2D];
     int n = 0;
     for (auto& fc : xfaces_)
@@ -258,6 +269,7 @@ class Halo2D {
   size_t nx_ = 0, ny_ = 0;
   Neighbors nb_;
   std::vector<Face> xfaces_, yfaces_;
+  bool blocks_ = false;     // strided faces moved in place by the transport (Transport::takes_blocks)
   bool corners_ = false;    // two-phase corner mode
   bool one_phase_ = false;  // corner blocks to the diagonal neighbours
   std::unique_ptr<comm::Exchange> ex_;    // all faces, or the y faces in corner mode

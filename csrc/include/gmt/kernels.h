@@ -235,14 +235,25 @@ int gmt_ipc_exchange(const gmt_ipc_plan* plan, void* stream);
  *      complete and visible system-wide, `value` is stored into flags[k]
  *      (GMT_SPACE_PINNED_COHERENT memory) so the host can hand chunk k to MPI
  *      while later chunks are still being copied.  The chunk table and the
- *      per-chunk arrival counters (zero between launches) are device memory. */
+ *      per-chunk arrival counters (zero between launches) are device memory.
+ *      A chunk with rows > 0 is strided on its field side: it is the packed
+ *      doubles [first, first + bytes/8) of a column-major block of `rows`
+ *      doubles per column at pitch `ld` doubles starting at `block` (a halo
+ *      face read straight out of the field: no separate pack launch, no
+ *      device send buffer).  gmt_stage_copy gathers such a chunk from
+ *      `block` into dst; gmt_stage_scatter writes src into `block` (a
+ *      received chunk from page-locked memory straight into the ghost rows;
+ *      rows == 0: a plain copy src -> dst). */
 typedef struct gmt_stage_chunk {
   const void* src;
   void* dst;
   int64_t bytes;
+  int64_t rows, ld, first; /* strided field side (rows == 0: contiguous) */
+  double* block;
 } gmt_stage_chunk;
 int gmt_stage_copy(int n_chunks, const gmt_stage_chunk* chunks, unsigned* counters, uint64_t* flags,
                    uint64_t value, int wgs_per_chunk, void* stream);
+int gmt_stage_scatter(int n_chunks, const gmt_stage_chunk* chunks, int wgs_per_chunk, void* stream);
 
 /* One kernel per entry point: the variants the defaults were chosen against
  * are measured by csrc/bench/variant_bench.hip, not shipped in this ABI. */

@@ -112,6 +112,7 @@ int gmt_rt_event_destroy(gmt_event_t e);
 int gmt_rt_event_record(gmt_event_t e, gmt_stream_t s);
 int gmt_rt_event_synchronize(gmt_event_t e);
 int gmt_rt_event_query(gmt_event_t e); /* 0 = complete, 1 = pending, else error */
+int gmt_rt_stream_query(gmt_stream_t s); /* 0 = idle, 1 = work pending, else the stream's error */
 int gmt_rt_event_elapsed_ms(float* ms, gmt_event_t start, gmt_event_t end);
 int gmt_rt_stream_begin_capture(gmt_stream_t s);
 int gmt_rt_stream_end_capture(gmt_stream_t s, gmt_graph_t* g);

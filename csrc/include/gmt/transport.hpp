@@ -6,8 +6,10 @@
 // (mpi_stencil2d_gt.cc:147-176).  On an MI355X node MPI is the control plane
 // and the data plane is one of:
 //
-//   mpi-host   pack -> D2H into pinned staging -> MPI -> H2D -> unpack
-//              (reference stage_host / buf:1; works everywhere)
+//   mpi-host   face -> page-locked staging (one kernel gathers the strided
+//              face, per-chunk flags) -> MPI -> one kernel scatters from
+//              page-locked memory into the ghost rows (reference stage_host /
+//              buf:1; works everywhere)
 //   mpi-direct device/managed pointers straight to MPI — only when MPI can
 //              read them: a GPU-aware MPI (GMT_MPI_GPU_AWARE=1), managed or
 //              host memory, or the host backend
@@ -41,11 +43,22 @@ namespace comm {
 
 class Control;
 
+// A column-major block of a field: `rows` contiguous doubles per column,
+// `cols` columns at pitch `ld` doubles (a halo face in place)
+struct Block {
+  double* base = nullptr;
+  size_t rows = 0, cols = 0, ld = 0;
+};
+
 struct Msg {
-  void* buf;     // device (or managed/host) memory
+  void* buf;     // device (or managed/host) memory; nullptr with a block on a strided transport
   size_t bytes;
   int peer;      // rank in the transport's communicator
   int tag;       // matches a send on the peer with the same tag
+  // the message's packed contents in place (rows x cols, packed column by
+  // column): a transport with takes_blocks() reads sends from / writes
+  // receives into the field directly — no separate pack / unpack launch
+  Block block = {};
 };
 
 class Exchange {
@@ -95,6 +108,10 @@ class Transport {
   }
   // the host control plane under the transport, when it has one
   virtual Control* control() { return nullptr; }
+  // plans accept messages given as a field Block (buf == nullptr) and move
+  // them in place (mpi-host's kernel staging: the face is gathered straight
+  // into page-locked memory and scattered back out of it)
+  virtual bool takes_blocks() const { return false; }
   int rank() const { return rank_; }
   int size() const { return size_; }
 

@@ -48,7 +48,7 @@ struct Cfg {
   static constexpr int NL = K / S;              // levels per stage
   static constexpr int U = unroll_for(NL);
   static constexpr int P = SLIDE ? 7 : 6;       // input rows in flight
-  static constexpr int RS = SLIDE ? U : P + 2;  // DMA ring slots
+  static constexpr int RS = P + 2;              // DMA ring slots (compile-time slot indices when U % RS == 0)
   static constexpr int HS = SLIDE ? 3 : 6;      // hand-off ring slots
   // step lag of each stage behind the previous one: narrow strips 2 (the
   // hand-off rows of step s are requested before the barrier that ends step
@@ -59,7 +59,7 @@ struct Cfg {
   static constexpr int LAG = DLAG * (S - 1);    // the output stage's step lag
   static_assert(K % S == 0, "equal stages");
   static_assert(NC % 2 == 0 && KL % 2 == 0, "column pairs");
-  static_assert(!SLIDE || (U % 3 == 0 && U % RS == 0 && U % HS == 0 && RS >= P + 2), "compile-time slots");
+  static_assert(!SLIDE || (U % 3 == 0 && U % HS == 0), "compile-time register and hand-off slots");
   static_assert(SLIDE || HS >= 5, "hand ring: rows of steps s-4..s");
 };
 
@@ -380,12 +380,14 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   };
   // wide strips: input row i (i = s0 + j, s0 a multiple of U: every slot
   // index is a constant of the unrolled step)
-  auto load_one = [&](auto Jc) {  // the newest input row of step s0 + Jc + 1
+  constexpr bool kRingFixed = C::U % kRS == 0;  // DMA ring slot of a row: a constant of the unrolled step
+  auto load_one = [&](auto Jc, int s) {  // the newest input row of step s + 1 (s = s0 + Jc)
     constexpr int i = decltype(Jc)::value + 1 - RD;  // its index mod U (+ a multiple of U)
     constexpr int im = ((i % 3) + 3) % 3;
     if constexpr (kIn) {
       // row s+1: every piece landed before the barrier that ended step s-1
-      R[im] = lds_row<NC>(ring + (((i % kRS) + kRS) % kRS) * kRow, lane);
+      const int slot = kRingFixed ? (i % kRS) : (s + 1) % kRS;
+      R[im] = lds_row<NC>(ring + slot * kRow, lane);
     } else {
       R[im] = lds_row<NC>(hand_rd + (((i % kHS) + kHS) % kHS) * kRow, lane);
     }
@@ -413,7 +415,7 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
       constexpr int m0 = (((i2 - 2) % 3) + 3) % 3, m1 = (((i2 - 1) % 3) + 3) % 3, m2 = ((i2 % 3) + 3) % 3;
       v = level(R[m0], R[m1], R[m2], rbase - dir * PB);
       __builtin_amdgcn_sched_barrier(0);
-      load_one(Jc);  // into R[m0], free now
+      load_one(Jc, s);  // into R[m0], free now
     } else {
       v = level(r0, r1, r2, rbase - dir * PB);
     }
@@ -438,7 +440,7 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
     }
     // the ring slot of row s-2 (narrow) / s+P-RS (wide) is free: prefetch row
     // s+P into it
-    dma(s + kP, SLIDE ? (j + kP) % kRS : (s + kP) % kRS);
+    dma(s + kP, (SLIDE && kRingFixed) ? (j + kP) % kRS : (s + kP) % kRS);
     if constexpr (SLIDE) {
       // this wave's piece of row s+2 (issued at step s+2-P) has landed once
       // at most P-2 younger DMAs are outstanding: then the barrier publishes

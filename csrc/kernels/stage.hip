@@ -16,6 +16,25 @@
 namespace gmt {
 namespace stage {
 
+// packed doubles [first, first + n) of a column-major block (rows per column,
+// pitch ld) <-> a contiguous run: one double per lane per step (halo faces
+// are 2..20 rows deep, so a column's rows are adjacent lanes: one 16..160-B
+// run per column, the field read or written once)
+template <bool GATHER>
+__device__ __forceinline__ void strided_part(const gmt_stage_chunk& c, int part, int g) {
+  const int64_t n = c.bytes / 8;
+  const uint32_t rows = static_cast<uint32_t>(c.rows);
+  const int64_t step = static_cast<int64_t>(g) * kBlock;
+  double* run = GATHER ? static_cast<double*>(c.dst) : const_cast<double*>(static_cast<const double*>(c.src));
+  for (int64_t t = static_cast<int64_t>(part) * kBlock + threadIdx.x; t < n; t += step) {
+    const uint64_t e = static_cast<uint64_t>(c.first + t);
+    const uint64_t col = e / rows, row = e - col * rows;
+    double* f = c.block + row + col * static_cast<uint64_t>(c.ld);
+    if constexpr (GATHER) run[t] = *f;
+    else *f = run[t];
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void stage_copy_kernel(const gmt_stage_chunk* __restrict__ chunks,
                                                             unsigned* __restrict__ counters,
                                                             uint64_t* __restrict__ flags, uint64_t value, int g) {
@@ -24,7 +43,9 @@ __global__ __launch_bounds__(kBlock) void stage_copy_kernel(const gmt_stage_chun
   const char* src = static_cast<const char*>(c.src);
   char* dst = static_cast<char*>(c.dst);
   const int64_t step = static_cast<int64_t>(g) * kBlock * 16;
-  if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
+  if (c.rows > 0) {
+    strided_part<true>(c, part, g);
+  } else if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
     const int64_t n16 = c.bytes / 16 * 16;
     int64_t o = (static_cast<int64_t>(part) * kBlock + threadIdx.x) * 16;
     // two 16-B loads in flight per lane per iteration
@@ -55,6 +76,22 @@ __global__ __launch_bounds__(kBlock) void stage_copy_kernel(const gmt_stage_chun
   }
 }
 
+// received chunks from page-locked host memory into the field (strided) or
+// a device buffer: the GPU reads the host buffer over the link
+__global__ __launch_bounds__(kBlock) void stage_scatter_kernel(const gmt_stage_chunk* __restrict__ chunks, int g) {
+  const int k = blockIdx.x / g, part = blockIdx.x % g;
+  const gmt_stage_chunk c = chunks[k];
+  if (c.rows > 0) {
+    strided_part<false>(c, part, g);
+    return;
+  }
+  const char* src = static_cast<const char*>(c.src);
+  char* dst = static_cast<char*>(c.dst);
+  for (int64_t o = static_cast<int64_t>(part) * kBlock + threadIdx.x; o < c.bytes;
+       o += static_cast<int64_t>(g) * kBlock)
+    dst[o] = src[o];
+}
+
 }  // namespace stage
 }  // namespace gmt
 
@@ -66,5 +103,15 @@ extern "C" int gmt_stage_copy(int n_chunks, const gmt_stage_chunk* chunks, unsig
   if (n_chunks == 0) return 0;
   stage::stage_copy_kernel<<<grid_1d(static_cast<int64_t>(n_chunks) * wgs_per_chunk), kBlock, 0,
                              static_cast<hipStream_t>(stream)>>>(chunks, counters, flags, value, wgs_per_chunk);
+  GMT_RET_LAUNCH();
+}
+
+// the table is read by the kernel: a host (pinned) or device pointer
+extern "C" int gmt_stage_scatter(int n_chunks, const gmt_stage_chunk* chunks, int wgs_per_chunk, void* stream) {
+  using namespace gmt;
+  if (n_chunks < 0 || wgs_per_chunk < 1 || (n_chunks > 0 && !chunks)) return static_cast<int>(hipErrorInvalidValue);
+  if (n_chunks == 0) return 0;
+  stage::stage_scatter_kernel<<<grid_1d(static_cast<int64_t>(n_chunks) * wgs_per_chunk), kBlock, 0,
+                                static_cast<hipStream_t>(stream)>>>(chunks, wgs_per_chunk);
   GMT_RET_LAUNCH();
 }

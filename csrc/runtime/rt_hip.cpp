@@ -199,6 +199,12 @@ int gmt_rt_event_query(gmt_event_t e) {
   if (r == hipErrorNotReady) return 1;
   return static_cast<int>(r);
 }
+int gmt_rt_stream_query(gmt_stream_t s) {
+  hipError_t r = hipStreamQuery(S(s));
+  if (r == hipSuccess) return 0;
+  if (r == hipErrorNotReady) return 1;
+  return static_cast<int>(r);
+}
 int gmt_rt_event_elapsed_ms(float* ms, gmt_event_t a, gmt_event_t b) {
   RT_RET(hipEventElapsedTime(ms, E(a), E(b)));
 }

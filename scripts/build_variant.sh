@@ -21,8 +21,16 @@ case "$expr" in
   *) sed -i "$expr" $D/src/jacobi5tb.hpp ;;
 esac
 [ "$expr" != cur ] && cmp -s csrc/kernels/jacobi5tb.hpp $D/src/jacobi5tb.hpp && { echo "sed changed nothing"; exit 1; }
-ls $D/src/jacobi5tb*.hip | xargs -P 8 -I{} sh -c '/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Icsrc/include -munsafe-fp-atomics -c {} -o '$D'/obj/$(basename {} .hip).o'
+# ONLY=kf: rebuild only that instantiation unit (+ jacobi5tb.hip) and take
+# the other K from the production build (each unit's device code is its own
+# code object, so the units need not share the edited header)
+srcs=$(ls $D/src/jacobi5tb*.hip)
+[ -n "$ONLY" ] && srcs="$D/src/jacobi5tb_$ONLY.hip $D/src/jacobi5tb.hip"
+echo $srcs | tr ' ' '\n' | xargs -P 8 -I{} sh -c '/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Icsrc/include -munsafe-fp-atomics -c {} -o '$D'/obj/$(basename {} .hip).o'
 others=$(ls build/obj/kernels/*.o | grep -v jacobi5tb)
+if [ -n "$ONLY" ]; then
+  for o in build/obj/kernels/jacobi5tb_k*.o; do [ -e $D/obj/$(basename $o) ] || others="$others $o"; done
+fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/libgmt.so $D/obj/*.o $others build/obj/runtime/rt_hip.o \
   -Wl,-soname,libgmt.so -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lamdhip64 -lrocprofiler-sdk-roctx -ldl
 echo "built $D/libgmt.so"
