@@ -339,43 +339,40 @@ int JacobiSolver::halo_mask() const {
 }
 
 void JacobiSolver::xk_launch(int K, int n, const int64_t* rects, int parity, int sig_rects, int sig_rows,
-                             gmt_stream_t st) {
+                             gmt_stream_t st, int sig_cols) {
   const double* u = buf_[parity].data();
   double* un = buf_[parity ^ 1].data();
   const int64_t dom[4] = {xo_, nx_, yo_, ny_};
   const int mask = halo_mask();
   unsigned* count = reinterpret_cast<unsigned*>(sig_.data());
-  const bool sig = sig_rects > 0 || sig_rows > 0;
+  const bool sig = sig_rects > 0 || sig_rows > 0 || sig_cols != 0;
   gmt_tb_opts o{K,   cfg_.wg_waves, cfg_.seg_rows, exact_ ? 1 : 0, sig_rects, sig ? count : nullptr,
-                sig ? sig_.data() + 1 : nullptr, sig_rows, st == sb_ && sb_ ? comm_cus_ : 0};
+                sig ? sig_.data() + 1 : nullptr, sig_rows, st == sb_ && sb_ ? comm_cus_ : 0, sig_cols};
   GMT_CHECK("jacobi tb", gmt_jacobi5tb(&o, n, rects, dom, mask, u, un, ld_, ny_ + 2 * g_, st ? st : s_));
 }
 
-// Output rects of a band-first pass.  W/E halo sides: full-height bands one
-// workgroup's strips wide (the signalling rects, short segments), first.
-// S/N halo sides: no rects of their own — the main rect's segments next to
-// those sides are its row bands (gmt_tb_opts.signal_rows = g_: dispatched
-// first, N ones walked bottom-up, each output wave signals once its first
-// g_ rows are stored), so the S/N bands cost no extra workgroups or
-// pipeline warm-ups.  False when the domain is too small for the bands.
-bool JacobiSolver::band_rects(int K, int64_t* rects, int* n_bands, int* sig_rows) const {
+// The bands of a band-first pass, all inside the one output rect (the
+// interior): no band rects, no extra strips, segments or warm-ups.
+// W/E halo sides: the rect's first / last strip group, every segment at
+// full length, dispatched first; each of their workgroups signals when done
+// (gmt_tb_opts.signal_cols) — with the pass's later rounds still to run.
+// S/N halo sides: the other groups' segments next to those sides are row
+// bands (gmt_tb_opts.signal_rows = g_: dispatched next, N ones walked
+// bottom-up, each output wave signals once its first g_ rows are stored).
+// (Round 3 took the W/E bands as separate rects with 3/4-length segments:
+// 1.05-1.08x the serial pass on the N = 8 shares, profiles/r03_shares.md.)
+// False when the domain is too small for the bands.
+bool JacobiSolver::band_rects(int K, int64_t* rects, int* sig_cols, int* sig_rows) const {
   const int mask = halo_mask();
   const bool hw = mask & 1, he = mask & 2, hs = mask & 4, hn = mask & 8;
   const int64_t wb = std::max<int64_t>(gmt_jacobi5tb_group_cols(K, cfg_.wg_waves), g_);
-  const int64_t x0 = xo_ + (hw ? wb : 0), x1 = xo_ + nx_ - (he ? wb : 0);
   const int rb = (hs ? 1 : 0) + (hn ? 1 : 0);
-  if (wb <= 0 || x1 - x0 < wb || (rb > 0 && ny_ < rb * std::max<int64_t>(32, g_)) || ny_ < 64) return false;
-  int n = 0;
-  auto add = [&](int64_t ax, int64_t anx, int64_t ay, int64_t any) {
-    const int64_t r[4] = {ax, anx, ay, any};
-    std::copy(r, r + 4, rects + 4 * n++);
-  };
-  if (hw) add(xo_, wb, yo_, ny_);
-  if (he) add(x1, wb, yo_, ny_);
-  *n_bands = n;
+  if (wb <= 0 || (rb > 0 && ny_ < rb * std::max<int64_t>(32, g_)) || ny_ < 64) return false;
+  const int64_t r[4] = {xo_, nx_, yo_, ny_};
+  std::copy(r, r + 4, rects);
+  *sig_cols = (hw ? 1 : 0) | (he ? 2 : 0);
   *sig_rows = rb > 0 ? g_ : 0;
-  add(x0, x1 - x0, yo_, ny_);
-  return n > 0 || rb > 0;
+  return *sig_cols != 0 || rb > 0;
 }
 
 void JacobiSolver::exchange_now(int parity) {
@@ -404,9 +401,9 @@ void JacobiSolver::enqueue_block(int parity, int K) {
     return;
   }
   if (!fresh_[parity]) exchange_now(parity);
-  int64_t rects[4 * 5];
-  int nb = 0, rows = 0;
-  if (!cfg_.overlap || !band_rects(K, rects, &nb, &rows)) {
+  int64_t rects[4];
+  int cols = 0, rows = 0;
+  if (!cfg_.overlap || !band_rects(K, rects, &cols, &rows)) {
     xk_launch(K, 1, dom, parity, 0, 0);
     fresh_[parity ^ 1] = false;
     return;
@@ -418,11 +415,11 @@ void JacobiSolver::enqueue_block(int parity, int K) {
   GMT_CHECK("wait", gmt_rt_stream_wait_event(cs_, ev_start_));
   if (sb_) {  // the pass on the compute CUs, joined back into s_ below
     GMT_CHECK("wait", gmt_rt_stream_wait_event(sb_, ev_start_));
-    xk_launch(K, nb + 1, rects, parity, nb, rows, sb_);
+    xk_launch(K, 1, rects, parity, 0, rows, sb_, cols);
     GMT_CHECK("event", gmt_rt_event_record(ev_band_, sb_));
     GMT_CHECK("wait", gmt_rt_stream_wait_event(s_, ev_band_));
   } else {
-    xk_launch(K, nb + 1, rects, parity, nb, rows);
+    xk_launch(K, 1, rects, parity, 0, rows, nullptr, cols);
   }
   GMT_CHECK("signal wait", gmt_signal_wait(sig_.data() + 1, sig_.data() + 2,
                                            reinterpret_cast<unsigned*>(sig_.data() + 3), cs_));
@@ -435,9 +432,9 @@ void JacobiSolver::enqueue_block(int parity, int K) {
 }
 
 bool JacobiSolver::band_mode(int K) const {
-  int64_t rects[4 * 5];
-  int nb = 0, rows = 0;
-  return cfg_.overlap && halo_[0] && halo_[0]->active() && band_rects(K, rects, &nb, &rows);
+  int64_t rects[4];
+  int cols = 0, rows = 0;
+  return cfg_.overlap && halo_[0] && halo_[0]->active() && band_rects(K, rects, &cols, &rows);
 }
 
 void JacobiSolver::step_block() {

@@ -266,11 +266,12 @@ int gmt_jacobi5tb(const gmt_tb_opts* o, int n_rect, const int64_t* rects, const 
     if (r[1] <= 0 || r[3] <= 0) continue;
     if (r[0] < K || r[2] < K || r[0] + r[1] + K > ld || r[2] + r[3] + K > nrows) return 1;
   }
-  const bool sig = o->signal_rects > 0 || o->signal_rows > 0;
+  const bool cols = (o->signal_cols & 3) != 0;
+  const bool sig = o->signal_rects > 0 || o->signal_rows > 0 || cols;
   if (o->signal_rects < 0 || o->signal_rects > n_rect || (sig && (!o->signal_count || !o->signal)) ||
-      o->signal_rows < 0 || (o->signal_rows > 0 && o->signal_rects >= n_rect))
+      o->signal_rows < 0 || ((o->signal_rows > 0 || cols) && o->signal_rects >= n_rect) || (o->signal_cols & ~3))
     return 1;
-  for (int k = 0; k < o->signal_rects + (o->signal_rows > 0 ? 1 : 0); ++k)
+  for (int k = 0; k < o->signal_rects + (o->signal_rows > 0 || cols ? 1 : 0); ++k)
     if (rects[4 * k + 1] <= 0 || rects[4 * k + 3] <= 0) return 1;
   if (o->signal_rows > 0) {  // the same feasibility rule as the GPU launcher
     const int rb = ((mask & 4) ? 1 : 0) + ((mask & 8) ? 1 : 0);

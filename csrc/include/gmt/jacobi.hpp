@@ -131,8 +131,9 @@ class JacobiSolver {
   void enqueue_block(int parity, int k);  // k <= ks_ fused sweeps
   // one fused k-sweep launch on `n` output rects (gmt_jacobi5tb)
   void xk_launch(int k, int n, const int64_t* rects, int parity, int sig_rects, int sig_rows,
-                 gmt_stream_t st = nullptr);
-  bool band_rects(int k, int64_t* rects, int* n_bands, int* sig_rows) const;
+                 gmt_stream_t st = nullptr, int sig_cols = 0);
+  // the band-first pass's rect (the interior) and its column / row bands
+  bool band_rects(int k, int64_t* rects, int* sig_cols, int* sig_rows) const;
   bool band_mode(int k) const;  // the fused k-sweep pass runs band-first (overlap)
   void exchange_now(int parity);  // blocking-order halo exchange of buf_[parity] on the compute stream
   void step_block();

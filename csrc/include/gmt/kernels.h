@@ -169,6 +169,13 @@ typedef struct gmt_tb_opts {
      gmt_rt_stream_create_cumask): the segment planner sizes the launch for
      the resident workgroups of the remaining ones (0 = every CU). */
   int reserved_cus;
+  /* Column bands (0 = none; bit 0 W, bit 1 E): the first / last strip
+     group of rect signal_rects — every one of its segments, full length —
+     is dispatched before the rest of the launch and each of its workgroups
+     counts toward the same signal when done: the rect's W / E halo columns
+     are ready after the first round of workgroups, with no band rects of
+     their own (no extra strips, segments or pipeline warm-ups). */
+  int signal_cols;
 } gmt_tb_opts;
 int gmt_jacobi5tb_supported(int sweeps);
 /* Largest sweep count whose kernel runs without scratch: GMT_TB_MAX_SWEEPS

@@ -108,9 +108,11 @@ int jacobi5tb_run(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, con
   const int K = o.sweeps;
   if (!gmt_jacobi5tb_supported(K)) return static_cast<int>(hipErrorInvalidValue);
   if (n_rect < 0 || n_rect > kMaxRect) return static_cast<int>(hipErrorInvalidValue);
+  const bool cols = (o.signal_cols & 3) != 0;
   if (o.wg_waves < 0 || o.wg_waves > kMaxThreads / kWave || o.seg_rows < 0 || o.signal_rects < 0 || o.reserved_cus < 0 ||
-      o.signal_rects > n_rect || ((o.signal_rects > 0 || o.signal_rows > 0) && (!o.signal_count || !o.signal)) ||
-      o.signal_rows < 0 || (o.signal_rows > 0 && o.signal_rects >= n_rect))
+      o.signal_rects > n_rect ||
+      ((o.signal_rects > 0 || o.signal_rows > 0 || cols) && (!o.signal_count || !o.signal)) ||
+      o.signal_rows < 0 || ((o.signal_rows > 0 || cols) && o.signal_rects >= n_rect) || (o.signal_cols & ~3))
     return static_cast<int>(hipErrorInvalidValue);
   if ((reinterpret_cast<uintptr_t>(u) & 7u) || (reinterpret_cast<uintptr_t>(un) & 7u) || ld <= 0)
     return static_cast<int>(hipErrorInvalidValue);
@@ -118,7 +120,7 @@ int jacobi5tb_run(const gmt_tb_opts* opts, int n_rect, const int64_t* rects, con
   for (int k = 0; k < n_rect; ++k) {
     const int64_t* r = rects + 4 * k;
     if (r[1] <= 0 || r[3] <= 0) {
-      if (k < o.signal_rects || (o.signal_rows > 0 && k == o.signal_rects))  // signalling rects are never empty
+      if (k < o.signal_rects || ((o.signal_rows > 0 || cols) && k == o.signal_rects))  // signalling rects are never empty
         return static_cast<int>(hipErrorInvalidValue);
       continue;
     }

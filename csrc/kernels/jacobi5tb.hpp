@@ -105,6 +105,13 @@ struct Args {
   int rb_rect;                   // -1: none
   int rb_s, rb_n;                // the rect's first / last segments are row bands
   int64_t sig_rows, sig_total, sig_dispatch;
+  // column bands (gmt_tb_opts.signal_cols): rect cb_rect's first (cb_lo)
+  // and last (cb_hi) strip groups — every segment at full length — are
+  // dispatched before everything else of the rect, and each of their
+  // workgroups counts one arrival when done (they are the first of the
+  // sig_wgs leading workgroups)
+  int cb_rect;                   // -1: none
+  int cb_lo, cb_hi;
 };
 
 // NC doubles of one strip row held by a lane (its columns c0 .. c0+NC-1)
@@ -507,30 +514,58 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   // so the launch's tail is made of fast ones: (A) the edge segments, all
   // strip groups; (B) the interior segments' first and last strip groups;
   // (C) the rest.
+  // (K) before all of them: the column bands of a band-first pass
+  // (Args::cb_rect: the first / last strip group, every segment).  The
+  // categories below then cover the other groups only.
   const int64_t ry0 = a.r[k][2], ry1 = a.r[k][2] + a.r[k][3];
   const int64_t e0 = a.e0[k], e1 = a.e1[k];
-  const int64_t nedge = (e0 > 0) + (e1 > 0), nbnd = ngroups < 2 ? ngroups : 2;
+  const int64_t nedge = (e0 > 0) + (e1 > 0);
   const int rbs = k == a.rb_rect ? a.rb_s : 0, rbn = k == a.rb_rect ? a.rb_n : 0, rb = rbs + rbn;
+  // column-band groups: 0 (cb_lo) and ngroups - 1 (cb_hi); one group when there is only one
+  const int cblo = k == a.cb_rect ? a.cb_lo : 0;
+  const int cbhi = k == a.cb_rect && ngroups > 1 ? a.cb_hi : 0;
+  const int64_t ncb = (cblo || (k == a.cb_rect && a.cb_hi && ngroups == 1)) + cbhi;
+  const int64_t nsb = nedge + a.nmid_b[k];  // segments of a boundary group
+  const int64_t ng = ngroups - ncb;         // the other groups: gi = cbf + 0 .. ng - 1
+  const int64_t cbf = ncb > 0 && (cblo || ngroups == 1) ? 1 : 0;
+  // the other boundary groups (0 / ngroups - 1 that are not column bands)
+  const bool b0 = cbf == 0, b1 = ngroups > 1 && !cbhi;
+  const int64_t nbnd = (b0 ? 1 : 0) + (b1 ? 1 : 0);
+  const int64_t n_cb = ncb * nsb, n_rb = rb * ng, n_ed = nedge * ng, n_bd = (a.nmid_b[k] - rb) * nbnd;
   int64_t gi, m = -1;  // m: interior segment index, -1: edge segment `edge`
   int edge = 0, dir = 1;
   bool band = false;
-  if (lt < rb * ngroups) {  // (R): S band = first interior segment, N band = last (walked bottom-up)
-    gi = lt % ngroups;
-    const bool north = lt >= ngroups || !rbs;
+  auto seg_of = [&](int64_t sg, int64_t nm) {  // segment sg of a group: edge 0, mids, edge 1
+    if (e0 > 0 && sg == 0) {
+      edge = 0;
+    } else if (sg < (e0 > 0) + nm) {
+      m = sg - (e0 > 0);
+    } else {
+      edge = 1;
+    }
+  };
+  if (lt < n_cb) {  // (K)
+    const int64_t c = lt / nsb;
+    gi = (c == 0 && cbf) ? 0 : ngroups - 1;
+    seg_of(lt % nsb, a.nmid_b[k]);
+  } else if (lt < n_cb + n_rb) {  // (R): S band = first interior segment, N band = last (walked bottom-up)
+    const int64_t l0 = lt - n_cb;
+    gi = cbf + l0 % ng;
+    const bool north = l0 >= ng || !rbs;
     const int64_t nm = (gi == 0 || gi == ngroups - 1) ? a.nmid_b[k] : a.nmid[k];
     m = north ? nm - 1 : 0;
     dir = north ? -1 : 1;
     band = true;
-  } else if (lt < rb * ngroups + nedge * ngroups) {  // (A)
-    const int64_t l1 = lt - rb * ngroups;
-    edge = (l1 / ngroups == 0 && e0 > 0) ? 0 : 1;
-    gi = l1 % ngroups;
-  } else if (lt < rb * ngroups + nedge * ngroups + (a.nmid_b[k] - rb) * nbnd) {  // (B)
-    const int64_t l2 = lt - rb * ngroups - nedge * ngroups;
+  } else if (lt < n_cb + n_rb + n_ed) {  // (A)
+    const int64_t l1 = lt - n_cb - n_rb;
+    edge = (l1 / ng == 0 && e0 > 0) ? 0 : 1;
+    gi = cbf + l1 % ng;
+  } else if (lt < n_cb + n_rb + n_ed + n_bd) {  // (B)
+    const int64_t l2 = lt - n_cb - n_rb - n_ed;
     m = rbs + l2 / nbnd;
-    gi = l2 % nbnd == 0 ? 0 : ngroups - 1;
+    gi = (l2 % nbnd == 0 && b0) ? 0 : ngroups - 1;
   } else {  // (C)
-    const int64_t l3 = lt - rb * ngroups - nedge * ngroups - (a.nmid_b[k] - rb) * nbnd;
+    const int64_t l3 = lt - n_cb - n_rb - n_ed - n_bd;
     m = rbs + l3 / (ngroups - 2);
     gi = 1 + l3 % (ngroups - 2);
   }
@@ -788,6 +823,9 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     if (o.reserved_cus < cus) per_cu = static_cast<int>(static_cast<int64_t>(per_cu) * (cus - o.reserved_cus) / cus);
   }
   const int sig_rects = o.signal_rects;  // non-empty rects (checked): the same indices after the compaction
+  // column bands: the first rect after the signalling ones (checked non-empty)
+  const int cbk = (o.signal_cols & 3) ? sig_rects : -1;
+  if (cbk >= a.n) return static_cast<int>(hipErrorInvalidValue);
   // row bands: the first rect after the signalling ones (checked non-empty)
   const int rbk = o.signal_rows > 0 ? sig_rects : -1;
   const int rbs = rbk >= 0 && (mask & 4) ? 1 : 0, rbn = rbk >= 0 && (mask & 8) ? 1 : 0;
@@ -811,6 +849,20 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   const int64_t nb = a.tstart[a.n];
   a.sig_wgs = a.tstart[sig_rects];
   a.rb_rect = -1;
+  a.cb_rect = -1;
+  int64_t cb_groups = 0, cb_strips = 0;
+  if (cbk >= 0) {
+    // every segment of rect cbk's first / last strip group: its leading workgroups
+    const int64_t groups = (a.nstrip[cbk] + a.nw - 1) / a.nw;
+    a.cb_rect = cbk;
+    a.cb_lo = (o.signal_cols & 1) ? 1 : 0;
+    a.cb_hi = (o.signal_cols & 2) ? 1 : 0;
+    cb_groups = groups == 1 ? 1 : a.cb_lo + a.cb_hi;
+    if (groups == 1) cb_strips = a.nstrip[cbk];
+    else cb_strips = (a.cb_lo ? std::min<int64_t>(a.nw, a.nstrip[cbk]) : 0) +
+                     (a.cb_hi ? a.nstrip[cbk] - (groups - 1) * a.nw : 0);
+    a.sig_wgs += cb_groups * ((sp.e0[cbk] > 0) + (sp.e1[cbk] > 0) + sp.nmid_b[cbk]);
+  }
   a.sig_total = a.sig_wgs;
   a.sig_dispatch = a.sig_wgs;
   if (rbk >= 0) {
@@ -825,8 +877,9 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     a.rb_n = rbn;
     a.sig_rows = o.signal_rows;
     const int64_t groups = (a.nstrip[rbk] + a.nw - 1) / a.nw;
-    a.sig_total += rb * a.nstrip[rbk];   // one arrival per output wave (= strip) of every band
-    a.sig_dispatch += rb * groups;       // rect rbk's band tiles follow the signalling rects
+    const bool cbr = rbk == cbk;         // column-band groups take no row bands
+    a.sig_total += rb * (a.nstrip[rbk] - (cbr ? cb_strips : 0));  // one arrival per output wave (= strip) of every band
+    a.sig_dispatch += rb * (groups - (cbr ? cb_groups : 0));      // rect rbk's band tiles follow the signalling ones
   }
   a.prio = nb <= per_cu ? 1 : 0;
   a.sig_count = o.signal_count;

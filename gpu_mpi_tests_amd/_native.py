@@ -43,6 +43,19 @@ class Copy2dDesc(ctypes.Structure):
 MAX_COPY2D = 8
 
 
+class StageChunk(ctypes.Structure):
+    """gmt_stage_chunk (csrc/include/gmt/kernels.h)."""
+    _fields_ = [
+        ("src", c_vp),
+        ("dst", c_vp),
+        ("bytes", c_i64),
+        ("rows", c_i64),
+        ("ld", c_i64),
+        ("first", c_i64),
+        ("block", c_vp),
+    ]
+
+
 class TbOpts(ctypes.Structure):
     """gmt_tb_opts (csrc/include/gmt/kernels.h)."""
     _fields_ = [
@@ -55,6 +68,7 @@ class TbOpts(ctypes.Structure):
         ("signal", c_vp),
         ("signal_rows", c_int),
         ("reserved_cus", c_int),
+        ("signal_cols", c_int),
     ]
 
 _SIGS = {
@@ -84,6 +98,10 @@ _SIGS = {
     "gmt_jacobi5tb_plan": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_i64, c_i64, c_vp]),
     "gmt_jacobi5tb_group_cols": (c_i64, [c_int, c_int]),
     "gmt_signal_wait": (c_int, [c_vp, c_vp, c_vp, c_vp]),
+    "gmt_stage_copy": (c_int, [c_int, c_vp, c_vp, c_vp, ctypes.c_uint64, c_int, c_vp]),
+    "gmt_stage_scatter": (c_int, [c_int, c_vp, c_int, c_vp]),
+    "gmt_poly_check": (c_int, [c_i64, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_vp, c_i64, c_vp, c_vp]),
+    "gmt_add_scalar": (c_int, [c_i64, c_i64, c_dbl, c_vp, c_i64, c_vp]),
     "gmt_error_string": (ctypes.c_char_p, [c_int]),
     "gmt_device_synchronize": (c_int, []),
     "gmt_build_info": (ctypes.c_char_p, []),

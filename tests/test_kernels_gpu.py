@@ -3,6 +3,7 @@
 GPU-only (``-m gpu``).  Sizes include odd extents, non-multiples of 64/512,
 unaligned views (scalar fallback paths) and multi-block tails.
 """
+import ctypes
 import os
 
 import pytest
@@ -268,3 +269,78 @@ def test_vsum_matches_fp64_reference(n):
 def test_abs_max_matches_reference(ny, nx):
     z = torch.randn(ny, nx + 3, dtype=torch.float64, device=DEV)[:, 1:nx + 1]
     assert float(ops.abs_max(z)) == float(z.abs().max())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+@pytest.mark.parametrize("rows,cols,chunk", [(2, 1000, 1 << 10), (20, 333, 4096), (3, 7, 8)])
+def test_stage_gather_scatter_field_blocks(rows, cols, chunk):
+    """mpi-host's in-place staging (csrc/kernels/stage.hip): a strided halo
+    face gathered chunk by chunk straight out of the field into page-locked
+    memory (with the per-chunk flags), then scattered back out of it into
+    another block — bitwise against the packed face."""
+    L = _native.lib()
+    ld = rows + 37
+    field = _rand(cols, ld, seed=rows)            # column-major: `cols` columns of ld doubles
+    face = field[:, 5:5 + rows]                   # rows x cols block, pitch ld
+    n = rows * cols
+    stage = torch.zeros(n, dtype=torch.float64).pin_memory()
+    nchunk = (n * 8 + chunk - 1) // chunk
+    descs = (_native.StageChunk * nchunk)()
+    for k in range(nchunk):
+        off = k * chunk
+        descs[k] = _native.StageChunk(None, stage.data_ptr() + off, min(chunk, n * 8 - off), rows, ld, off // 8,
+                                      face.data_ptr())
+    table = torch.empty(ctypes.sizeof(descs), dtype=torch.uint8, device=DEV)
+    table.copy_(torch.frombuffer(bytearray(descs), dtype=torch.uint8))
+    counters = torch.zeros(nchunk, dtype=torch.int32, device=DEV)
+    flags = torch.zeros(nchunk, dtype=torch.int64).pin_memory()
+    _native.check(L.gmt_stage_copy(nchunk, table.data_ptr(), counters.data_ptr(), flags.data_ptr(), 7, 4, _stream()),
+                  "stage_copy")
+    torch.cuda.synchronize()
+    packed = face.contiguous().reshape(-1).cpu()   # packed column by column: rows per column contiguous
+    assert torch.equal(stage, packed)
+    assert (flags == 7).all()
+    # scatter into another field's block
+    out = torch.full_like(field, -1.0)
+    dst = out[:, 9:9 + rows]
+    for k in range(nchunk):
+        off = k * chunk
+        descs[k] = _native.StageChunk(stage.data_ptr() + off, None, min(chunk, n * 8 - off), rows, ld, off // 8,
+                                      dst.data_ptr())
+    table.copy_(torch.frombuffer(bytearray(descs), dtype=torch.uint8))
+    _native.check(L.gmt_stage_scatter(nchunk, table.data_ptr(), 3, _stream()), "stage_scatter")
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, 9:9 + rows].cpu(), face.cpu())
+    keep = torch.ones(ld, dtype=torch.bool)
+    keep[9:9 + rows] = False
+    assert (out[:, keep] == -1.0).all()
+
+
+def test_poly_check_counts_mismatches():
+    """The per-exchange halo check kernel: x^3 + y^2 + offset on a lattice,
+    vs a plain fp64 torch evaluation; one perturbed cell and one NaN counted."""
+    L = _native.lib()
+    nx, ny, ld = 7, 300, 11
+    x0, dx, y0, dy, off = -0.25, 1.0 / 64, 3.0, 1.0 / 128, 17.0
+    xs = x0 + torch.arange(nx, dtype=torch.float64) * dx
+    ys = y0 + torch.arange(ny, dtype=torch.float64) * dy
+    z = torch.zeros(ny, ld, dtype=torch.float64)
+    z[:, :nx] = (xs[None, :] ** 3 + ys[:, None] ** 2) + off
+    z = z.to(DEV)
+    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
+    args = (nx, ny, x0, dx, y0, dy, off, 1e-9, z.data_ptr(), ld, bad.data_ptr(), _stream())
+    _native.check(L.gmt_poly_check(*args), "poly_check")
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 0
+    z[10, 3] += 1.0
+    z[200, 6] = float("nan")
+    _native.check(L.gmt_poly_check(*args), "poly_check")
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 2
+    _native.check(L.gmt_add_scalar(nx, ny, 1.0, z.data_ptr(), ld, _stream()), "add_scalar")
+    torch.cuda.synchronize()
+    assert float(z[0, 0].item()) == float(((xs[0] ** 3 + ys[0] ** 2) + off + 1.0).item())
+    assert float(z[0, nx].item()) == 0.0  # outside the block: untouched
