@@ -49,7 +49,12 @@ struct Cfg {
   static constexpr int U = unroll_for(NL);
   static constexpr int P = SLIDE ? 7 : 6;       // input rows in flight
   static constexpr int RS = P + 2;              // DMA ring slots (compile-time slot indices when U % RS == 0)
-  static constexpr int HS = SLIDE ? 3 : 6;      // hand-off ring slots
+  // FLOW (wide strips): stages synchronise through per-ring progress
+  // counters in LDS instead of one workgroup barrier per step, so a stage
+  // stalls only for its own producer / consumer (hand-off rings of 5 slots:
+  // up to three steps of slack)
+  static constexpr bool FLOW = false;
+  static constexpr int HS = SLIDE ? (FLOW ? 5 : 3) : 6;  // hand-off ring slots
   // step lag of each stage behind the previous one: narrow strips 2 (the
   // hand-off rows of step s are requested before the barrier that ends step
   // s); wide strips 3 (a writer leaves its newest hand-off row in flight
@@ -59,7 +64,8 @@ struct Cfg {
   static constexpr int LAG = DLAG * (S - 1);    // the output stage's step lag
   static_assert(K % S == 0, "equal stages");
   static_assert(NC % 2 == 0 && KL % 2 == 0, "column pairs");
-  static_assert(!SLIDE || (U % 3 == 0 && U % HS == 0), "compile-time register and hand-off slots");
+  static_assert(!SLIDE || (U % 3 == 0 && (FLOW || U % HS == 0)), "compile-time register and hand-off slots");
+  static constexpr int CTL = FLOW ? 64 : 0;     // bytes of progress counters per strip
   static_assert(SLIDE || HS >= 5, "hand ring: rows of steps s-4..s");
 };
 
@@ -67,7 +73,7 @@ struct Cfg {
 template <int K>
 __host__ __device__ constexpr int64_t strip_lds() {
   using C = Cfg<K>;
-  return static_cast<int64_t>(C::RS) * C::ROW + static_cast<int64_t>(C::S - 1) * C::HS * C::ROW;
+  return static_cast<int64_t>(C::RS) * C::ROW + static_cast<int64_t>(C::S - 1) * C::HS * C::ROW + C::CTL;
 }
 
 struct Args {
@@ -226,6 +232,41 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   // hand-off rings: read ring J - 1, write ring J
   char* const hand_rd = ring + kRS * kRow + (J > 0 ? J - 1 : 0) * kHS * kRow;
   char* const hand_wr = ring + kRS * kRow + J * kHS * kRow;
+  // FLOW progress counters (after the hand-off rings): [j] rows < v that
+  // stage j wrote to its ring are complete; [4 + j] rows < v of ring j were
+  // read by stage j + 1; [8 + q] rows < v of DMA piece q landed; [12] rows
+  // < v of the DMA ring were read by stage 0.  Every spin is bounded (a
+  // protocol error yields wrong results, never a hung GPU).
+  constexpr bool FLOW = SLIDE && C::FLOW;
+  int* const ctl = reinterpret_cast<int*>(ring + kRS * kRow + (C::S - 1) * kHS * kRow);
+  auto ctl_put = [&](int i, int v) {
+    if (lane == 0) __atomic_store_n(ctl + i, v, __ATOMIC_RELAXED);
+  };
+  // the spin is one asm block: a loop in the unrolled step's control flow
+  // costs its register allocation dozens of copies per step
+  const uint32_t ctl_lds = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ctl));
+  auto wait_ge = [&](int i, int want) {
+    int v, cnt;
+    uint32_t sv;
+    asm volatile(
+        "s_mov_b32 %2, 0x10000\n"
+        "1:\n\t"
+        "ds_read_b32 %0, %3\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_readfirstlane_b32 %1, %0\n\t"
+        "s_cmp_ge_i32 %1, %4\n\t"
+        "s_cbranch_scc1 2f\n\t"
+        "s_sleep 1\n\t"
+        "s_sub_u32 %2, %2, 1\n\t"
+        "s_cbranch_scc0 1b\n"
+        "2:"
+        : "=&v"(v), "=&s"(sv), "=&s"(cnt)
+        : "v"(ctl_lds + 4u * static_cast<uint32_t>(i)), "s"(__builtin_amdgcn_readfirstlane(want))
+        : "memory", "scc");
+    (void)v;
+    (void)sv;
+    (void)cnt;
+  };
   // every kernel argument the loop needs, as values: the asm memory clobbers
   // below would otherwise force a reload of the kernarg segment per use
   const int64_t ld = a.ld;
@@ -344,10 +385,16 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   if constexpr (SLIDE) {
     // wide strips: every loading stage issues its piece of rows 0..P-1 and
     // waits for rows 0 and 1; one extra barrier publishes them (every wave of
-    // the workgroup takes it, idle ones included)
+    // the workgroup takes it, idle ones included) and the FLOW counters
     if constexpr (kDma) {
       static_for<0, kP>([&](auto I) { dma(decltype(I)::value, decltype(I)::value); });
       wait_vmcnt<DPS * (kP - 2)>();
+    }
+    if constexpr (FLOW) {
+      if constexpr (kDma) ctl_put(8 + J, 2);
+      if constexpr (!kOut) ctl_put(J, 0);
+      if constexpr (J > 0) ctl_put(4 + J - 1, 0);
+      if constexpr (kIn) ctl_put(12, 0);
     }
     step_barrier();
   } else if constexpr (kIn) {
@@ -396,7 +443,10 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
       const int slot = kRingFixed ? (i % kRS) : (s + 1) % kRS;
       R[im] = lds_row<NC>(ring + slot * kRow, lane);
     } else {
-      R[im] = lds_row<NC>(hand_rd + (((i % kHS) + kHS) % kHS) * kRow, lane);
+      // FLOW rings (5 slots) do not divide the unroll: the slot of the
+      // absolute row s + 1 - RD
+      const int slot = C::FLOW ? ((s + 1 - RD) % kHS + kHS) % kHS : ((i % kHS) + kHS) % kHS;
+      R[im] = lds_row<NC>(hand_rd + slot * kRow, lane);
     }
   };
   if constexpr (SLIDE) {
@@ -422,6 +472,17 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
       constexpr int m0 = (((i2 - 2) % 3) + 3) % 3, m1 = (((i2 - 1) % 3) + 3) % 3, m2 = ((i2 % 3) + 3) % 3;
       v = level(R[m0], R[m1], R[m2], rbase - dir * PB);
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (FLOW) {
+        // the input row is complete; this step's hand-off slot and DMA ring
+        // slot are free (every wait refers to earlier steps of other waves)
+        if constexpr (kIn) {
+          static_for<0, C::NDMA>([&](auto Q) { wait_ge(8 + decltype(Q)::value, s + 2); });
+        } else {
+          wait_ge(J - 1, s + 2 - RD);
+        }
+        if constexpr (!kOut) wait_ge(4 + J, s - kHS + 1);
+        if constexpr (kDma) wait_ge(12, s + kP - kRS + 1);
+      }
       load_one(Jc, s);  // into R[m0], free now
     } else {
       v = level(r0, r1, r2, rbase - dir * PB);
@@ -442,7 +503,7 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
       }
       store_step(s, v);  // issued every step (warm-up rows are out of range)
     } else {
-      const int slot = SLIDE ? j % kHS : s % kHS;
+      const int slot = (SLIDE && !FLOW) ? j % kHS : s % kHS;
       lds_put<NC>(hand_wr + slot * kRow, lane, v);
     }
     // the ring slot of row s-2 (narrow) / s+P-RS (wide) is free: prefetch row
@@ -454,8 +515,18 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
       // it to stage 0, which reads row s+2 in the middle of step s+1
       if constexpr (kDma) wait_vmcnt<DPS * (kP - 2)>();
       // every LDS access but this step's hand-off writes (issued last) done
-      if constexpr (kOut) step_barrier();
-      else asm volatile("s_waitcnt lgkmcnt(%0)\n\ts_barrier" ::"n"(NC / 2) : "memory");
+      if constexpr (FLOW) {
+        if constexpr (kOut) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NC / 2) : "memory");
+        if constexpr (kDma) ctl_put(8 + J, s + 3);
+        if constexpr (!kOut) ctl_put(J, s);               // row s - 1 complete
+        if constexpr (J > 0) ctl_put(4 + J - 1, s + 2 - RD);  // row s + 1 - RD read
+        if constexpr (kIn) ctl_put(12, s + 2);            // row s + 1 read
+      } else if constexpr (kOut) {
+        step_barrier();
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(%0)\n\ts_barrier" ::"n"(NC / 2) : "memory");
+      }
     } else {
       // hand-off row written (visible to the workgroup after the barrier),
       // then the next step's rows requested, then the barrier
@@ -588,7 +659,7 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   if (strip >= a.nstrip[k]) {  // no strip for this wave
     if constexpr (G > 1) {
       // the workgroup's per-step barriers (wide strips: and the prologue's)
-      for (int s = 0; s < nsteps + (C::SLIDE ? 1 : 0); ++s) step_barrier();
+      for (int s = 0; s < (C::SLIDE ? (C::FLOW ? 1 : nsteps + 1) : nsteps); ++s) step_barrier();
     }
     return;
   }

@@ -131,7 +131,7 @@ def test_app_jacobi_ipc_graph_matches_serial(np_):
     hipGraphs with several ranks sharing the GPU; bitwise vs the serial run."""
     out = _app(["mpi_jacobi2d", "301", "23", "--check", "--tblock", "--tsteps=4", "--warmup=3", "--graph",
                 "--transport=ipc"], np_=np_)
-    assert re.search(r"transport = ipc overlap=\d graph=1", out), out
+    assert re.search(r"transport = ipc overlap=\d( \([\w-]+\))? graph=1", out), out
     m = re.search(r"check\s*: max\|diff\| vs serial = ([0-9.eE+-]+) OK", out)
     assert m and float(m.group(1)) == 0.0, out
 
