@@ -17,7 +17,11 @@ namespace tb {
 
 constexpr int kMaxK1 = 10;  // largest single-wave K
 
-constexpr bool tb_wide(int K) { return K == 20; }
+// The wide K = 20 kernel is bitwise-correct and cuts VALU per update by 14%,
+// but on MI355X it runs 10% below the narrow one (profiles/r04_wide.md):
+// built only when this is flipped (scripts/build_variant.sh A/B builds).
+constexpr bool kWideK20 = false;
+constexpr bool tb_wide(int K) { return kWideK20 && K == 20; }
 constexpr int tb_nc(int K) { return tb_wide(K) ? 6 : 4; }
 constexpr int tb_stages(int K) { return K <= kMaxK1 ? 1 : (tb_wide(K) ? 4 : 2); }
 constexpr int tb_cols(int K) { return tb_nc(K) * 64; }

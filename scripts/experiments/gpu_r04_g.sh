@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4 (g): after the GPU suite passed (r04_f: 776 tests),
-#  (1) wide K = 20 kernel diagnostics (P = 5 / 9, no sched_barrier, no step
-#      barrier) vs production and round 3,
+#  (1) wide K = 20 kernel (build/ab_wide, opt-in) and its diagnostics (P = 9, no step
+#      barrier, FLOW counters) vs production (narrow, = round 3),
 #  (2) the strong-scaling shares, serial vs band-first with column bands,
 #  (3) mpi-host: faces staged in place vs packed (GMT_HOST_BLOCKS=0).
 set -o pipefail
@@ -17,7 +17,7 @@ for p in "" "--periodic"; do
   LD_LIBRARY_PATH=$R/build/ab_flow timeout -k 10 120 build/bin/mpi_jacobi2d --ny=700 --nx=1900 0 47 --check --tblock --tsteps=20 $p 2>&1 | grep -E "vs serial" | tee -a $OUT/flow_check.txt
 done
 for rep in 1 2; do
-  for v in r03 new p5 p9 nobar flow; do
+  for v in new wide flow nobar p9; do
     lp=""; [ "$v" != new ] && lp=$R/build/ab_$v
     : > $OUT/$v.$rep.log
     for shp in "--jacobi-n=32768 --iters=20" "--jacobi-ny=8192 --jacobi-nx=16384 --iters=100"; do
