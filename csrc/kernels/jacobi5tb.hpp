@@ -7,7 +7,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <map>
+#include <mutex>
 #include <utility>
+#include <vector>
 
 #include "common.hpp"
 #include "gmt/kernels.h"
@@ -810,15 +813,69 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
     fill(std::min<int64_t>(seg_rows, lmax), &wgs);
     return p;
   }
+  // The launch's time is its makespan: workgroups start in dispatch order
+  // on the first free slot (resident_wgs of them) and run (rows + 2K + lag)
+  // steps, rounded up to the unroll, rule-path ones ~1.8x longer per step
+  // (tests the loop census: 5837 vs 3218 VALU per 19 steps at K = 20).
+  // Round 3 priced a plan as rounds x (L + 2K), blind to the short edge and
+  // boundary-group workgroups that finish early and leave their slots idle
+  // for the rest of a round: 15% of a one-round 8192 x 16384 pass
+  // (profiles/r04_shares.md).  The dispatch order modelled is tb_block's:
+  // per rect, column bands, row bands, edge segments, boundary groups, rest.
+  constexpr int64_t u = Cfg<K>::U;
+  auto steps = [&](int64_t rows) { return static_cast<double>((rows + 2 * K + Cfg<K>::LAG + u - 1) / u * u); };
+  std::vector<double> dur;
+  std::vector<double> slot;
+  auto makespan = [&]() {
+    dur.clear();
+    for (int k = 0; k < a.n; ++k) {
+      const int64_t groups = (a.nstrip[k] + a.nw - 1) / a.nw, nbnd = groups < 2 ? groups : 2;
+      const int64_t ny = a.r[k][3], ry0 = a.r[k][2], ry1 = ry0 + ny;
+      const bool yrule = (ry0 - K < a.dom[2] && !(a.mask & 4)) || (ry1 + K > a.dom[2] + a.dom[3] && !(a.mask & 8));
+      const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
+      const bool xrule = (rx0 - Cfg<K>::KL < a.dom[0] && !(a.mask & 1)) ||
+                         (rx1 + Cfg<K>::KL > a.dom[0] + a.dom[1] && !(a.mask & 2));
+      const double fr = 1.8;
+      const double fe = yrule ? fr : 1.0;              // an edge segment touches its Dirichlet row
+      const double fb = xrule || (yrule && p.e0[k] == 0 && p.e1[k] == 0) ? fr : 1.0;
+      const double fm = yrule && p.e0[k] == 0 && p.e1[k] == 0 ? fr : 1.0;
+      for (int64_t g = 0; g < groups; ++g) {
+        if (p.e0[k] > 0) dur.push_back(fe * steps(p.e0[k]));
+        if (p.e1[k] > 0) dur.push_back(fe * steps(p.e1[k]));
+      }
+      for (int64_t g = 0; g < nbnd; ++g)
+        for (int64_t m = 0; m < p.nmid_b[k]; ++m) dur.push_back(fb * steps(p.lmid_b[k]));
+      for (int64_t g = nbnd; g < groups; ++g)
+        for (int64_t m = 0; m < p.nmid[k]; ++m) dur.push_back(fm * steps(p.lmid[k]));
+    }
+    // list scheduling on the resident slots (a min-heap of free times)
+    const size_t ns = static_cast<size_t>(std::max<int64_t>(1, resident_wgs));
+    slot.assign(std::min(ns, dur.size()), 0.0);
+    size_t used = 0;
+    double end = 0.0;
+    auto cmp = [](double x, double y) { return x > y; };
+    for (double d : dur) {
+      double t0 = 0.0;
+      if (used < slot.size()) {
+        slot[used++] = d;
+        if (used == slot.size()) std::make_heap(slot.begin(), slot.end(), cmp);
+        end = std::max(end, d);
+        continue;
+      }
+      std::pop_heap(slot.begin(), slot.end(), cmp);
+      t0 = slot.back();
+      slot.back() = t0 + d;
+      std::push_heap(slot.begin(), slot.end(), cmp);
+      end = std::max(end, t0 + d);
+    }
+    return end;
+  };
   int64_t best_l = 128;
   double best = 1e300;
   for (int64_t L = 128; L <= std::min<int64_t>(2048, lmax); L += 32) {
     fill(L, &wgs);
-    const double rounds = static_cast<double>((wgs + resident_wgs - 1) / resident_wgs);
-    // a segment runs L + 2K (+2 with two stages) steps, rounded up to the unroll
-    constexpr int64_t u = Cfg<K>::U;
-    const double cost = rounds * static_cast<double>((L + 2 * K + Cfg<K>::LAG + u - 1) / u * u);
-    if (cost < best) {
+    const double cost = makespan();
+    if (cost < best - 1e-9) {
       best = cost;
       best_l = L;
     }
@@ -903,7 +960,23 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   const int64_t rb_min = std::max<int64_t>(32, o.signal_rows);
   if (rbk >= 0 && (rbk >= a.n || rbs + rbn == 0 || a.r[rbk][3] < (rbs + rbn) * rb_min))
     return static_cast<int>(hipErrorInvalidValue);
-  const SegPlan sp = plan_segments<K>(a, o.seg_rows, lmax, per_cu, sig_rects, rbk, rbs + rbn, rb_min);
+  // the plan depends only on the launch geometry: cached (the makespan
+  // search costs milliseconds; the engine launches the same passes over and over)
+  SegPlan sp;
+  {
+    std::vector<int64_t> key = {a.n, a.nw, a.mask, o.seg_rows, lmax, per_cu, sig_rects, rbk, rbs + rbn, rb_min};
+    for (int k = 0; k < a.n; ++k) key.insert(key.end(), a.r[k], a.r[k] + 4);
+    key.insert(key.end(), a.dom, a.dom + 4);
+    static std::mutex mu;
+    static std::map<std::vector<int64_t>, SegPlan> cache;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it == cache.end()) {
+      if (cache.size() > 256) cache.clear();
+      it = cache.emplace(key, plan_segments<K>(a, o.seg_rows, lmax, per_cu, sig_rects, rbk, rbs + rbn, rb_min)).first;
+    }
+    sp = it->second;
+  }
   a.tstart[0] = 0;
   for (int k = 0; k < a.n; ++k) {
     a.e0[k] = sp.e0[k];
@@ -951,6 +1024,17 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     const bool cbr = rbk == cbk;         // column-band groups take no row bands
     a.sig_total += rb * (a.nstrip[rbk] - (cbr ? cb_strips : 0));  // one arrival per output wave (= strip) of every band
     a.sig_dispatch += rb * (groups - (cbr ? cb_groups : 0));      // rect rbk's band tiles follow the signalling ones
+  }
+  // one output rect: its rule-path and band workgroups (everything before
+  // the interior groups' mid segments) are dispatched round-robin over the
+  // XCDs too, so each XCD's slots get their share of the short and the slow
+  // ones (the makespan model of plan_segments assumes so); the interior
+  // tiles stay XCD-contiguous (adjacent strips share their overlap in L2)
+  if (a.n == 1) {
+    const int64_t groups = (a.nstrip[0] + a.nw - 1) / a.nw;
+    const int64_t rbc = a.rb_rect == 0 ? a.rb_s + a.rb_n : 0;
+    const int64_t n_rest = groups > 2 ? (groups - 2) * (a.nmid[0] - rbc) : 0;
+    a.sig_dispatch = std::max<int64_t>(a.sig_dispatch, nb - n_rest);
   }
   a.prio = nb <= per_cu ? 1 : 0;
   a.sig_count = o.signal_count;
