@@ -83,7 +83,16 @@ class SocketControl : public Control {
       std::printf("gmt control: bad id or rank %d of %d\n", rank, size);
       abort_job(EXIT_FAILURE);
     }
-    const std::string base(tok);
+    // "gmtctl-<pid>-<nonce>-<secret>": names from the public part, the
+    // secret in every hello (an id without one authenticates with "")
+    std::string base(tok), secret;
+    const size_t cut = base.find('-', base.find('-', 7) + 1);
+    if (cut != std::string::npos) {
+      secret = base.substr(cut + 1);
+      base.resize(cut);
+    }
+    char want[64] = {0};
+    std::snprintf(want, sizeof(want), "%s", secret.c_str());
     auto name = [&](int r) { return base + "-" + std::to_string(r); };
     int lfd = -1;
     if (rank < size - 1) {  // higher ranks connect to us
@@ -109,15 +118,30 @@ class SocketControl : public Control {
         ::usleep(2000);
       }
       int32_t me = rank;
-      if (!full_io(fd_[p], &me, sizeof(me), true)) fail("hello", p);
+      if (!full_io(fd_[p], &me, sizeof(me), true) || !full_io(fd_[p], want, sizeof(want), true)) fail("hello", p);
     }
     for (int k = rank + 1; k < size; ++k) {  // accept every higher rank
       pollfd pf{lfd, POLLIN, 0};
       if (::poll(&pf, 1, static_cast<int>(timeout_ * 1000)) <= 0) fail("a higher rank never connected");
       const int f = ::accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
+      if (f < 0) fail("accept");
+      // only this user's processes, and only with the job's secret
+      ucred cr{};
+      socklen_t cl = sizeof(cr);
+      if (::getsockopt(f, SOL_SOCKET, SO_PEERCRED, &cr, &cl) != 0 || cr.uid != ::geteuid()) {
+        ::close(f);
+        --k;  // not a rank of this job: keep waiting for the real one
+        continue;
+      }
       int32_t who = -1;
-      if (f < 0 || !full_io(f, &who, sizeof(who), false) || who <= rank || who >= size || fd_[who] >= 0)
-        fail("accept");
+      char got[64] = {0};
+      if (!full_io(f, &who, sizeof(who), false) || !full_io(f, got, sizeof(got), false) ||
+          std::memcmp(got, want, sizeof(want)) != 0) {
+        ::close(f);
+        --k;
+        continue;
+      }
+      if (who <= rank || who >= size || fd_[who] >= 0) fail("accept");
       fd_[who] = f;
     }
     if (lfd >= 0) ::close(lfd);
@@ -353,11 +377,16 @@ class SocketControl : public Control {
 
 }  // namespace
 
+// id = "gmtctl-<pid>-<name nonce>-<secret>": the abstract socket names use
+// only the part before the secret (they are visible to every local user in
+// /proc/net/unix); every hello carries the secret, which only the job's
+// ranks received (over the launcher's own channel)
 void make_socket_control_id(char* id) {
   std::memset(id, 0, kControlIdBytes);
   std::random_device rd;
-  const unsigned long long r = (static_cast<unsigned long long>(rd()) << 32) ^ rd();
-  std::snprintf(id, kControlIdBytes, "gmtctl-%d-%016llx", static_cast<int>(getpid()), r);
+  auto r64 = [&] { return (static_cast<unsigned long long>(rd()) << 32) ^ rd(); };
+  const unsigned long long n = r64(), s0 = r64(), s1 = r64();
+  std::snprintf(id, kControlIdBytes, "gmtctl-%d-%016llx-%016llx%016llx", static_cast<int>(getpid()), n, s0, s1);
 }
 
 std::unique_ptr<Control> make_socket_control(int rank, int size, const char* id) {

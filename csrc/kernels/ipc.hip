@@ -129,10 +129,13 @@ __global__ __launch_bounds__(kBlock) void ipc_exchange_kernel(Args a) {
     // each role signals on its own: a rank's "ready" must not wait for its
     // own receives (those wait for the peers' "ready")
     if (last_arrival(a.counter + (send ? 0 : 1), static_cast<unsigned>(nrb))) {
+      // the other workgroups' data reached this one through their fence ->
+      // counter RMW -> this acquire; one system-scope release here makes the
+      // chain a formal release sequence for the peer's acquire of the
+      // signal (one thread, once per exchange)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       for (int j = k0; j < k1; ++j) {
         uint64_t* sig = a.chan[j].signal;
-        // relaxed: the workgroup's system-scope release fence above (and the
-        // other workgroups' before their arrivals) already published the data
         if (sig) __hip_atomic_store(sig, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }

@@ -821,7 +821,8 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
   // boundary-group workgroups that finish early and leave their slots idle
   // for the rest of a round: 15% of a one-round 8192 x 16384 pass
   // (profiles/r04_shares.md).  The dispatch order modelled is tb_block's:
-  // per rect, column bands, row bands, edge segments, boundary groups, rest.
+  // per rect, column bands, row bands, edge segments, boundary groups, rest,
+  // on one pool of slots (the XCD-contiguous tile order is not modelled).
   constexpr int64_t u = Cfg<K>::U;
   auto steps = [&](int64_t rows) { return static_cast<double>((rows + 2 * K + Cfg<K>::LAG + u - 1) / u * u); };
   std::vector<double> dur;
@@ -1025,17 +1026,9 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     a.sig_total += rb * (a.nstrip[rbk] - (cbr ? cb_strips : 0));  // one arrival per output wave (= strip) of every band
     a.sig_dispatch += rb * (groups - (cbr ? cb_groups : 0));      // rect rbk's band tiles follow the signalling ones
   }
-  // one output rect: its rule-path and band workgroups (everything before
-  // the interior groups' mid segments) are dispatched round-robin over the
-  // XCDs too, so each XCD's slots get their share of the short and the slow
-  // ones (the makespan model of plan_segments assumes so); the interior
-  // tiles stay XCD-contiguous (adjacent strips share their overlap in L2)
-  if (a.n == 1) {
-    const int64_t groups = (a.nstrip[0] + a.nw - 1) / a.nw;
-    const int64_t rbc = a.rb_rect == 0 ? a.rb_s + a.rb_n : 0;
-    const int64_t n_rest = groups > 2 ? (groups - 2) * (a.nmid[0] - rbc) : 0;
-    a.sig_dispatch = std::max<int64_t>(a.sig_dispatch, nb - n_rest);
-  }
+  // (Dispatching the rule-path workgroups round-robin over the XCDs instead
+  // of XCD-contiguous with the rest cost the Dirichlet 8192 x 16384 and
+  // 16384 x 8192 passes 3-6%: profiles/r04_shares.md.)
   a.prio = nb <= per_cu ? 1 : 0;
   a.sig_count = o.signal_count;
   a.signal = o.signal;
