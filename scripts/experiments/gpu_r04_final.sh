@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 4, rebuilt tree: GPU tests, smoke, driver-config bench, kernel-trace
+# stats of the bench.  Each GPU step under its own time limit; stop at the
+# first failure.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+OUT=gpurun_out/r04_final1
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 1000 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/ > $OUT/pytest.log 2>&1 || { tail -60 $OUT/pytest.log; exit 1; }
+tail -3 $OUT/pytest.log > $OUT/pytest_tail.txt; cat $OUT/pytest_tail.txt
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -30 $OUT/smoke.log; exit 1; }
+tail -2 $OUT/smoke.log
+timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.out 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
+tail -1 $OUT/bench.out > $OUT/bench.json; cat $OUT/bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/prof_bench.out 2>&1 || { tail -30 $OUT/prof_bench.out; exit 1; }
+find $OUT/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $OUT/bench_kernel_stats.csv
+head -12 $OUT/bench_kernel_stats.csv
