@@ -159,14 +159,23 @@ __device__ __forceinline__ void wait_vmcnt() {
 // barrier, so s_barrier needs no vmcnt(0)).
 __device__ __forceinline__ void step_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// LDS row layout: piece q (q < NC/2) of every lane in its own 1-KB block,
+// lane l's columns 2q, 2q+1 at byte 1024 q + 16 l (kPieces), so every
+// ds_read_b128 / ds_write_b128 of a row is one contiguous KB: no bank
+// conflicts (the row-ordered layout, lane l at 8 NC l, cost the 4-column
+// kernel 2e9 conflict cycles per three 32768^2 passes, profiles/r04_wide/
+// r04_c_pmc.md); the LDS-DMA fetches each piece with 16 B per lane at an
+// NC*8-byte stride instead of contiguous 16 B.
+constexpr bool kPieces = true;
+
 // a lane's NC columns of an LDS row (NC / 2 ds_read_b128)
 template <int NC>
 __device__ __forceinline__ dv<NC> lds_row(const char* slot, int lane) {
-  const d2* p = reinterpret_cast<const d2*>(slot) + (NC / 2) * lane;
+  const d2* p = kPieces ? reinterpret_cast<const d2*>(slot) + lane : reinterpret_cast<const d2*>(slot) + (NC / 2) * lane;
   dv<NC> r;
   static_for<0, NC / 2>([&](auto Q) {
     constexpr int q = decltype(Q)::value;
-    const d2 a = p[q];
+    const d2 a = kPieces ? p[q * 64] : p[q];
     r.c[2 * q] = a.x;
     r.c[2 * q + 1] = a.y;
   });
@@ -175,10 +184,10 @@ __device__ __forceinline__ dv<NC> lds_row(const char* slot, int lane) {
 
 template <int NC>
 __device__ __forceinline__ void lds_put(char* slot, int lane, const dv<NC>& v) {
-  d2* p = reinterpret_cast<d2*>(slot) + (NC / 2) * lane;
+  d2* p = kPieces ? reinterpret_cast<d2*>(slot) + lane : reinterpret_cast<d2*>(slot) + (NC / 2) * lane;
   static_for<0, NC / 2>([&](auto Q) {
     constexpr int q = decltype(Q)::value;
-    p[q] = d2{v.c[2 * q], v.c[2 * q + 1]};
+    p[kPieces ? q * 64 : q] = d2{v.c[2 * q], v.c[2 * q + 1]};
   });
 }
 
@@ -296,18 +305,21 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   //  neighbouring row or is zero-filled: garbage outside every output cone)
   const int64_t nrow_in = std::min<int64_t>(L + 2 * K, a.last_row + 1 - yl);
   const __amdgpu_buffer_rsrc_t lrs = row_rsrc(u + yl * ld, static_cast<uint32_t>(nrow_in) * ld8);
-  const uint32_t loff = static_cast<uint32_t>(cf) * 8u + static_cast<uint32_t>(lane) * 16u;
+  // piece q of lane `lane`: global columns NC*lane + 2q, +1 (kPieces) or
+  // the row's bytes [1024 q + 16 lane, +16)
+  const uint32_t loff = static_cast<uint32_t>(cf) * 8u + static_cast<uint32_t>(lane) * (kPieces ? NC * 8u : 16u);
+  constexpr uint32_t kPieceStride = kPieces ? 16u : 1024u;
   auto dma = [&](int s, int slot) {
     if constexpr (kDma) {
       char* dst = ring + slot * kRow;
       const uint32_t o = dbase + static_cast<uint32_t>(s) * rstep;
       if constexpr (SLIDE) {
         constexpr uint32_t q = J;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + q * 1024u, 16, loff + q * 1024u + o, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + q * 1024u, 16, loff + q * kPieceStride + o, 0, 0, 0);
       } else {
         static_for<0, C::NDMA>([&](auto Q) {
           constexpr uint32_t q = decltype(Q)::value;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + q * 1024u, 16, loff + q * 1024u + o, 0, 0, 0);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + q * 1024u, 16, loff + q * kPieceStride + o, 0, 0, 0);
         });
       }
     }
