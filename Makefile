@@ -148,7 +148,10 @@ asan-host:
 
 # tuning harnesses (standalone, not part of the libraries): stream_sweep, and
 # variant_bench — the A/B kernel variants checked and timed against libgmt
-sweep: $(BUILD)/bench/stream_sweep $(BUILD)/bench/variant_bench $(BUILD)/bench/d1_walk
+sweep: $(BUILD)/bench/stream_sweep $(BUILD)/bench/variant_bench $(BUILD)/bench/d1_walk $(BUILD)/bench/sdma_probe
+$(BUILD)/bench/sdma_probe: csrc/bench/sdma_probe.hip
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 $(BUILD)/bench/stream_sweep: csrc/bench/stream_sweep.hip
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<

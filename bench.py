@@ -105,11 +105,12 @@ def plan_str(plan):
 
 
 def bench_native(env, shape, steps, warmup, overlap, dims, graph, tblock, wg_waves, seg_rows, init="random",
-                 seed=0, calibrate=True):
+                 seed=0, calibrate=True, transport="auto"):
     from gpu_mpi_tests_amd.engine import NativeJacobi
 
     eng = NativeJacobi(shape[0], shape[1], env, dims=dims, overlap=overlap, graph=graph, tblock=tblock,
-                       wg_waves=wg_waves, seg_rows=seg_rows, init=init, seed=seed, calibrate=calibrate)
+                       wg_waves=wg_waves, seg_rows=seg_rows, init=init, seed=seed, calibrate=calibrate,
+                       transport=transport)
     # calibration (one timed pass of every pass size on this share, max over
     # ranks) -> the plan; then one launch of every pass type of the timed
     # plan; the initial field is restored
@@ -123,7 +124,7 @@ def bench_native(env, shape, steps, warmup, overlap, dims, graph, tblock, wg_wav
     return eng, dt, info
 
 
-def check_engine(env, dims, tsteps, graph, init="analytic", seed=0):
+def check_engine(env, dims, tsteps, graph, init="analytic", seed=0, transport="auto"):
     """Distributed-correctness gate (reference: mpi_stencil2d_gt.cc:555-570
     err_norm): the engine with this job's process grid and sweeps per pass on
     a small Dirichlet domain, overlap on and off, vs the serial NumPy
@@ -143,7 +144,7 @@ def check_engine(env, dims, tsteps, graph, init="analytic", seed=0):
     worst = 0.0
     for ov in (True, False):
         e = NativeJacobi(ny, nx, env, dims=dims, overlap=ov, graph=graph, tblock=k if k > 1 else False,
-                         init=init, seed=seed)
+                         init=init, seed=seed, transport=transport)
         e.run(steps)
         e.synchronize()
         part = (e.off_y, e.off_x, e.interior())
@@ -211,7 +212,7 @@ def self_halo_latency(env, shape, tsteps, iters):
         eng.close()
 
 
-def ref_halo(env, n_local, n_other, iters):
+def ref_halo(env, n_local, n_other, iters, transport="auto"):
     """The reference's own headline measurement (mpi_stencil2d_gt test_deriv /
     test_sum: 2-deep ghost faces of n_other doubles — 8 MiB at the defaults —
     exchanged between 1-D slab neighbours, dim 0 packed, dim 1 in place, the
@@ -220,7 +221,7 @@ def ref_halo(env, n_local, n_other, iters):
     median, max over ranks."""
     from gpu_mpi_tests_amd.engine import deriv_bench
 
-    r = deriv_bench(n_local, n_other, n_iter=iters, n_warmup=5, env=env, check=True)
+    r = deriv_bench(n_local, n_other, n_iter=iters, n_warmup=5, env=env, check=True, transport=transport)
     out = {"ref_halo_config": f"mpi_stencil2d_gt {n_local}x{n_other} per rank, 1-D slabs, "
                               f"{iters} exchanges, {r['transport']}"}
     for d in (0, 1):
@@ -265,7 +266,7 @@ def bench_daxpy(env, n, iters):
     return 24.0 * n / dt / 1e9 * env.world_size, dt
 
 
-def daxpy_allreduce(env, n, iters):
+def daxpy_allreduce(env, n, iters, transport="auto"):
     """BASELINE config "mpi_daxpy N ranks x 1 GPU, RCCL allreduce of partial
     sums": the reference's distributed DAXPY check (mpi_daxpy_nvtx.cc:207-310)
     with its closed form — x = (i+1)/n, y = -x, y <- 2x + y = x, so each rank's
@@ -281,7 +282,7 @@ def daxpy_allreduce(env, n, iters):
     ops.fill_poly(x, 3, 1.0 / n, 1.0 / n, 0.0, 0.0)  # x[i] = (i+1)/n
     y = -x
     ops.daxpy(2.0, x, y)
-    comm = Comm(env)
+    comm = Comm(env, transport)
     part = torch.empty(1, dtype=torch.float64, device=dev)
     t_sum, t_red = [], []
     try:
@@ -311,6 +312,145 @@ def daxpy_allreduce(env, n, iters):
             "daxpy_partial_sum_us": round(gdist.allreduce_max(float(np.median(t_sum)), env) * 1e6, 2),
             "daxpy_allreduce_us": round(gdist.allreduce_max(float(np.median(t_red)), env) * 1e6, 2),
             "daxpy_allreduce_kind": kind}
+
+
+PROBE_KINDS = ("rccl", "ipc")
+
+
+def _env_transport():
+    """The engine transport an environment variable forces, or ''."""
+    eng = os.environ.get("GMT_ENGINE_TRANSPORT", "").strip().lower()
+    app = os.environ.get("GMT_TRANSPORT", "").strip().lower()
+    return eng if eng not in ("", "auto") else (app if app in PROBE_KINDS else "")
+
+
+def probe_kinds(args):
+    """Data planes to time at start-up (before this process touches the GPU).
+    auto: N > 1 with every rank on its own GPU, where both RCCL and IPC (peer
+    mappings over xGMI) can carry the halo; on: also on the CPU backend (its
+    socket / memfd emulations) or with ranks sharing a GPU (IPC only)."""
+    world = int(os.environ.get("WORLD_SIZE", "1") or 1)
+    if world < 2 or args.transport != "auto" or args.transport_probe == "off" or _env_transport():
+        return []
+    lw = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)) or world)
+    ndev = 0 if args.device == "cpu" else torch.cuda.device_count()  # counting does not initialise the GPU
+    if args.transport_probe == "on":
+        return list(PROBE_KINDS) if ndev == 0 or lw <= ndev else ["ipc"]
+    return list(PROBE_KINDS) if 0 < ndev and lw <= ndev else []
+
+
+def run_probe(args, argv, kinds):
+    """Time every candidate data plane in a CHILD process group (this process
+    has not initialised the GPU yet): a candidate that faults, hangs or fails
+    the bitwise gate takes only the child down and is dropped, never the job.
+    The children rendezvous on their own port and are killed as a process
+    group at --probe-timeout.  Returns this rank's candidates (plus the
+    child's exit status and wall time)."""
+    import signal
+    import subprocess
+    import tempfile
+
+    rank = int(os.environ.get("RANK", "0") or 0)
+    port = int(os.environ.get("MASTER_PORT", "29500") or 29500)
+    cenv = dict(os.environ, MASTER_PORT=str(args.probe_port or (port + 101 if port + 101 < 65536 else port - 101)),
+                GMT_TIMEOUT=str(min(90.0, args.probe_timeout)))
+    # torchrun's agent hosts the store on MASTER_PORT only: the children host their own
+    cenv.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+    fd, path = tempfile.mkstemp(prefix=f"gmt_probe_r{rank}_", suffix=".json")
+    os.close(fd)
+    cmd = [sys.executable, os.path.abspath(__file__), *argv, "--probe-child", path, "--probe-kinds", ",".join(kinds)]
+    t0 = time.perf_counter()
+    p = subprocess.Popen(cmd, stdout=sys.stderr, start_new_session=True, env=cenv)
+    try:
+        rc = p.wait(timeout=args.probe_timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)  # the child's own session: exactly the process group started here
+        p.wait()
+        rc = "timeout"
+    res = {}
+    try:  # written after every candidate: what finished before a crash counts
+        with open(path) as f:
+            txt = f.read()
+        res = json.loads(txt) if txt else {}
+    except (OSError, ValueError) as ex:
+        rc = f"{rc}, unreadable result: {ex}"
+    finally:
+        os.unlink(path)
+    res["_rc"] = rc
+    res["_s"] = round(time.perf_counter() - t0, 2)
+    return res
+
+
+def probe_child(args, dims, shape, tsteps, graph):
+    """--probe-child: every candidate's bitwise gate on this process grid,
+    then its blocking K-wide exchange of the headline field (mean
+    over --probe-iters, max over ranks), written as JSON to the given path
+    after each candidate.  Fault injection: GMT_PROBE_CRASH=R:KIND makes rank
+    R's child die (status 139, as on a GPU memory fault) when it reaches KIND."""
+    from gpu_mpi_tests_amd.engine import NativeJacobi
+
+    env = gdist.init(device=args.device)
+    crash = os.environ.get("GMT_PROBE_CRASH", "").split(":")
+    out = {}
+    for t in args.probe_kinds.split(","):
+        mark(env, f"transport probe: {t}")
+        if len(crash) == 2 and crash[0] == str(env.rank) and crash[1] == t:
+            print(f"GMT FAULT INJECTION: rank {env.rank} transport probe child dies at {t}", file=sys.stderr,
+                  flush=True)
+            os._exit(139)
+        rec = {}
+        try:
+            rec["gate_max_diff"] = check_engine(env, dims, tsteps, graph, "analytic", 0, transport=t)
+            if rec["gate_max_diff"] == 0.0:
+                eng = NativeJacobi(shape[0], shape[1], env, dims=dims, overlap=False, graph=False,
+                                   tblock=tsteps if tsteps > 1 else False, transport=t, calibrate=False)
+                try:
+                    rec["exchange_us"] = round(halo_latency(env, eng, args.probe_iters) * 1e6, 2)
+                    rec["label"] = eng.transport
+                finally:
+                    eng.close()
+        except Exception as ex:  # a failing candidate is data, not a crash
+            rec["error"] = f"{type(ex).__name__}: {ex}"[:300]
+        out[t] = rec
+        with open(args.probe_child, "w") as f:
+            json.dump(out, f)
+    gdist.shutdown()
+
+
+def agree_transport(env, probe, kinds, margin=0.97):
+    """Every rank's probe -> one choice for all: a candidate counts if it
+    passed the gate and timed on EVERY rank; its exchange time is the max over
+    ranks; IPC replaces RCCL only when it is faster by more than 3%.
+    Returns (transport, {kind: record}, probe wall seconds)."""
+    allp = [None] * env.world_size
+    torch.distributed.all_gather_object(allp, probe, group=env.host_group)
+    cands = {}
+    for t in kinds:
+        recs = [(p.get(t) or {}) for p in allp]
+        ok = all(r.get("gate_max_diff") == 0.0 and r.get("exchange_us") for r in recs)
+        c = {"gate": "pass" if ok else "fail"}
+        if ok:
+            c["exchange_us"] = max(r["exchange_us"] for r in recs)
+            c["label"] = recs[0].get("label", t)
+        else:
+            whys = []
+            for i, (p, r) in enumerate(zip(allp, recs)):
+                why = [f"probe exit {p.get('_rc')}"] if p.get("_rc") != 0 else []
+                if r.get("error"):
+                    why.append(r["error"])
+                elif r.get("gate_max_diff"):
+                    why.append(f"gate max diff {r['gate_max_diff']}")
+                if why:
+                    whys.append(f"rank {i}: {', '.join(why)}")
+            c["error"] = "; ".join(whys[:4])[:600]
+        cands[t] = c
+    passing = {t: c["exchange_us"] for t, c in cands.items() if c["gate"] == "pass"}
+    choice = "auto"
+    if passing:
+        choice = min(passing, key=passing.get)
+        if choice != "rccl" and "rccl" in passing and passing[choice] > margin * passing["rccl"]:
+            choice = "rccl"
+    return choice, cands, max(float(p.get("_s", 0.0)) for p in allp)
 
 
 def main(argv=None):
@@ -359,10 +499,24 @@ def main(argv=None):
     ap.add_argument("--timeout", type=float, default=300.0,
                     help="hang watchdog: seconds without progress before the job fails naming the rank and "
                          "phase (GMT_TIMEOUT overrides; 0 = off)")
+    ap.add_argument("--transport", choices=("auto",) + PROBE_KINDS, default="auto",
+                    help="engine data plane at N > 1 (auto: timed at start-up, see --transport-probe)")
+    ap.add_argument("--transport-probe", choices=("auto", "on", "off"), default="auto",
+                    help="auto: with one rank per GPU, time RCCL and IPC (xGMI peer mappings) on the real "
+                         "faces in an isolated child process group and keep the faster that passes the "
+                         "bitwise gate; on: also on the CPU backend; off: RCCL")
+    ap.add_argument("--probe-timeout", type=float, default=240.0, help="seconds for the transport probe")
+    ap.add_argument("--probe-iters", type=int, default=50, help="timed exchanges per probed transport")
+    ap.add_argument("--probe-port", type=int, default=0, help="the probe's rendezvous port (0: MASTER_PORT+101)")
+    ap.add_argument("--probe-child", type=str, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--probe-kinds", type=str, default="", help=argparse.SUPPRESS)
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = ap.parse_args(argv)
     # read by the engine library when its first entry point arms the watchdog
     os.environ.setdefault("GMT_TIMEOUT", str(args.timeout))
 
+    kinds = [] if args.probe_child else probe_kinds(args)
+    probe = run_probe(args, argv, kinds) if kinds else None
     env = gdist.init(device=args.device)
     if args.gpus != env.world_size and env.rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
@@ -377,10 +531,19 @@ def main(argv=None):
         shape = (args.size, args.size)
     graph = args.graph == "on"
     tsteps = (args.tsteps or DEFAULT_TSTEPS) if args.tblock == "on" else 1
+    if args.probe_child:
+        probe_child(args, dims or gdims, shape, tsteps, graph)
+        return
     extras = {}
+    transport = args.transport
+    if kinds:
+        mark(env, "transport choice")
+        transport, cands, probe_s = agree_transport(env, probe, kinds)
+        extras["transport_candidates"] = cands
+        extras["transport_probe_s"] = probe_s
     if not args.skip_check:
         mark(env, "correctness gate")
-        diff = check_engine(env, dims or gdims, tsteps, graph, args.init, args.seed)
+        diff = check_engine(env, dims or gdims, tsteps, graph, args.init, args.seed, transport)
         extras["check_max_diff"] = diff
         extras.update(peer_status(env, dims or gdims))
         if diff != 0.0:
@@ -392,7 +555,7 @@ def main(argv=None):
     mark(env, "headline stencil run")
     solver, dt, info = bench_native(env, shape, args.steps, args.warmup, overlap, dims, graph,
                                     tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows,
-                                    args.init, args.seed, not args.no_calibrate)
+                                    args.init, args.seed, not args.no_calibrate, transport)
     points = shape[0] * shape[1]
     mlups = points * args.steps / dt / 1e6
     ms_per_step = dt / args.steps * 1e3
@@ -422,7 +585,7 @@ def main(argv=None):
             mark(env, "swapped process grid run")
             eng3, dt3, info3 = bench_native(env, shape, args.steps, args.warmup, overlap, (hx, hp), graph,
                                             tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows,
-                                            args.init, args.seed, not args.no_calibrate)
+                                            args.init, args.seed, not args.no_calibrate, transport)
             eng3.close()
             extras["stencil_alt_dims"] = f"{hx}x{hp}"
             extras["stencil_alt_dims_MLUPS"] = round(points * args.steps / dt3 / 1e6, 1)
@@ -435,14 +598,14 @@ def main(argv=None):
             steps2 = max(100, 4 * args.steps)
             eng2, dt2, info2 = bench_native(env, s2, steps2, max(args.warmup, 10), overlap, dims, graph,
                                             tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows,
-                                            args.init, args.seed, not args.no_calibrate)
+                                            args.init, args.seed, not args.no_calibrate, transport)
             eng2.close()
             extras[f"stencil_{args.small_size}_MLUPS"] = round(s2[0] * s2[1] * steps2 / dt2 / 1e6, 1)
             extras[f"stencil_{args.small_size}_ms_per_step"] = round(dt2 / steps2 * 1e3, 5)
             extras[f"stencil_{args.small_size}_pass_plan"] = f"{steps2} steps: {info2['pass_plan']}"
         if env.world_size > 1:
             mark(env, "reference halo benchmark")
-            extras.update(ref_halo(env, args.ref_n_local, args.ref_n_other, args.ref_iters))
+            extras.update(ref_halo(env, args.ref_n_local, args.ref_n_other, args.ref_iters, transport))
             if extras["ref_halo_dim0_bad_ghosts"] or extras["ref_halo_dim1_bad_ghosts"]:
                 if env.rank == 0:
                     print("bench.py: the reference halo benchmark found wrong ghost cells after an exchange "
@@ -457,7 +620,7 @@ def main(argv=None):
         extras["daxpy_n"] = args.daxpy_n
         extras["daxpy_ms"] = round(ddt * 1e3, 4)
         mark(env, "daxpy all-reduce")
-        extras.update(daxpy_allreduce(env, args.daxpy_n, iters=20))
+        extras.update(daxpy_allreduce(env, args.daxpy_n, iters=20, transport=transport))
         if not extras["daxpy_allsum_rel_err"] <= 1e-9:
             if env.rank == 0:
                 print(f"bench.py: DAXPY ALLSUM {extras['daxpy_allsum']} differs from the closed form "

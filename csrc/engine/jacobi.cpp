@@ -116,6 +116,7 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
     Span2D<double> f(buf_[b].data() + (xo_ - g_), nx_ + 2 * g_, ny_ + 2 * g_, ld_);
     halo_[b] = std::make_unique<Halo2D>(t_, f, g_, g_, nb_, false, GMT_SPACE_DEVICE, ks_ > 1);
   }
+  if (const char* e = std::getenv("GMT_PACK_WGS")) beside_pack_wgs_ = std::max(0, std::atoi(e));
   if (ks_ > 1 && halo_[0]->active() && (c.overlap || c.overlap_auto)) split_cus();
   watchdog_kick("jacobi: halo plans ready");
   if (c.overlap_auto) autotune_overlap();
@@ -424,8 +425,10 @@ void JacobiSolver::enqueue_block(int parity, int K) {
   GMT_CHECK("signal wait", gmt_signal_wait(sig_.data() + 1, sig_.data() + 2,
                                            reinterpret_cast<unsigned*>(sig_.data() + 3), cs_));
   Halo2D& hn = *halo_[parity ^ 1];
+  hn.set_pack_wgs(beside_pack_wgs_);  // beside the pass: few resident pack workgroups
   hn.start(cs_);
   hn.finish(cs_);
+  hn.set_pack_wgs(0);
   GMT_CHECK("event", gmt_rt_event_record(ev_halo_, cs_));
   GMT_CHECK("wait", gmt_rt_stream_wait_event(s_, ev_halo_));
   fresh_[parity ^ 1] = true;

@@ -65,6 +65,10 @@ int gmt_copy2d_batched(int n_desc, const gmt_copy2d_desc* d, int elem_bytes, voi
   return 0;
 }
 
+int gmt_copy2d_batched_wgs(int n_desc, const gmt_copy2d_desc* d, int elem_bytes, int, void* s) {
+  return gmt_copy2d_batched(n_desc, d, elem_bytes, s);
+}
+
 int64_t gmt_sum_axis_workspace(int, int64_t, int64_t) { return 1; }
 
 int gmt_sum_axis(int keep_dim, int64_t nx, int64_t ny, const double* z, int64_t ld, double* out,

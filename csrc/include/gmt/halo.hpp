@@ -165,6 +165,11 @@ class Halo2D {
     return (!ex_ || ex_->graph_capturable()) && (!ex_x_ || ex_x_->graph_capturable());
   }
   size_t bytes_sent() const { return bytes_; }
+  // pack/unpack launches of the exchanges enqueued from now on: at most n
+  // workgroups in a grid-stride loop (0 = the full grid); an exchange that
+  // runs beside a pass holding nearly every CU slot gets few resident
+  // workgroups instead of hundreds that trickle through the free slots
+  void set_pack_wgs(int n) { pack_wgs_ = n; }
   size_t messages() const { return nmsg_; }
 
   // packed: optional event recorded once the send buffers are packed, just
@@ -243,7 +248,7 @@ class Halo2D {
     for (auto& fc : xfaces_)
       d[n++] = {fc.send.data, fc.sbuf.data(), static_cast<int64_t>(fc.send.ld),
                 static_cast<int64_t>(gx_), gx_, static_cast<int64_t>(fc.send.ncols)};
-    GMT_CHECK("halo pack", gmt_copy2d_batched(n, d, sizeof(double), s));
+    GMT_CHECK("halo pack", gmt_copy2d_batched_wgs(n, d, sizeof(double), pack_wgs_, s));
   }
   void unpack_x_faces(gmt_stream_t s) {
     if (xfaces_.empty() || blocks_) return;  // blocks: the transport wrote the ghosts in place
@@ -252,7 +257,7 @@ class Halo2D {
     for (auto& fc : xfaces_)
       d[n++] = {fc.rbuf.data(), fc.recv.data, static_cast<int64_t>(gx_),
                 static_cast<int64_t>(fc.recv.ld), gx_, static_cast<int64_t>(fc.recv.ncols)};
-    GMT_CHECK("halo unpack", gmt_copy2d_batched(n, d, sizeof(double), s));
+    GMT_CHECK("halo unpack", gmt_copy2d_batched_wgs(n, d, sizeof(double), pack_wgs_, s));
   }
   void pack_y_faces(gmt_stream_t s) {
     for (auto& fc : yfaces_)
@@ -269,6 +274,7 @@ class Halo2D {
   size_t nx_ = 0, ny_ = 0;
   Neighbors nb_;
   std::vector<Face> xfaces_, yfaces_;
+  int pack_wgs_ = 0;        // set_pack_wgs
   bool blocks_ = false;     // strided faces moved in place by the transport (Transport::takes_blocks)
   bool corners_ = false;    // two-phase corner mode
   bool one_phase_ = false;  // corner blocks to the diagonal neighbours

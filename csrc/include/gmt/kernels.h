@@ -54,6 +54,11 @@ typedef struct gmt_copy2d_desc {
 } gmt_copy2d_desc;
 int gmt_copy2d_batched(int n_desc, const gmt_copy2d_desc* descs, int elem_bytes,
                        void* stream);
+// The same copy by at most max_wgs workgroups in a grid-stride loop (0: one
+// element per thread, the full grid) — for exchanges that run beside a pass
+// holding nearly every CU slot (profiles/r04_overlap.md).
+int gmt_copy2d_batched_wgs(int n_desc, const gmt_copy2d_desc* descs, int elem_bytes, int max_wgs,
+                           void* stream);
 
 /* ---- K9: axis sums of a 2-D field of nx x ny (row pitch ld).
  *      keep_dim == 0: out[x] = sum_y z[y][x]   (length nx)

@@ -17,6 +17,9 @@
 //    per row, so one lane = one row, one dwordx4 load + one dwordx4 store);
 //  * otherwise element-wise (e.g. the 1-double-wide W/E faces of the Jacobi
 //    decomposition).
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.hpp"
 #include "gmt/kernels.h"
 
@@ -62,10 +65,50 @@ __global__ __launch_bounds__(kBlock) void copy2d_batched_kernel(Copy2dBatch b) {
   *d = *s;
 }
 
+// The same copy as a grid-stride loop over few workgroups (max_wgs > 0):
+// beside a pass that holds nearly every CU slot, a launch of hundreds of
+// short workgroups trickles through the few free slots one dispatch at a
+// time (profiles/r04_overlap.md); a few resident workgroups, each with four
+// 16-B loads in flight per lane, move the same faces without waiting for
+// slots to free.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void copy2d_stride_kernel(Copy2dBatch b, int64_t total_all) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  int k = 0;
+  auto at = [&](int64_t e, int& kk) -> int64_t {  // descriptor of element e (e only grows) and its offset
+    while (kk + 1 < b.n && e >= b.block_start[kk + 1]) ++kk;
+    return e - b.block_start[kk];
+  };
+  for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e0 < total_all; e0 += 4 * stride) {
+    T v[4];
+    T* d[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t e = e0 + u * stride;
+      d[u] = nullptr;
+      if (e < total_all) {
+        const int64_t i = at(e, k);
+        const int64_t w = b.width[k], row = i / w, col = i - row * w;
+        v[u] = *(reinterpret_cast<const T*>(b.src[k]) + row * b.src_ld[k] + col);
+        d[u] = reinterpret_cast<T*>(b.dst[k]) + row * b.dst_ld[k] + col;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (d[u]) *d[u] = v[u];
+    k = 0;  // e0 + 0 * stride of the next iteration may sit in an earlier descriptor than e0 + 3 * stride
+  }
+}
+
 }  // namespace gmt
 
 extern "C" int gmt_copy2d_batched(int n_desc, const gmt_copy2d_desc* descs, int elem_bytes,
                                   void* stream) {
+  return gmt_copy2d_batched_wgs(n_desc, descs, elem_bytes, 0, stream);
+}
+
+extern "C" int gmt_copy2d_batched_wgs(int n_desc, const gmt_copy2d_desc* descs, int elem_bytes, int max_wgs,
+                                      void* stream) {
   using namespace gmt;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (n_desc < 0 || n_desc > GMT_MAX_COPY2D) return static_cast<int>(hipErrorInvalidValue);
@@ -103,6 +146,23 @@ extern "C" int gmt_copy2d_batched(int n_desc, const gmt_copy2d_desc* descs, int 
   }
   if (b.n == 0) return 0;
   for (int k = b.n + 1; k <= GMT_MAX_COPY2D; ++k) b.block_start[k] = b.block_start[b.n];
+  const int cap = max_wgs;
+  if (cap > 0) {
+    // element offsets instead of block offsets
+    int64_t acc = 0;
+    for (int k = 0; k < b.n; ++k) {
+      b.block_start[k] = acc;
+      acc += b.width[k] * b.height[k];
+    }
+    for (int k = b.n; k <= GMT_MAX_COPY2D; ++k) b.block_start[k] = acc;
+    const unsigned nb = static_cast<unsigned>(std::min<int64_t>(cap, (acc + kBlock - 1) / kBlock));
+    switch (unit) {
+      case 16: copy2d_stride_kernel<d2><<<nb, kBlock, 0, s>>>(b, acc); break;
+      case 8: copy2d_stride_kernel<double><<<nb, kBlock, 0, s>>>(b, acc); break;
+      default: copy2d_stride_kernel<float><<<nb, kBlock, 0, s>>>(b, acc); break;
+    }
+    GMT_RET_LAUNCH();
+  }
   const unsigned nb = grid_1d(b.block_start[b.n]);
   switch (unit) {
     case 16: copy2d_batched_kernel<d2><<<nb, kBlock, 0, s>>>(b); break;

@@ -76,6 +76,7 @@ _SIGS = {
     "gmt_stencil5_1d": (c_int, [c_i64, c_vp, c_dbl, c_vp, c_vp, c_vp]),
     "gmt_stencil5_2d": (c_int, [c_int, c_i64, c_i64, c_vp, c_dbl, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "gmt_copy2d_batched": (c_int, [c_int, c_vp, c_int, c_vp]),
+    "gmt_copy2d_batched_wgs": (c_int, [c_int, c_vp, c_int, c_int, c_vp]),
     "gmt_sum_axis_workspace": (c_i64, [c_int, c_i64, c_i64]),
     "gmt_sum_axis": (c_int, [c_int, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "gmt_diff_sq_workspace": (c_i64, [c_i64, c_i64]),

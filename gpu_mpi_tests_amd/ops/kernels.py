@@ -107,8 +107,10 @@ def stencil5_2d(inp: torch.Tensor, dim: int, out: torch.Tensor | None = None,
 
 
 # ------------------------------------------------------- halo pack / unpack
-def copy2d_batched(pairs: Sequence[tuple[torch.Tensor, torch.Tensor]]) -> None:
-    """Copy each ``src`` 2-D view into ``dst`` (same shape) in ONE launch.  K6/K7/K8."""
+def copy2d_batched(pairs: Sequence[tuple[torch.Tensor, torch.Tensor]], max_wgs: int = 0) -> None:
+    """Copy each ``src`` 2-D view into ``dst`` (same shape) in ONE launch.  K6/K7/K8.
+    max_wgs > 0: at most that many workgroups in a grid-stride loop (the
+    exchange a band-first pass hides, Halo2D::set_pack_wgs)."""
     pairs = [(s, d) for s, d in pairs if s.numel() > 0]
     if not pairs:
         return
@@ -139,8 +141,8 @@ def copy2d_batched(pairs: Sequence[tuple[torch.Tensor, torch.Tensor]]) -> None:
             arr[k].dst_ld = d.stride(0)
             arr[k].width = s.shape[1]
             arr[k].height = s.shape[0]
-        _native.check(L.gmt_copy2d_batched(len(chunk), ctypes.cast(arr, ctypes.c_void_p), elem,
-                                           stream), "gmt_copy2d_batched")
+        _native.check(L.gmt_copy2d_batched_wgs(len(chunk), ctypes.cast(arr, ctypes.c_void_p), elem,
+                                               int(max_wgs), stream), "gmt_copy2d_batched_wgs")
 
 
 # ---------------------------------------------------------------- reductions

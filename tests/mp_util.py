@@ -15,6 +15,39 @@ import traceback
 import torch.multiprocessing as mp
 
 
+def _plain(v):
+    """Tensors -> NumPy copies.  torch.multiprocessing pickles a tensor as a
+    shared-memory handle the receiver fetches from the SENDER's fd server: a
+    rank that exits right after posting leaves the parent an EOFError (the
+    round-3 '-n 8' failure), so results travel by value."""
+    import torch
+
+    if isinstance(v, torch.Tensor):
+        return _ByValue(v.detach().cpu().numpy().copy())
+    if isinstance(v, (list, tuple)):
+        return type(v)(_plain(x) for x in v)
+    if isinstance(v, dict):
+        return {k: _plain(x) for k, x in v.items()}
+    return v
+
+
+class _ByValue:
+    def __init__(self, a):
+        self.a = a
+
+
+def _restore(v):
+    import torch
+
+    if isinstance(v, _ByValue):
+        return torch.from_numpy(v.a)
+    if isinstance(v, (list, tuple)):
+        return type(v)(_restore(x) for x in v)
+    if isinstance(v, dict):
+        return {k: _restore(x) for k, x in v.items()}
+    return v
+
+
 def _entry(rank, world, port, fn, args, q, errpath):
     # this rank's stderr (Python and native) goes to its own file
     fd = os.open(errpath, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
@@ -28,7 +61,7 @@ def _entry(rank, world, port, fn, args, q, errpath):
     try:
         env = gdist.init(device="cpu")
         res = fn(env, *args)
-        q.put((rank, "ok", res))
+        q.put((rank, "ok", _plain(res)))
     except Exception:
         q.put((rank, "err", traceback.format_exc()))
     finally:
@@ -92,7 +125,7 @@ def run_dist(fn, world, port, *args, timeout=240):
                                      f"{dead[0][0] if dead else 0}:\n{_tail(errs[dead[0][0] if dead else 0])}") from None
             if status != "ok":
                 raise AssertionError(f"rank {rank} failed:\n{val}\nits stderr:\n{_tail(errs[rank])}")
-            out[rank] = val
+            out[rank] = _restore(val)
     finally:
         for p in procs:
             p.join(timeout=30)

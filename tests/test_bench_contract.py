@@ -186,3 +186,40 @@ def test_rccl_init_timeout_names_the_rank_cpu():
     assert "returned" not in p.stdout
     assert "rank 0 of 2" in p.stderr and "RCCL communicator init failed" in p.stderr, p.stderr
     assert "never" in p.stderr, p.stderr
+
+
+def test_bench_transport_probe_cpu():
+    """The start-up data-plane choice (bench.py --transport-probe; on the GPU
+    it runs by default at one rank per GPU): an isolated child process group
+    gates and times both transports (the CPU backend's RCCL socket and IPC
+    memfd emulations); every candidate's exchange time is in the line and the
+    job runs on the faster one."""
+    port, pport = str(free_port()), str(free_port())
+    rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
+                "--device", "cpu", "--size", "192", "--steps", "3", "--warmup", "1", "--skip-extras",
+                "--transport-probe", "on", "--probe-port", pport, "--probe-iters", "5"])
+    cands = rec["transport_candidates"]
+    assert set(cands) == {"rccl", "ipc"}, cands
+    for c in cands.values():
+        assert c["gate"] == "pass" and c["exchange_us"] > 0, cands
+    best = min(cands, key=lambda t: cands[t]["exchange_us"])
+    chosen = rec["config"]["transport"].replace("-host", "")
+    assert chosen == best or (chosen == "rccl" and cands["ipc"]["exchange_us"] > 0.97 * cands["rccl"]["exchange_us"])
+    assert rec["check_max_diff"] == 0.0 and rec["transport_probe_s"] > 0
+
+
+def test_bench_transport_probe_drops_a_crashing_candidate_cpu():
+    """A candidate whose probe dies (rank 1's child exits 139 at the IPC
+    candidate, as a GPU memory fault would end it) is dropped: the job itself
+    is untouched, runs on RCCL, and the line names the failure."""
+    port, pport = str(free_port()), str(free_port())
+    rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
+                "--device", "cpu", "--size", "192", "--steps", "3", "--warmup", "1", "--skip-extras",
+                "--transport-probe", "on", "--probe-port", pport, "--probe-iters", "5", "--probe-timeout", "20"],
+               GMT_PROBE_CRASH="1:ipc")
+    cands = rec["transport_candidates"]
+    assert cands["rccl"]["gate"] == "pass" and cands["rccl"]["exchange_us"] > 0, cands
+    assert cands["ipc"]["gate"] == "fail" and "probe exit" in cands["ipc"]["error"], cands
+    assert rec["config"]["transport"] == "rccl-host" and rec["check_max_diff"] == 0.0

@@ -131,6 +131,23 @@ def test_copy2d_batched(elem):
     assert torch.equal(dst[:, 2:4], src[:, 2:4]) and torch.equal(dst[10:13], src[10:13])
 
 
+@pytest.mark.parametrize("max_wgs", [1, 3, 128])
+@pytest.mark.parametrize("elem", [torch.float64, torch.float32])
+def test_copy2d_batched_few_workgroups(elem, max_wgs):
+    """The grid-stride form (few resident workgroups, 4 loads in flight per
+    lane) moves exactly what the full-grid form moves: faces of every width
+    class, a descriptor boundary inside one lane's 4-element batch."""
+    src = torch.arange(300 * 70, dtype=elem, device=DEV).view(300, 70)
+    views = [src[:, 2:22], src[:, 69:70], src[10:13, :], src[1:280, 3:36], src[5:6, 0:70]]
+    bufs = [torch.full(v.shape, -1, dtype=elem, device=DEV) for v in views]
+    ops.copy2d_batched(list(zip(views, bufs)), max_wgs=max_wgs)
+    for v, b in zip(views, bufs):
+        assert torch.equal(v, b)
+    dst = torch.zeros_like(src)
+    ops.copy2d_batched([(bufs[0], dst[:, 2:22]), (bufs[3], dst[1:280, 3:36])], max_wgs=max_wgs)
+    assert torch.equal(dst[:, 2:22], src[:, 2:22]) and torch.equal(dst[1:280, 3:36], src[1:280, 3:36])
+
+
 def test_copy2d_many_descriptors():
     src = _rand(64, 64, seed=8)
     pairs = [(src[i : i + 1, :], torch.empty(1, 64, dtype=torch.float64, device=DEV)) for i in range(11)]
