@@ -353,7 +353,7 @@ def run_probe(args, argv, kinds):
     rank = int(os.environ.get("RANK", "0") or 0)
     port = int(os.environ.get("MASTER_PORT", "29500") or 29500)
     cenv = dict(os.environ, MASTER_PORT=str(args.probe_port or (port + 101 if port + 101 < 65536 else port - 101)),
-                GMT_TIMEOUT=str(min(90.0, args.probe_timeout)))
+                GMT_TIMEOUT=str(min(60.0, args.probe_timeout)))
     # torchrun's agent hosts the store on MASTER_PORT only: the children host their own
     cenv.pop("TORCHELASTIC_USE_AGENT_STORE", None)
     fd, path = tempfile.mkstemp(prefix=f"gmt_probe_r{rank}_", suffix=".json")
@@ -505,7 +505,7 @@ def main(argv=None):
                     help="auto: with one rank per GPU, time RCCL and IPC (xGMI peer mappings) on the real "
                          "faces in an isolated child process group and keep the faster that passes the "
                          "bitwise gate; on: also on the CPU backend; off: RCCL")
-    ap.add_argument("--probe-timeout", type=float, default=240.0, help="seconds for the transport probe")
+    ap.add_argument("--probe-timeout", type=float, default=150.0, help="seconds for the transport probe")
     ap.add_argument("--probe-iters", type=int, default=50, help="timed exchanges per probed transport")
     ap.add_argument("--probe-port", type=int, default=0, help="the probe's rendezvous port (0: MASTER_PORT+101)")
     ap.add_argument("--probe-child", type=str, default=None, help=argparse.SUPPRESS)

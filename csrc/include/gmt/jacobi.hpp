@@ -167,8 +167,9 @@ class JacobiSolver {
   gmt_stream_t sb_ = nullptr;
   int comm_cus_ = 0;
   // pack/unpack workgroups of the exchange a band-first pass hides
-  // (Halo2D::set_pack_wgs; GMT_PACK_WGS overrides, 0 = full grid)
-  int beside_pack_wgs_ = 128;
+  // (Halo2D::set_pack_wgs): 0 = the full grid; GMT_PACK_WGS=N for A/B (64
+  // and 128 measured no better on the N = 8 shares, profiles/r04_overlap.md)
+  int beside_pack_wgs_ = 0;
   // a band-first pass was enqueued since the last synchronize(): only then
   // do the side streams and the band signal's error word need a look (a
   // D2H read and two stream syncs are ~2% of an N = 8 pass)
