@@ -52,6 +52,13 @@ void engine_watchdog(int rank, const char* phase) {
 // the request is invalid.
 std::unique_ptr<comm::Transport> engine_transport(int rank, int world, int transport, const void* id) {
   if (world < 1 || rank < 0 || rank >= world) return nullptr;
+  // the GPU's socket, once per process, before the first transport allocates
+  static const int numa_node = [] {
+    int dev = -1, node = -1;
+    if (gmt_rt_get_device(&dev) == 0 && dev >= 0) (void)gmt_rt_bind_numa(dev, &node);
+    return node;
+  }();
+  (void)numa_node;
   if (transport == GMT_ENGINE_RCCL) {
     gmt_ccl_id cid;
     std::memcpy(&cid, id, sizeof(cid));

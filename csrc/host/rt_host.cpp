@@ -218,6 +218,10 @@ int gmt_rt_stream_create(gmt_stream_t* s, int) {
   return kOk;
 }
 int gmt_rt_stream_create_cumask(gmt_stream_t* s, int, const uint32_t*) { return gmt_rt_stream_create(s, 0); }
+int gmt_rt_bind_numa(int, int* node) {
+  *node = -1;
+  return kOk;
+}
 int gmt_rt_device_cu_count(int* n) {
   *n = 1;
   return kOk;

@@ -26,6 +26,7 @@ struct RankBinding {
   int local_rank = 0, local_size = 1;
   int device = 0, n_devices = 1, ranks_per_device = 1;
   size_t mem_per_rank = 0;
+  int numa_node = -1;  // CPUs bound to this NUMA node (gmt_rt_bind_numa), -1 = unbound
   gmt_device_info info{};
 };
 
@@ -81,6 +82,8 @@ inline RankBinding set_rank_device(MPI_Comm comm, bool print) {
     std::printf("RANK[%d/%d] => DEVICE[%d/%d] mem=%zd\n", b.rank + 1, b.world_size, b.device + 1,
                 b.n_devices, b.mem_per_rank);
   GMT_CHECK("set device", gmt_rt_set_device(b.device));
+  // the GPU's socket: before any transport allocates its staging buffers
+  GMT_CHECK("numa bind", gmt_rt_bind_numa(b.device, &b.numa_node));
   watchdog_start(b.rank, b.device);
   watchdog_kick("device bound");
   return b;

@@ -104,6 +104,10 @@ int gmt_rt_stream_create(gmt_stream_t* s, int high_priority);
 int gmt_rt_stream_create_cumask(gmt_stream_t* s, int n_words, const uint32_t* mask);
 /* compute units of the current device */
 int gmt_rt_device_cu_count(int* n);
+/* Bind every thread of the process to the CPUs of device dev's NUMA node
+   (gmt/numa_bind.hpp; opt-in: GMT_NUMA_BIND=1).  *node = the node, or -1
+   when nothing changed (the host backend: always -1). */
+int gmt_rt_bind_numa(int dev, int* node);
 int gmt_rt_stream_destroy(gmt_stream_t s);
 int gmt_rt_stream_synchronize(gmt_stream_t s);
 int gmt_rt_stream_wait_event(gmt_stream_t s, gmt_event_t e);

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 
+#include "gmt/numa_bind.hpp"
 #include "gmt/rt.h"
 
 #define RT_RET(call) return static_cast<int>(call)
@@ -171,6 +172,12 @@ int gmt_rt_stream_create_cumask(gmt_stream_t* s, int n_words, const uint32_t* ma
   hipStream_t h = nullptr;
   const hipError_t e = hipExtStreamCreateWithCUMask(&h, static_cast<uint32_t>(n_words), mask);
   *s = reinterpret_cast<gmt_stream_t>(h);
+  RT_RET(e);
+}
+int gmt_rt_bind_numa(int dev, int* node) {
+  hipDeviceProp_t p;
+  const hipError_t e = hipGetDeviceProperties(&p, dev);
+  *node = e == hipSuccess ? gmt::bind_numa_near(p.pciDomainID, p.pciBusID, p.pciDeviceID) : -1;
   RT_RET(e);
 }
 int gmt_rt_device_cu_count(int* n) {
