@@ -486,6 +486,9 @@ def main(argv=None):
                     help="plan passes from the built-in cost table instead of timing each pass size "
                          "on the real share at start-up")
     ap.add_argument("--daxpy-n", type=int, default=1 << 28)
+    ap.add_argument("--small-steps", type=int, default=0,
+                    help="timed steps of the second stencil domain (0: max(1000, 4 x --steps) on the GPU, "
+                         "max(100, 4 x --steps) on the CPU backend)")
     ap.add_argument("--small-size", type=int, default=8192,
                     help="second stencil domain (BASELINE single-GPU config 8192^2; 0 = skip)")
     ap.add_argument("--skip-extras", action="store_true", help="headline stencil only")
@@ -595,7 +598,10 @@ def main(argv=None):
         if args.small_size:
             mark(env, "small-domain stencil run")
             s2 = (args.small_size, args.small_size)
-            steps2 = max(100, 4 * args.steps)
+            # 1000 sweeps of 8192^2 are 14 ms of GPU work: 100 (1.4 ms) read
+            # 3-4% low, mostly the host round trip and the clock ramp around
+            # so short a timed region (profiles/r04_shares.md)
+            steps2 = args.small_steps or max(1000 if env.is_gpu else 100, 4 * args.steps)
             eng2, dt2, info2 = bench_native(env, s2, steps2, max(args.warmup, 10), overlap, dims, graph,
                                             tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows,
                                             args.init, args.seed, not args.no_calibrate, transport)
