@@ -141,6 +141,11 @@ class IpcExchange : public Exchange {
       const Msg& m = sends_[i];
       gmt_ipc_chan& ch = send[i];
       ch.src = m.buf;
+      if (m.block.base) {  // a halo face read in place: runs of block.rows doubles
+        ch.src = m.block.base;
+        ch.src_run = static_cast<int64_t>(m.block.rows * sizeof(double));
+        ch.src_ld = static_cast<int64_t>(m.block.ld * sizeof(double));
+      }
       ch.dst = stage_[i].data();
       ch.bytes = static_cast<int64_t>(m.bytes);
       ch.src_stride = 0;
@@ -162,6 +167,11 @@ class IpcExchange : public Exchange {
       }
       ch.src_stride = static_cast<int64_t>(m.bytes ? m.bytes : 1);
       ch.dst = m.buf;
+      if (m.block.base) {  // straight into the ghost cells
+        ch.dst = m.block.base;
+        ch.dst_run = static_cast<int64_t>(m.block.rows * sizeof(double));
+        ch.dst_ld = static_cast<int64_t>(m.block.ld * sizeof(double));
+      }
       ch.dst_stride = 0;
       ch.bytes = static_cast<int64_t>(m.bytes);
       ch.wait = flags_.data() + j;  // the sender's slot for this exchange is ready
@@ -224,6 +234,14 @@ class IpcTransport : public Transport {
   }
   Kind kind() const override { return Kind::Ipc; }
   const char* name() const override { return "ipc"; }
+  // halo faces move in place: the sender's exchange kernel gathers a strided
+  // face straight into its staging slot and the receiver's scatters it
+  // straight into the ghost cells (no pack / unpack launches, one pass over
+  // the data fewer on each side); GMT_IPC_BLOCKS=0 packs them, for A/B
+  bool takes_blocks() const override {
+    const char* e = std::getenv("GMT_IPC_BLOCKS");
+    return !(e && e[0] == '0');
+  }
   std::unique_ptr<Exchange> plan(const std::vector<Msg>& r, const std::vector<Msg>& s) override {
     return std::make_unique<IpcExchange>(*ctl_, &cache_, r, s);
   }

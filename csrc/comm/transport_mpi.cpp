@@ -398,6 +398,7 @@ class MpiHostTransport : public MpiTransport {
     const char* e = std::getenv("GMT_HOST_BLOCKS");
     return MpiHostExchange::kernel_staging() && !(e && e[0] == '0');
   }
+  bool orders_block_receives() const override { return true; }
   std::unique_ptr<Exchange> plan(const std::vector<Msg>& r, const std::vector<Msg>& s) override {
     return std::make_unique<MpiHostExchange>(comm_, chunk_, r, s);
   }

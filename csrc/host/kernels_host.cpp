@@ -329,7 +329,8 @@ int gmt_ipc_plan_init(gmt_ipc_plan* p, int n_send, const gmt_ipc_chan* sends, in
   auto* c = static_cast<gmt_ipc_chan*>(p->table);
   for (int k = 0; k < n_send + n_recv; ++k) {
     c[k] = k < n_send ? sends[k] : recvs[k - n_send];
-    if (c[k].bytes < 0) return 1;
+    if (c[k].bytes < 0 || c[k].src_run < 0 || c[k].dst_run < 0) return 1;
+    if (c[k].src_run && c[k].dst_run && c[k].src_run != c[k].dst_run) return 1;
   }
   p->n_send = n_send;
   p->n_recv = n_recv;
@@ -364,8 +365,16 @@ int gmt_ipc_exchange(const gmt_ipc_plan* p, void*) {
           }
         }
       }
-      std::memcpy(static_cast<char*>(c.dst) + (e & 1) * c.dst_stride,
-                  static_cast<const char*>(c.src) + (e & 1) * c.src_stride, static_cast<size_t>(c.bytes));
+      char* d = static_cast<char*>(c.dst) + (e & 1) * c.dst_stride;
+      const char* s = static_cast<const char*>(c.src) + (e & 1) * c.src_stride;
+      if (c.src_run == 0 && c.dst_run == 0) {
+        std::memcpy(d, s, static_cast<size_t>(c.bytes));
+      } else {  // one side strided: run by run (both runs equal the face's width)
+        const int64_t run = c.src_run ? c.src_run : c.dst_run;
+        for (int64_t o = 0, r = 0; o < c.bytes; o += run, ++r)
+          std::memcpy(d + (c.dst_run ? r * c.dst_ld : o), s + (c.src_run ? r * c.src_ld : o),
+                      static_cast<size_t>(std::min<int64_t>(run, c.bytes - o)));
+      }
     }
     for (int k = k0; k < k0 + n; ++k)
       if (chan[k].signal) __atomic_store_n(chan[k].signal, e, __ATOMIC_RELEASE);

@@ -124,7 +124,16 @@ class Halo2D {
       const size_t n = static_cast<size_t>(gy - 1) * f_.ld + f_.nrows;
       double* s = &f_(0, send_col);
       double* r = &f_(0, recv_col);
-      if (pack_y) {
+      if (blocks_ && one_phase_ && !t_.orders_block_receives()) {
+        // the interior rows of the columns only: the corner cells come from
+        // the corner blocks, which this transport may write in any order
+        // with the faces
+        const size_t m = nx_ * static_cast<size_t>(gy);
+        sends.push_back({nullptr, m * sizeof(double), peer, send_tag + kTagY,
+                         {&f_(gx, send_col), nx_, static_cast<size_t>(gy), f_.ld}});
+        recvs.push_back({nullptr, m * sizeof(double), peer, recv_tag + kTagY,
+                         {&f_(gx, recv_col), nx_, static_cast<size_t>(gy), f_.ld}});
+      } else if (pack_y) {
         Face fc;
         fc.sbuf = Buffer<double>(n, buf_space);
         fc.rbuf = Buffer<double>(n, buf_space);

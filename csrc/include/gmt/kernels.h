@@ -225,6 +225,10 @@ typedef struct gmt_ipc_chan {
   int64_t dst_stride;
   const uint64_t* wait;
   uint64_t* signal;
+  /* strided side (a halo face moved in place, Transport::takes_blocks): the
+     message is runs of src_run / dst_run bytes, src_ld / dst_ld bytes apart;
+     run 0 = contiguous.  The staging slot side is always contiguous. */
+  int64_t src_run, src_ld, dst_run, dst_ld;
 } gmt_ipc_chan;
 typedef struct gmt_ipc_plan {
   void* table;         /* device memory of gmt_ipc_table_bytes(n_send + n_recv) bytes */

@@ -110,8 +110,15 @@ class Transport {
   virtual Control* control() { return nullptr; }
   // plans accept messages given as a field Block (buf == nullptr) and move
   // them in place (mpi-host's kernel staging: the face is gathered straight
-  // into page-locked memory and scattered back out of it)
+  // into page-locked memory and scattered back out of it; ipc: the exchange
+  // kernel gathers into / scatters out of its staging slots)
   virtual bool takes_blocks() const { return false; }
+  // a plan writes its Block receives after its flat ones (mpi-host defers
+  // the field scatters): a flat receive may then overlap a Block receive
+  // and the Block wins, as the corner blocks over the y faces' stale corner
+  // cells need.  Without it (ipc: every receive in one kernel, no order)
+  // Halo2D sends y faces as Blocks that leave the corner cells out.
+  virtual bool orders_block_receives() const { return false; }
   int rank() const { return rank_; }
   int size() const { return size_; }
 

@@ -104,20 +104,30 @@ __global__ __launch_bounds__(kBlock) void ipc_exchange_kernel(Args a) {
     char* dst = static_cast<char*>(ch.dst) + (e & 1) * ch.dst_stride;
     const int64_t lo = (c - a.cstart[k]) * kBlockBytes;
     const int64_t hi = lo + kBlockBytes < ch.bytes ? lo + kBlockBytes : ch.bytes;
-    if ((((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) && ((hi - lo) & 15) == 0) {
+    // a strided side maps message byte o to run o / run_bytes at o % run_bytes
+    // (faces are far below 4 GiB: 32-bit division)
+    auto at = [](int64_t o, int64_t run, int64_t ld) -> int64_t {
+      if (run == 0) return o;
+      const uint32_t q = static_cast<uint32_t>(o) / static_cast<uint32_t>(run);
+      return static_cast<int64_t>(q) * ld + (o - static_cast<int64_t>(q) * run);
+    };
+    const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) |
+                         static_cast<uintptr_t>(ch.src_run | ch.src_ld | ch.dst_run | ch.dst_ld);
+    if ((al & 15) == 0 && ((hi - lo) & 15) == 0) {
       d2 v[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t o = lo + 16 * (threadIdx.x + u * kBlock);
-        if (o < hi) v[u] = *reinterpret_cast<const d2*>(src + o);
+        if (o < hi) v[u] = *reinterpret_cast<const d2*>(src + at(o, ch.src_run, ch.src_ld));
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t o = lo + 16 * (threadIdx.x + u * kBlock);
-        if (o < hi) *reinterpret_cast<d2*>(dst + o) = v[u];
+        if (o < hi) *reinterpret_cast<d2*>(dst + at(o, ch.dst_run, ch.dst_ld)) = v[u];
       }
     } else {
-      for (int64_t o = lo + threadIdx.x; o < hi; o += kBlock) dst[o] = src[o];
+      for (int64_t o = lo + threadIdx.x; o < hi; o += kBlock)
+        dst[at(o, ch.dst_run, ch.dst_ld)] = src[at(o, ch.src_run, ch.src_ld)];
     }
   }
   // every wave's copies complete (the barrier waits for them), then ONE
@@ -207,7 +217,12 @@ extern "C" int gmt_ipc_plan_init(gmt_ipc_plan* p, int n_send, const gmt_ipc_chan
   cs[0] = 0;
   for (int k = 0; k < n; ++k) {
     c[k] = k < n_send ? sends[k] : recvs[k - n_send];
-    if (c[k].bytes < 0) {
+    // strided sides: whole runs, a pitch no shorter than the run, offsets
+    // that fit the kernel's 32-bit division
+    auto bad_side = [&](int64_t run, int64_t ld) {
+      return run < 0 || (run > 0 && (ld < run || c[k].bytes % run != 0 || c[k].bytes > 0xffffffffll));
+    };
+    if (c[k].bytes < 0 || bad_side(c[k].src_run, c[k].src_ld) || bad_side(c[k].dst_run, c[k].dst_ld)) {
       std::free(host);
       return static_cast<int>(hipErrorInvalidValue);
     }
