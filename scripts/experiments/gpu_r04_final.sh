@@ -4,7 +4,7 @@
 # first failure.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
-OUT=gpurun_out/r04_final1
+OUT=${OUT:-gpurun_out/r04_final2}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 1000 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/ > $OUT/pytest.log 2>&1 || { tail -60 $OUT/pytest.log; exit 1; }
