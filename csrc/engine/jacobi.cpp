@@ -210,7 +210,7 @@ void JacobiSolver::calibrate_costs() {
     if (K == 1 || gmt_jacobi5tb_supported(K)) ks.push_back(K);
   Buffer<double> d(ks.size(), GMT_SPACE_DEVICE);
   std::vector<double> host(ks.size(), 1e300);
-  constexpr int kPasses = 2, kSweeps = 2;
+  constexpr int kSweeps = 2;
   auto one = [&](int K) {
     if (K == 1) {
       step();
@@ -221,6 +221,15 @@ void JacobiSolver::calibrate_costs() {
   };
   for (int K : ks) one(K);
   synchronize();
+  // enough passes per measurement for ~4 ms of GPU work: on small shares
+  // (8192^2: 0.3 ms a pass) two passes were within the launch and sync
+  // overhead of each other and the plan flipped between 18- and 20-sweep
+  // passes from run to run (profiles/r04_shares.md)
+  double t1 = wtime();
+  one(ks_);
+  synchronize();
+  t1 = (wtime() - t1) * 1e3;
+  const int kPasses = std::max(2, std::min(32, static_cast<int>(std::ceil(4.0 / std::max(t1, 1e-3)))));
   for (int sweep = 0; sweep < kSweeps; ++sweep)
     for (size_t i = 0; i < ks.size(); ++i) {
       const double t0 = wtime();
