@@ -229,6 +229,12 @@ void JacobiSolver::calibrate_costs() {
   one(ks_);
   synchronize();
   t1 = (wtime() - t1) * 1e3;
+  {  // one pass count for every rank: the passes carry the exchanges
+    GMT_CHECK("calib H2D", gmt_rt_memcpy(d.data(), &t1, sizeof(double)));
+    t_.allreduce_max(d.data(), 1, s_);
+    GMT_CHECK("calib D2H", gmt_rt_memcpy_async(&t1, d.data(), sizeof(double), s_));
+    GMT_CHECK("calib sync", gmt_rt_stream_synchronize(s_));
+  }
   const int kPasses = std::max(2, std::min(32, static_cast<int>(std::ceil(4.0 / std::max(t1, 1e-3)))));
   for (int sweep = 0; sweep < kSweeps; ++sweep)
     for (size_t i = 0; i < ks.size(); ++i) {
