@@ -825,6 +825,16 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
     fill(std::min<int64_t>(seg_rows, lmax), &wgs);
     return p;
   }
+  // A/B of the model's choice: GMT_TB_PLAN_L=L plans segments of L rows with
+  // everything else (edges, rule groups, bands) as the model would
+  static const int64_t forced_l = [] {
+    const char* e = std::getenv("GMT_TB_PLAN_L");
+    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(0);
+  }();
+  if (forced_l > 0) {
+    fill(std::min<int64_t>(std::max<int64_t>(forced_l, 64), lmax), &wgs);
+    return p;
+  }
   // The launch's time is its makespan: workgroups start in dispatch order
   // on the first free slot (resident_wgs of them) and run (rows + 2K + lag)
   // steps, rounded up to the unroll, rule-path ones ~1.8x longer per step
