@@ -57,7 +57,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 DEFAULT_TSTEPS = 20  # max fused sweeps per memory pass / halo exchange; the engine plans the mix (profiles/r02_tb.md)
 
 from gpu_mpi_tests_amd import ops  # noqa: E402
-from gpu_mpi_tests_amd.engine import MAX_TSTEPS, watchdog_timeout  # noqa: E402
+from gpu_mpi_tests_amd.engine import MAX_TSTEPS, watchdog_epitaph, watchdog_timeout  # noqa: E402
 from gpu_mpi_tests_amd.parallel import dist as gdist  # noqa: E402
 from gpu_mpi_tests_amd.parallel.decomp import choose_dims  # noqa: E402
 
@@ -212,23 +212,26 @@ def self_halo_latency(env, shape, tsteps, iters):
         eng.close()
 
 
-def ref_halo(env, n_local, n_other, iters, transport="auto"):
+def ref_halo(env, n_local, n_other, iters, transport="auto", check_iters=20):
     """The reference's own headline measurement (mpi_stencil2d_gt test_deriv /
     test_sum: 2-deep ghost faces of n_other doubles — 8 MiB at the defaults —
     exchanged between 1-D slab neighbours, dim 0 packed, dim 1 in place, the
     derivative kernel after each exchange; then the 1024-double all-reduce),
     over this job's transport (RCCL; IPC when ranks share a GPU).  Per-exchange
-    median, max over ranks."""
+    median, max over ranks.  The timed run is the reference's loop as is; a
+    separate untimed run of ``check_iters`` exchanges raises the field before
+    every exchange and checks every ghost cell after it (gmt/deriv.hpp)."""
     from gpu_mpi_tests_amd.engine import deriv_bench
 
-    r = deriv_bench(n_local, n_other, n_iter=iters, n_warmup=5, env=env, check=True, transport=transport)
+    r = deriv_bench(n_local, n_other, n_iter=iters, n_warmup=5, env=env, check=False, transport=transport)
+    rc = deriv_bench(n_local, n_other, n_iter=check_iters, n_warmup=1, env=env, check=True, transport=transport)
     out = {"ref_halo_config": f"mpi_stencil2d_gt {n_local}x{n_other} per rank, 1-D slabs, "
-                              f"{iters} exchanges, {r['transport']}"}
+                              f"{iters} timed exchanges + {check_iters} checked untimed, {r['transport']}"}
     for d in (0, 1):
         out[f"ref_halo_dim{d}_us"] = round(gdist.allreduce_max(r[f"dim{d}"]["median_s"], env) * 1e6, 2)
         out[f"ref_halo_dim{d}_err_norm"] = gdist.allreduce_max(r[f"dim{d}"]["err_norm"], env)
-        # every exchange's ghost rows vs the analytic field (gmt/deriv.hpp check)
-        out[f"ref_halo_dim{d}_bad_ghosts"] = int(gdist.allreduce_max(float(r[f"dim{d}"]["bad_ghosts"]), env))
+        # every checked exchange's ghost rows vs the analytic field
+        out[f"ref_halo_dim{d}_bad_ghosts"] = int(gdist.allreduce_max(float(rc[f"dim{d}"]["bad_ghosts"]), env))
         # scale-free: round-off of x^3 + y^2 at the reference's spacing grows
         # with the extent; a missing or wrong ghost cell gives O(1) and more
         out[f"ref_halo_dim{d}_rel_err"] = gdist.allreduce_max(
@@ -340,43 +343,49 @@ def probe_kinds(args):
 
 
 def run_probe(args, argv, kinds):
-    """Time every candidate data plane in a CHILD process group (this process
-    has not initialised the GPU yet): a candidate that faults, hangs or fails
-    the bitwise gate takes only the child down and is dropped, never the job.
-    The children rendezvous on their own port and are killed as a process
-    group at --probe-timeout.  Returns this rank's candidates (plus the
-    child's exit status and wall time)."""
+    """Time every candidate data plane in a CHILD process group of its own
+    (this process has not initialised the GPU yet): a candidate that faults,
+    hangs or fails the bitwise gate takes only its child down and is
+    dropped, never the job nor the other candidates.  Each candidate's
+    children rendezvous on their own port and are killed as a process group
+    at --probe-timeout.  Returns this rank's candidates (each with its
+    child's exit status) and the probe's wall time."""
     import signal
     import subprocess
     import tempfile
 
     rank = int(os.environ.get("RANK", "0") or 0)
     port = int(os.environ.get("MASTER_PORT", "29500") or 29500)
-    cenv = dict(os.environ, MASTER_PORT=str(args.probe_port or (port + 101 if port + 101 < 65536 else port - 101)),
-                GMT_TIMEOUT=str(min(60.0, args.probe_timeout)))
-    # torchrun's agent hosts the store on MASTER_PORT only: the children host their own
-    cenv.pop("TORCHELASTIC_USE_AGENT_STORE", None)
-    fd, path = tempfile.mkstemp(prefix=f"gmt_probe_r{rank}_", suffix=".json")
-    os.close(fd)
-    cmd = [sys.executable, os.path.abspath(__file__), *argv, "--probe-child", path, "--probe-kinds", ",".join(kinds)]
-    t0 = time.perf_counter()
-    p = subprocess.Popen(cmd, stdout=sys.stderr, start_new_session=True, env=cenv)
-    try:
-        rc = p.wait(timeout=args.probe_timeout)
-    except subprocess.TimeoutExpired:
-        os.killpg(p.pid, signal.SIGKILL)  # the child's own session: exactly the process group started here
-        p.wait()
-        rc = "timeout"
+    base = args.probe_port or (port + 101 if port + 101 + len(kinds) < 65536 else port - 101 - len(kinds))
     res = {}
-    try:  # written after every candidate: what finished before a crash counts
-        with open(path) as f:
-            txt = f.read()
-        res = json.loads(txt) if txt else {}
-    except (OSError, ValueError) as ex:
-        rc = f"{rc}, unreadable result: {ex}"
-    finally:
-        os.unlink(path)
-    res["_rc"] = rc
+    t0 = time.perf_counter()
+    for i, kind in enumerate(kinds):
+        cenv = dict(os.environ, MASTER_PORT=str(base + i), GMT_TIMEOUT=str(min(60.0, args.probe_timeout)))
+        # torchrun's agent hosts the store on MASTER_PORT only: the children host their own
+        cenv.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+        fd, path = tempfile.mkstemp(prefix=f"gmt_probe_r{rank}_{kind}_", suffix=".json")
+        os.close(fd)
+        cmd = [sys.executable, os.path.abspath(__file__), *argv, "--probe-child", path, "--probe-kinds", kind]
+        t1 = time.perf_counter()
+        p = subprocess.Popen(cmd, stdout=sys.stderr, start_new_session=True, env=cenv)
+        try:
+            rc = p.wait(timeout=args.probe_timeout)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)  # the child's own session: exactly the process group started here
+            p.wait()
+            rc = "timeout"
+        rec = {}
+        try:
+            with open(path) as f:
+                txt = f.read()
+            rec = (json.loads(txt) if txt else {}).get(kind, {})
+        except (OSError, ValueError) as ex:
+            rc = f"{rc}, unreadable result: {ex}"
+        finally:
+            os.unlink(path)
+        rec["_rc"] = rc
+        rec["_s"] = round(time.perf_counter() - t1, 2)
+        res[kind] = rec
     res["_s"] = round(time.perf_counter() - t0, 2)
     return res
 
@@ -420,12 +429,22 @@ def probe_child(args, dims, shape, tsteps, graph):
 def agree_transport(env, probe, kinds, margin=0.97):
     """Every rank's probe -> one choice for all: a candidate counts if it
     passed the gate and timed on EVERY rank; its exchange time is the max over
-    ranks; IPC replaces RCCL only when it is faster by more than 3%.
-    Returns (transport, {kind: record}, probe wall seconds)."""
+    ranks; IPC replaces RCCL only when it is faster by more than 3%.  Every
+    rank calls this (world > 1), probed or not, so ranks whose environments
+    disagree on probing (device counts, LOCAL_WORLD_SIZE) cannot leave one
+    side waiting in the collective: only kinds that every rank probed count.
+    Returns (transport, {kind: record} or None, probe wall seconds)."""
     allp = [None] * env.world_size
-    torch.distributed.all_gather_object(allp, probe, group=env.host_group)
+    torch.distributed.all_gather_object(allp, {"kinds": list(kinds), "probe": probe or {}}, group=env.host_group)
+    common = [t for t in kinds if all(t in (p["kinds"] or []) for p in allp)]
+    if not any(p["kinds"] for p in allp):
+        return "auto", None, 0.0
+    allp_kinds = {tuple(p["kinds"]) for p in allp}
+    allp = [p["probe"] for p in allp]
     cands = {}
-    for t in kinds:
+    if len(allp_kinds) > 1:
+        cands["_mismatch"] = {"gate": "fail", "error": f"ranks probed different kinds: {sorted(allp_kinds)}"}
+    for t in common:
         recs = [(p.get(t) or {}) for p in allp]
         ok = all(r.get("gate_max_diff") == 0.0 and r.get("exchange_us") for r in recs)
         c = {"gate": "pass" if ok else "fail"}
@@ -434,8 +453,8 @@ def agree_transport(env, probe, kinds, margin=0.97):
             c["label"] = recs[0].get("label", t)
         else:
             whys = []
-            for i, (p, r) in enumerate(zip(allp, recs)):
-                why = [f"probe exit {p.get('_rc')}"] if p.get("_rc") != 0 else []
+            for i, r in enumerate(recs):
+                why = [f"probe exit {r.get('_rc')}"] if r.get("_rc", 0) != 0 else []
                 if r.get("error"):
                     why.append(r["error"])
                 elif r.get("gate_max_diff"):
@@ -444,13 +463,176 @@ def agree_transport(env, probe, kinds, margin=0.97):
                     whys.append(f"rank {i}: {', '.join(why)}")
             c["error"] = "; ".join(whys[:4])[:600]
         cands[t] = c
-    passing = {t: c["exchange_us"] for t, c in cands.items() if c["gate"] == "pass"}
+    passing = {t: c["exchange_us"] for t, c in cands.items() if c["gate"] == "pass" and not t.startswith("_")}
     choice = "auto"
     if passing:
         choice = min(passing, key=passing.get)
         if choice != "rccl" and "rccl" in passing and passing[choice] > margin * passing["rccl"]:
             choice = "rccl"
     return choice, cands, max(float(p.get("_s", 0.0)) for p in allp)
+
+
+def result_record(args, env, shape, mlups, ms_per_step, info, dims):
+    """The driver's JSON line without its extras (``line()`` merges them)."""
+    py, px = dims
+    points = shape[0] * shape[1]
+    rec = {
+        "metric": "2D 5-pt Jacobi stencil MLUPS (fp64)",
+        "value": round(mlups, 1),
+        "unit": "MLUPS",
+        "n_gpus": env.world_size,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": args.scaling,
+        "vs_baseline": None,
+        "dtype": "fp64",
+        "data": (f"synthetic: random-init field, uniform [0,1) hashed from the global lattice point "
+                 f"(seed {args.seed}), Dirichlet boundary" if args.init == "random" else
+                 "synthetic: analytic x^3+y^2 initial field, Dirichlet boundary"),
+        "config": {
+            "model": f"mpi_stencil2d jacobi5 {shape[0]}x{shape[1]} fp64",
+            "global_batch": points,
+            "seq_len": None,
+            "parallelism": f"spatial2d py{py} x px{px}, "
+                           f"{'overlap' if info['overlap'] else 'serial'}",
+            "engine": info["engine"],
+            "hipgraph": info["graph"],
+            "overlap_tuning": info.get("overlap_tuning"),
+            "temporal_blocking": info["tblock"],
+            "sweeps_per_pass": info.get("tsteps", 1),
+            "pass_plan": info.get("pass_plan"),
+            "exact_levels": info.get("exact"),
+            "init": args.init,
+            "max_abs_u0": info.get("max_abs_u0"),
+            "pass_cost_ms": info.get("pass_cost_ms"),
+            "transport": info["transport"],
+            "halo_bytes_per_rank": info["halo_bytes_per_rank"],
+            "device": str(env.device),
+        },
+    }
+
+    return rec
+
+
+def _epitaph(env, rec):
+    """Returns a function that (re)registers the current result line (``rec()``)
+    as the watchdog's last words (rank 0; the other ranks exit 0 silently)."""
+    dev = "cuda" if env.is_gpu else "cpu"
+
+    def update():
+        watchdog_epitaph(json.dumps(rec()) if env.rank == 0 else "", 0, dev)
+
+    return update
+
+
+def _maybe_hang(env, phase):
+    """Fault injection for the extras' isolation test: GMT_BENCH_HANG=R:PHASE
+    makes rank R stop forever when it reaches PHASE (a substring of the phase
+    name); the other ranks block in that phase's collective."""
+    spec = os.environ.get("GMT_BENCH_HANG", "")
+    r, _, ph = spec.partition(":")
+    if spec and r == str(env.rank) and ph and ph in phase:
+        print(f"GMT FAULT INJECTION: rank {env.rank} hangs in bench phase '{phase}'", file=sys.stderr, flush=True)
+        while True:
+            time.sleep(3600)
+
+
+def run_extras(args, env, solver, info, shape, points, tsteps, overlap, dims, graph, transport, extras, epitaph):
+    """Every BASELINE quantity besides the headline, each failure-isolated:
+    an exception is recorded as "<name>_error" and the next extra runs (a
+    hang is the watchdog's, see main).  The data-plane extras run on the
+    transport the job runs on (the probe's choice when it dropped one)."""
+    iters = max(20, min(args.steps, 200))
+
+    def extra(name, fn):
+        mark(env, name)
+        _maybe_hang(env, name)
+        try:
+            fn()
+        except Exception as ex:  # isolated: the line records it, the job goes on
+            extras[f"{name.replace(' ', '_')}_error"] = f"{type(ex).__name__}: {ex}"[:300]
+        epitaph()
+
+    def halo():
+        if env.world_size > 1:
+            extras["halo_exchange_us"] = round(halo_latency(env, solver, iters) * 1e6, 2)
+            extras["halo_exchange_kind"] = (f"{info['transport']}, {info['tsteps']}-wide faces + corners "
+                                            f"of the {shape[0]}x{shape[1]} field, process grid "
+                                            f"{info['dims'][0]}x{info['dims'][1]}")
+        extras["residual_l2"] = solver.residual()
+
+    extra("halo latency", halo)
+    solver.close()
+    if env.is_gpu:
+        torch.cuda.empty_cache()
+    if env.world_size == 1:
+        def self_halo():
+            t, nbytes, kind = self_halo_latency(env, shape, tsteps, iters)
+            extras["halo_exchange_us"] = round(t * 1e6, 2)
+            extras["halo_exchange_kind"] = (f"1-rank periodic {kind} self-exchange, {tsteps}-wide faces + "
+                                            f"corners of the {shape[0]}x{shape[1]} field ({nbytes} bytes)")
+
+        extra("self halo latency", self_halo)
+    # the other orientation of a non-square process grid (BASELINE names
+    # "2x4"; choose_dims may pick 4x2): the same run with PY and PX swapped,
+    # so both rates are on record (profiles/r03_shares.md)
+    hp, hx = info["dims"]
+    if env.world_size > 1 and hp != hx and args.scaling == "strong":
+        def alt():
+            eng3, dt3, info3 = bench_native(env, shape, args.steps, args.warmup, overlap, (hx, hp), graph,
+                                            tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows,
+                                            args.init, args.seed, not args.no_calibrate, transport)
+            eng3.close()
+            extras["stencil_alt_dims"] = f"{hx}x{hp}"
+            extras["stencil_alt_dims_MLUPS"] = round(points * args.steps / dt3 / 1e6, 1)
+            extras["stencil_alt_dims_overlap"] = info3["overlap"]
+            if env.is_gpu:
+                torch.cuda.empty_cache()
+
+        extra("swapped process grid run", alt)
+    if args.small_size:
+        def small():
+            s2 = (args.small_size, args.small_size)
+            # 1000 sweeps of 8192^2 are 14 ms of GPU work: 100 (1.4 ms) read
+            # 3-4% low, mostly the host round trip and the clock ramp around
+            # so short a timed region (profiles/r04_shares.md)
+            steps2 = args.small_steps or max(1000 if env.is_gpu else 100, 4 * args.steps)
+            eng2, dt2, info2 = bench_native(env, s2, steps2, max(args.warmup, 10), overlap, dims, graph,
+                                            tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows,
+                                            args.init, args.seed, not args.no_calibrate, transport)
+            eng2.close()
+            extras[f"stencil_{args.small_size}_MLUPS"] = round(s2[0] * s2[1] * steps2 / dt2 / 1e6, 1)
+            extras[f"stencil_{args.small_size}_ms_per_step"] = round(dt2 / steps2 * 1e3, 5)
+            extras[f"stencil_{args.small_size}_pass_plan"] = f"{steps2} steps: {info2['pass_plan']}"
+
+        extra("small-domain stencil run", small)
+    if env.world_size > 1:
+        def refh():
+            extras.update(ref_halo(env, args.ref_n_local, args.ref_n_other, args.ref_iters, transport))
+            bad = (extras["ref_halo_dim0_bad_ghosts"], extras["ref_halo_dim1_bad_ghosts"])
+            if any(bad):
+                raise RuntimeError(f"wrong ghost cells after an exchange (dim 0: {bad[0]}, dim 1: {bad[1]})")
+
+        extra("reference halo benchmark", refh)
+
+    def daxpy():
+        gbps, ddt = bench_daxpy(env, args.daxpy_n, iters=20)
+        extras["daxpy_GBps"] = round(gbps, 1)
+        extras["daxpy_GBps_per_gpu"] = round(gbps / env.world_size, 1)
+        extras["daxpy_n"] = args.daxpy_n
+        extras["daxpy_ms"] = round(ddt * 1e3, 4)
+
+    extra("daxpy", daxpy)
+
+    def allred():
+        extras.update(daxpy_allreduce(env, args.daxpy_n, iters=20, transport=transport))
+        if not extras["daxpy_allsum_rel_err"] <= 1e-9:
+            raise RuntimeError(f"DAXPY ALLSUM {extras['daxpy_allsum']} differs from the closed form "
+                               f"{extras['daxpy_allsum_exact']} (rel err {extras['daxpy_allsum_rel_err']:.3e})")
+
+    extra("daxpy all-reduce", allred)
 
 
 def main(argv=None):
@@ -539,11 +721,12 @@ def main(argv=None):
         return
     extras = {}
     transport = args.transport
-    if kinds:
+    if env.world_size > 1 and args.transport == "auto":
         mark(env, "transport choice")
         transport, cands, probe_s = agree_transport(env, probe, kinds)
-        extras["transport_candidates"] = cands
-        extras["transport_probe_s"] = probe_s
+        if cands is not None:
+            extras["transport_candidates"] = cands
+            extras["transport_probe_s"] = probe_s
     if not args.skip_check:
         mark(env, "correctness gate")
         diff = check_engine(env, dims or gdims, tsteps, graph, args.init, args.seed, transport)
@@ -562,125 +745,32 @@ def main(argv=None):
     points = shape[0] * shape[1]
     mlups = points * args.steps / dt / 1e6
     ms_per_step = dt / args.steps * 1e3
+    py, px = info["dims"] if info.get("dims") else gdims
+    extras["watchdog_timeout_s"] = watchdog_timeout("cuda" if env.is_gpu else "cpu")
+    base = result_record(args, env, shape, mlups, ms_per_step, info, (py, px))
+
+    def rec():
+        return {**base, **extras}
+
+    # From here on the headline is measured: every later phase is an extra.
+    # An extra that raises becomes an "<extra>_error" field; one that hangs
+    # ends the job through the watchdog, which then prints this line (with
+    # the extras finished so far and a "watchdog" field) and exits 0 on
+    # every rank instead of 124 — the headline is never lost to an extra.
+    epitaph = _epitaph(env, rec)
+    epitaph()
     if not args.skip_extras:
-        iters = max(20, min(args.steps, 200))
-        mark(env, "halo latency")
-        if env.world_size > 1:
-            extras["halo_exchange_us"] = round(halo_latency(env, solver, iters) * 1e6, 2)
-            extras["halo_exchange_kind"] = (f"{info['transport']}, {info['tsteps']}-wide faces + corners "
-                                            f"of the {shape[0]}x{shape[1]} field, process grid "
-                                            f"{info['dims'][0]}x{info['dims'][1]}")
-        extras["residual_l2"] = solver.residual()
-        solver.close()
-        del solver
-        if env.is_gpu:
-            torch.cuda.empty_cache()
-        if env.world_size == 1:
-            t, nbytes, kind = self_halo_latency(env, shape, tsteps, iters)
-            extras["halo_exchange_us"] = round(t * 1e6, 2)
-            extras["halo_exchange_kind"] = (f"1-rank periodic {kind} self-exchange, {tsteps}-wide faces + "
-                                            f"corners of the {shape[0]}x{shape[1]} field ({nbytes} bytes)")
-        # the other orientation of a non-square process grid (BASELINE names
-        # "2x4"; choose_dims may pick 4x2): the same run with PY and PX
-        # swapped, so both rates are on record (profiles/r03_shares.md)
-        hp, hx = info["dims"]
-        if env.world_size > 1 and hp != hx and args.scaling == "strong":
-            mark(env, "swapped process grid run")
-            eng3, dt3, info3 = bench_native(env, shape, args.steps, args.warmup, overlap, (hx, hp), graph,
-                                            tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows,
-                                            args.init, args.seed, not args.no_calibrate, transport)
-            eng3.close()
-            extras["stencil_alt_dims"] = f"{hx}x{hp}"
-            extras["stencil_alt_dims_MLUPS"] = round(points * args.steps / dt3 / 1e6, 1)
-            extras["stencil_alt_dims_overlap"] = info3["overlap"]
-            if env.is_gpu:
-                torch.cuda.empty_cache()
-        if args.small_size:
-            mark(env, "small-domain stencil run")
-            s2 = (args.small_size, args.small_size)
-            # 1000 sweeps of 8192^2 are 14 ms of GPU work: 100 (1.4 ms) read
-            # 3-4% low, mostly the host round trip and the clock ramp around
-            # so short a timed region (profiles/r04_shares.md)
-            steps2 = args.small_steps or max(1000 if env.is_gpu else 100, 4 * args.steps)
-            eng2, dt2, info2 = bench_native(env, s2, steps2, max(args.warmup, 10), overlap, dims, graph,
-                                            tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows,
-                                            args.init, args.seed, not args.no_calibrate, transport)
-            eng2.close()
-            extras[f"stencil_{args.small_size}_MLUPS"] = round(s2[0] * s2[1] * steps2 / dt2 / 1e6, 1)
-            extras[f"stencil_{args.small_size}_ms_per_step"] = round(dt2 / steps2 * 1e3, 5)
-            extras[f"stencil_{args.small_size}_pass_plan"] = f"{steps2} steps: {info2['pass_plan']}"
-        if env.world_size > 1:
-            mark(env, "reference halo benchmark")
-            # the reference benchmark and the all-reduce stay on the requested
-            # transport (auto: RCCL at one rank per GPU); the probe gated and
-            # timed the stencil engine's exchange only
-            extras.update(ref_halo(env, args.ref_n_local, args.ref_n_other, args.ref_iters, args.transport))
-            if extras["ref_halo_dim0_bad_ghosts"] or extras["ref_halo_dim1_bad_ghosts"]:
-                if env.rank == 0:
-                    print("bench.py: the reference halo benchmark found wrong ghost cells after an exchange "
-                          f"(dim 0: {extras['ref_halo_dim0_bad_ghosts']}, dim 1: {extras['ref_halo_dim1_bad_ghosts']})",
-                          file=sys.stderr)
-                gdist.shutdown()
-                sys.exit(6)
-        mark(env, "daxpy")
-        gbps, ddt = bench_daxpy(env, args.daxpy_n, iters=20)
-        extras["daxpy_GBps"] = round(gbps, 1)
-        extras["daxpy_GBps_per_gpu"] = round(gbps / env.world_size, 1)
-        extras["daxpy_n"] = args.daxpy_n
-        extras["daxpy_ms"] = round(ddt * 1e3, 4)
-        mark(env, "daxpy all-reduce")
-        extras.update(daxpy_allreduce(env, args.daxpy_n, iters=20, transport=args.transport))
-        if not extras["daxpy_allsum_rel_err"] <= 1e-9:
-            if env.rank == 0:
-                print(f"bench.py: DAXPY ALLSUM {extras['daxpy_allsum']} differs from the closed form "
-                      f"{extras['daxpy_allsum_exact']} (rel err {extras['daxpy_allsum_rel_err']:.3e})",
-                      file=sys.stderr)
-            gdist.shutdown()
-            sys.exit(4)
+        run_extras(args, env, solver, info, shape, points, tsteps, overlap, dims, graph, transport, extras, epitaph)
     else:
         solver.close()
-    py, px = info["dims"] if info.get("dims") else gdims
     mark(env, "report")
-    extras["watchdog_timeout_s"] = watchdog_timeout("cuda" if env.is_gpu else "cpu")
     if env.rank == 0:
-        rec = {
-            "metric": "2D 5-pt Jacobi stencil MLUPS (fp64)",
-            "value": round(mlups, 1),
-            "unit": "MLUPS",
-            "n_gpus": env.world_size,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": args.scaling,
-            "vs_baseline": None,
-            "dtype": "fp64",
-            "data": (f"synthetic: random-init field, uniform [0,1) hashed from the global lattice point "
-                     f"(seed {args.seed}), Dirichlet boundary" if args.init == "random" else
-                     "synthetic: analytic x^3+y^2 initial field, Dirichlet boundary"),
-            "config": {
-                "model": f"mpi_stencil2d jacobi5 {shape[0]}x{shape[1]} fp64",
-                "global_batch": points,
-                "seq_len": None,
-                "parallelism": f"spatial2d py{py} x px{px}, "
-                               f"{'overlap' if info['overlap'] else 'serial'}",
-                "engine": info["engine"],
-                "hipgraph": info["graph"],
-                "overlap_tuning": info.get("overlap_tuning"),
-                "temporal_blocking": info["tblock"],
-                "sweeps_per_pass": info.get("tsteps", 1),
-                "pass_plan": info.get("pass_plan"),
-                "exact_levels": info.get("exact"),
-                "init": args.init,
-                "max_abs_u0": info.get("max_abs_u0"),
-                "pass_cost_ms": info.get("pass_cost_ms"),
-                "transport": info["transport"],
-                "halo_bytes_per_rank": info["halo_bytes_per_rank"],
-                "device": str(env.device),
-            },
-            **extras,
-        }
-        print(json.dumps(rec), flush=True)
+        print(json.dumps(rec()), flush=True)
+    # the line is out: a hang in the teardown exits quietly
+    watchdog_epitaph("", 0, "cuda" if env.is_gpu else "cpu")
+    failed = [k for k in extras if k.endswith("_error")]
+    if failed and env.rank == 0:
+        print(f"bench.py: extras failed (the headline stands): {', '.join(failed)}", file=sys.stderr)
     gdist.shutdown()
 
 

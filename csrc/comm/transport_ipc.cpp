@@ -31,6 +31,11 @@ constexpr int kStageTag = 10000, kFlagTag = 20000, kReadyTag = 30000;
 struct IpcWire {
   gmt_ipc_handle h;
   uint64_t offset;
+  // the message's byte count on the side that sends this wire: both sides
+  // of a message must agree (a rank whose environment picked another face
+  // layout, e.g. GMT_IPC_BLOCKS, would otherwise read past the sender's
+  // staging slot or fill ghost cells with the wrong bytes)
+  uint64_t bytes;
 };
 
 // hipIpcOpenMemHandle maps an allocation once per process: cache by handle.
@@ -90,12 +95,13 @@ class IpcExchange : public Exchange {
 
     // wiring: the receiver of send i learns {its staging, its consumed flag};
     // the sender of receive j learns {its ready flag}
-    auto wire = [](void* p) {
+    auto wire = [](void* p, size_t bytes) {
       IpcWire w;
       std::memset(&w, 0, sizeof(w));
       size_t off = 0;
       GMT_CHECK("ipc get handle", gmt_rt_ipc_get_handle(&w.h, &off, p));
       w.offset = off;
+      w.bytes = bytes;
       return w;
     };
     std::vector<IpcWire> out_stage(ns), out_cflag(ns), out_rflag(nr), in_stage(nr), in_cflag(nr), in_rflag(ns);
@@ -105,19 +111,30 @@ class IpcExchange : public Exchange {
       if (m.peer == rank_) continue;
       hr.push_back({&in_stage[j], sizeof(IpcWire), m.peer, m.tag + kStageTag});
       hr.push_back({&in_cflag[j], sizeof(IpcWire), m.peer, m.tag + kFlagTag});
-      out_rflag[j] = wire(flags_.data() + j);
+      out_rflag[j] = wire(flags_.data() + j, m.bytes);
       hs.push_back({&out_rflag[j], sizeof(IpcWire), m.peer, m.tag + kReadyTag});
     }
     for (size_t i = 0; i < ns; ++i) {
       const Msg& m = sends_[i];
       if (m.peer == rank_) continue;
       hr.push_back({&in_rflag[i], sizeof(IpcWire), m.peer, m.tag + kReadyTag});
-      out_stage[i] = wire(stage_[i].data());
-      out_cflag[i] = wire(flags_.data() + nr + i);
+      out_stage[i] = wire(stage_[i].data(), m.bytes);
+      out_cflag[i] = wire(flags_.data() + nr + i, m.bytes);
       hs.push_back({&out_stage[i], sizeof(IpcWire), m.peer, m.tag + kStageTag});
       hs.push_back({&out_cflag[i], sizeof(IpcWire), m.peer, m.tag + kFlagTag});
     }
     ctl.exchange(hr, hs);
+    auto agree = [&](const Msg& m, uint64_t peer_bytes, const char* what) {
+      if (peer_bytes == m.bytes) return;
+      std::fprintf(stderr, "ipc: rank %d %s %zu bytes (tag %d) but rank %d's side of that message has %llu bytes; "
+                  "the ranks disagree on the face layout (GMT_IPC_BLOCKS must match on every rank)\n",
+                  rank_, what, m.bytes, m.tag, m.peer, static_cast<unsigned long long>(peer_bytes));
+      abort_job(2);
+    };
+    for (size_t j = 0; j < nr; ++j)
+      if (recvs_[j].peer != rank_) agree(recvs_[j], in_stage[j].bytes, "receives");
+    for (size_t i = 0; i < ns; ++i)
+      if (sends_[i].peer != rank_) agree(sends_[i], in_rflag[i].bytes, "sends");
     auto open = [&](const IpcWire& w) {
       void* base = cache_->open(w.h);
       opened_.push_back(base);

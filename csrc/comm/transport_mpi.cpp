@@ -12,6 +12,7 @@
 #include <tuple>
 
 #include "gmt/buffer.hpp"
+#include "gmt/watchdog.hpp"
 #include "gmt/comm.hpp"
 #include "gmt/control.hpp"
 #include "gmt/mpi.hpp"
@@ -206,8 +207,14 @@ class MpiHostExchange : public Exchange {
       }
     }
     for (auto& e : h2d_done_) GMT_CHECK("event", gmt_rt_event_create(&e, 0));
+    // the staging poll gives up after this long WITHOUT a chunk staged (the
+    // clock restarts at every staged chunk).  The first chunk also waits for
+    // whatever the stream holds ahead of the staging kernel, so the default
+    // is the hang watchdog's timeout (GMT_TIMEOUT), at least 10 s; an
+    // explicit GMT_WAIT_TIMEOUT_MS wins
     const char* w = std::getenv("GMT_WAIT_TIMEOUT_MS");
-    wait_limit_s_ = (w && std::atof(w) > 0 ? std::atof(w) : 10000.0) / 1e3;
+    const double wd = watchdog_state().timeout;
+    wait_limit_s_ = w && std::atof(w) > 0 ? std::atof(w) / 1e3 : std::max(10.0, wd);
   }
   ~MpiHostExchange() override {
     for (auto& e : events_) gmt_rt_event_destroy(e);
@@ -277,13 +284,14 @@ class MpiHostExchange : public Exchange {
       return kernel_ ? __atomic_load_n(flags_.data() + k, __ATOMIC_ACQUIRE) >= epoch_
                      : gmt_rt_event_query(events_[k]) == 0;
     };
-    const double t0 = MPI_Wtime();
+    double t0 = MPI_Wtime();
     long polls = 0;
     while (next < schunks_.size() || pending > 0) {
       bool progress = false;
       while (next < schunks_.size() && staged(next)) {
         send(next++);
         progress = true;
+        t0 = MPI_Wtime();
       }
       if (pending > 0) {
         int n = 0;

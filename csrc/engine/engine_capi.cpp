@@ -123,6 +123,7 @@ void gmt_engine_watchdog_kick(const char* phase) {
   std::snprintf(d, sizeof(slots[0]), "%s", phase ? phase : "python");
   gmt::watchdog_kick(d);
 }
+void gmt_engine_watchdog_epitaph(const char* json, int code) { gmt::watchdog_set_epitaph(json, code); }
 double gmt_engine_watchdog_timeout(void) {
   return gmt::watchdog_state().armed.load() ? gmt::watchdog_state().timeout : 0.0;
 }

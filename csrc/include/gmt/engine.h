@@ -83,6 +83,10 @@ void gmt_engine_comm_destroy(void* h);
  * arrives for that long.  A caller marks progress of its own phases here. */
 void gmt_engine_watchdog_kick(const char* phase);
 double gmt_engine_watchdog_timeout(void); /* 0 when not armed */
+/* Last words: when the watchdog fires, write `json` (an object) to stdout with
+ * a "watchdog" field naming the stall and exit with `code` instead of 124; ""
+ * exits with `code` silently; NULL restores the default. */
+void gmt_engine_watchdog_epitaph(const char* json, int code);
 
 /* The reference's halo-exchange benchmark (mpi_stencil2d_gt test_deriv for
  * dim 0 and dim 1, then test_sum), n_local x n_other per rank, 2 ghosts,

@@ -40,6 +40,12 @@ struct WatchdogState {
   int rank = -1, device = -1;
   long long hang_rank = -2, hang_after = 0;  // fault injection
   std::atomic<long long> exchanges{0};
+  // Last words (watchdog_set_epitaph): a JSON object written to stdout, with
+  // a "watchdog" field naming the stall, before the process exits with
+  // epitaph_code instead of 124 — a result already measured is not lost to a
+  // later phase that hangs.  Empty text: exit with the code, print nothing.
+  std::atomic<const char*> epitaph{nullptr};
+  std::atomic<int> epitaph_code{124};
 };
 
 // intentionally leaked: the detached thread may outlive static destruction
@@ -94,10 +100,34 @@ inline void watchdog_start(int rank, int device) {
                      "GMT WATCHDOG: rank %d host %s device %d: no progress for %.1f s "
                      "(timeout %.1f s, last phase '%s'); aborting the job\n",
                      w.rank, host, w.device, idle, w.timeout, w.phase.load());
+        if (const char* ep = w.epitaph.load()) {
+          const size_t n = std::strlen(ep);
+          const char* close = n ? std::strrchr(ep, '}') : nullptr;
+          if (close) {
+            // raw write(2): the main thread may hold stdio's lock
+            char tail[512];
+            const int m = std::snprintf(tail, sizeof(tail),
+                                        "%s\"watchdog\": \"rank %d: no progress for %.1f s in phase '%s'\"}\n",
+                                        close == ep + 1 ? "" : ", ", w.rank, idle, w.phase.load());
+            ssize_t rc = write(1, ep, static_cast<size_t>(close - ep));
+            rc = write(1, tail, static_cast<size_t>(m > 0 && m < static_cast<int>(sizeof(tail)) ? m : 0));
+            (void)rc;
+          }
+          abort_job(w.epitaph_code.load());
+        }
         abort_job(124);
       }
     }
   }).detach();
+}
+
+// Replaces the epitaph (a copy is kept; the previous one is leaked on
+// purpose: the watchdog thread may be reading it).  nullptr: none, the
+// watchdog exits 124 again.
+inline void watchdog_set_epitaph(const char* json, int code) {
+  WatchdogState& w = watchdog_state();
+  w.epitaph_code.store(code);
+  w.epitaph.store(json ? strdup(json) : nullptr);
 }
 
 // Fault injection point (halo exchange start): rank `hang_rank` stops here

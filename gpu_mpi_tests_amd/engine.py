@@ -109,6 +109,8 @@ def load(device: str = "cuda") -> ctypes.CDLL:
     lib.gmt_engine_deriv_bench.restype = c_int
     lib.gmt_engine_watchdog_kick.argtypes = [ctypes.c_char_p]
     lib.gmt_engine_watchdog_kick.restype = None
+    lib.gmt_engine_watchdog_epitaph.argtypes = [ctypes.c_char_p, c_int]
+    lib.gmt_engine_watchdog_epitaph.restype = None
     lib.gmt_engine_watchdog_timeout.argtypes = []
     lib.gmt_engine_watchdog_timeout.restype = ctypes.c_double
     # from libgmt (a dependency of the engine library: found through its handle)
@@ -128,6 +130,15 @@ def watchdog_kick(phase: str, device: str = "cpu") -> None:
     and the last phase; gmt/watchdog.hpp).  A no-op until an engine entry
     point has armed it."""
     load(device).gmt_engine_watchdog_kick(phase.encode()[:95])
+
+
+def watchdog_epitaph(text: "str | None", code: int = 0, device: str = "cpu") -> None:
+    """Last words for the hang watchdog: if it fires, ``text`` (a JSON object)
+    is written to stdout with a "watchdog" field naming the stalled rank and
+    phase, and the process exits with ``code`` instead of 124 ("" exits
+    silently; None restores the default).  bench.py registers its result
+    line once the headline is measured, so an extra that hangs cannot lose it."""
+    load(device).gmt_engine_watchdog_epitaph(None if text is None else text.encode(), int(code))
 
 
 def watchdog_timeout(device: str = "cpu") -> float:

@@ -223,3 +223,52 @@ def test_bench_transport_probe_drops_a_crashing_candidate_cpu():
     assert cands["rccl"]["gate"] == "pass" and cands["rccl"]["exchange_us"] > 0, cands
     assert cands["ipc"]["gate"] == "fail" and "probe exit" in cands["ipc"]["error"], cands
     assert rec["config"]["transport"] == "rccl-host" and rec["check_max_diff"] == 0.0
+
+
+def test_bench_probe_drops_rccl_every_extra_on_ipc_cpu():
+    """The probe's RCCL candidate dies (rank 1's child exits 139 at RCCL): the
+    job, the reference halo benchmark and the DAXPY all-reduce all run on the
+    surviving IPC data plane, with the extras on, and the line says why RCCL
+    was dropped ("next round" item 3)."""
+    port, pport = str(free_port()), str(free_port())
+    rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
+                "--device", "cpu", "--size", "192", "--steps", "3", "--warmup", "1",
+                "--daxpy-n", "20000", "--ref-n-local", "32", "--ref-n-other", "300", "--ref-iters", "4",
+                "--small-size", "96", "--transport-probe", "on", "--probe-port", pport, "--probe-iters", "5",
+                "--probe-timeout", "30"], GMT_PROBE_CRASH="1:rccl")
+    cands = rec["transport_candidates"]
+    assert cands["rccl"]["gate"] == "fail" and "probe exit 139" in cands["rccl"]["error"], cands
+    assert cands["ipc"]["gate"] == "pass", cands
+    assert rec["config"]["transport"] == "ipc-host"
+    assert rec["ref_halo_config"].endswith("ipc-host") and rec["daxpy_allreduce_kind"] == "ipc-host"
+    assert rec["ref_halo_dim0_bad_ghosts"] == 0 and rec["daxpy_allsum_rel_err"] <= 1e-9
+    assert not [k for k in rec if k.endswith("_error")], rec
+
+
+def test_bench_extra_hang_keeps_the_headline_cpu():
+    """An extra that hangs after the headline is measured (rank 1 stops in
+    the DAXPY all-reduce, rank 0 blocks in it): the watchdog prints the line
+    it was given — the headline, every extra finished before, and a
+    "watchdog" field naming the stall — and every rank exits 0."""
+    port = str(free_port())
+    rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
+                "--device", "cpu", "--size", "192", "--steps", "3", "--warmup", "1",
+                "--daxpy-n", "20000", "--ref-n-local", "32", "--ref-n-other", "300", "--ref-iters", "4",
+                "--small-size", "0"], timeout=300, GMT_TRANSPORT="rccl", GMT_TIMEOUT="6",
+               GMT_BENCH_HANG="1:daxpy all-reduce")
+    _check(rec, 2, 3, 1, points=192 * 192)
+    assert rec["check_max_diff"] == 0.0 and rec["daxpy_GBps"] > 0 and rec["ref_halo_dim0_us"] > 0
+    assert "daxpy_allsum" not in rec
+    assert "no progress" in rec["watchdog"] and "daxpy all-reduce" in rec["watchdog"], rec["watchdog"]
+
+
+def test_bench_extra_exception_is_recorded_cpu():
+    """An extra that raises is a field of the line, not an exit: a DAXPY of
+    an impossible size fails alone and the job still reports."""
+    rec = _run([sys.executable, "bench.py", "--device", "cpu", "--size", "128", "--steps", "4",
+                "--warmup", "1", "--daxpy-n", "-5", "--small-size", "0"])
+    _check(rec, 1, 4, 1, points=128 * 128)
+    assert "daxpy_error" in rec and "daxpy_all-reduce_error" in rec, sorted(rec)
+    assert rec["halo_exchange_us"] > 0

@@ -174,3 +174,26 @@ print(json.dumps(dict(same=bool((z == engine.lattice_uniform(gx, gy, 12345)).all
     assert p.returncode == 0, p.stdout + p.stderr
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["same"] and 0.0 <= r["lo"] and r["hi"] < 1.0
+
+
+def _ipc_layout_mismatch(env):
+    # rank 1 packs its faces, rank 0 moves them in place: the y faces of the
+    # one-phase corner exchange then differ in size between the two sides
+    os.environ["GMT_IPC_BLOCKS"] = "0" if env.rank == 1 else "1"
+    from gpu_mpi_tests_amd import engine
+
+    e = engine.NativeJacobi(64, 64, env, dims=(2, 1), periodic=True, tblock=4, transport="ipc")
+    e.close()
+    return "no abort"
+
+
+def test_ipc_plan_refuses_mismatched_face_layouts():
+    """a rank whose environment picks another face layout must not
+    exchange: the IPC plan compares every message's byte count with its peer's
+    during the handle exchange and aborts naming both ranks."""
+    from mp_util import run_dist
+
+    ensure_host_build()
+    with pytest.raises(AssertionError) as ei:
+        run_dist(_ipc_layout_mismatch, 2, free_port(), timeout=120)
+    assert "disagree on the face layout" in str(ei.value), str(ei.value)[-3000:]

@@ -187,6 +187,8 @@ def test_mpi_stencil2d_gt_alloc_per_call_is_untagged():
     lines then carry exactly the reference's fields."""
     out = run_app("mpi_stencil2d_gt", "32", "3", "--n-other=128", "--no-managed", "--alloc-per-call",
                   "--transport=mpi-host", np=2).stdout
+    # the header carries the reference's n_warmup byte for byte (mpi_stencil2d_gt.cc:658,687)
+    assert "n_warmup       = 10\n" in out
     tests = _TEST_RE.findall(out)
     assert len(tests) == 4 and all(t[-1] == "" for t in tests)
 
