@@ -104,13 +104,22 @@ def plan_str(plan):
     return "+".join(out)
 
 
+def _plane(plane):
+    """A data plane of the probe / --transport -> (engine transport, push):
+    "push" is the IPC transport with the inline halo exchange (each fused
+    pass stores its faces straight into the neighbours' ghost cells,
+    gmt/jacobi.hpp JacobiConfig::push)."""
+    return ("ipc", True) if plane == "push" else (plane, False)
+
+
 def bench_native(env, shape, steps, warmup, overlap, dims, graph, tblock, wg_waves, seg_rows, init="random",
                  seed=0, calibrate=True, transport="auto"):
     from gpu_mpi_tests_amd.engine import NativeJacobi
 
+    t, push = _plane(transport)
     eng = NativeJacobi(shape[0], shape[1], env, dims=dims, overlap=overlap, graph=graph, tblock=tblock,
                        wg_waves=wg_waves, seg_rows=seg_rows, init=init, seed=seed, calibrate=calibrate,
-                       transport=transport)
+                       transport=t, push=push and env.world_size > 1)
     # calibration (one timed pass of every pass size on this share, max over
     # ranks) -> the plan; then one launch of every pass type of the timed
     # plan; the initial field is restored
@@ -119,7 +128,8 @@ def bench_native(env, shape, steps, warmup, overlap, dims, graph, tblock, wg_wav
     info = {"engine": "native", "graph": eng.graph, "overlap": eng.overlap, "tblock": eng.tblock,
             "overlap_tuning": eng.tuned, "tsteps": eng.tsteps, "pass_plan": plan_str(eng.plan(steps)),
             "exact": eng.exact, "max_abs_u0": eng.max_abs_u0, "pass_cost_ms": eng.pass_cost_ms(),
-            "transport": eng.transport if env.world_size > 1 else "none",
+            "transport": (eng.transport + (" inline halo" if eng.push_active else "")
+                          if env.world_size > 1 else "none"),
             "halo_bytes_per_rank": eng.halo_bytes, "dims": (eng.py, eng.px)}
     return eng, dt, info
 
@@ -135,6 +145,7 @@ def check_engine(env, dims, tsteps, graph, init="analytic", seed=0, transport="a
 
     py, px = dims
     k = max(1, tsteps)
+    t, push = _plane(transport)
     # every rank big enough for the overlapped (band-first) pass: K-deep
     # bands plus an interior in y, three workgroup-wide strips in x
     wb = group_cols(k, 0, "cuda" if env.is_gpu else "cpu") if k > 1 else 0
@@ -142,9 +153,9 @@ def check_engine(env, dims, tsteps, graph, init="analytic", seed=0, transport="a
     steps = 2 * k + 3  # full passes, a remainder pass and (odd) single sweeps
     ref = serial_jacobi(ny, nx, steps, init=init, seed=seed) if env.rank == 0 else None
     worst = 0.0
-    for ov in (True, False):
+    for ov in ((True,) if push else (True, False)):
         e = NativeJacobi(ny, nx, env, dims=dims, overlap=ov, graph=graph, tblock=k if k > 1 else False,
-                         init=init, seed=seed, transport=transport)
+                         init=init, seed=seed, transport=t, push=push)
         e.run(steps)
         e.synchronize()
         part = (e.off_y, e.off_x, e.interior())
@@ -317,7 +328,7 @@ def daxpy_allreduce(env, n, iters, transport="auto"):
             "daxpy_allreduce_kind": kind}
 
 
-PROBE_KINDS = ("rccl", "ipc")
+PROBE_KINDS = ("rccl", "ipc", "push")
 
 
 def _env_transport():
@@ -338,7 +349,7 @@ def probe_kinds(args):
     lw = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)) or world)
     ndev = 0 if args.device == "cpu" else torch.cuda.device_count()  # counting does not initialise the GPU
     if args.transport_probe == "on":
-        return list(PROBE_KINDS) if ndev == 0 or lw <= ndev else ["ipc"]
+        return list(PROBE_KINDS) if ndev == 0 or lw <= ndev else ["ipc", "push"]
     return list(PROBE_KINDS) if 0 < ndev and lw <= ndev else []
 
 
@@ -390,37 +401,59 @@ def run_probe(args, argv, kinds):
     return res
 
 
+def probe_pass_ms(env, eng, tsteps, passes):
+    """ms per fused pass of the engine as built (exchange or inline halo, and
+    overlap, included), max over ranks: what the candidate costs the run."""
+    eng.run(tsteps)
+    eng.synchronize()
+    gdist.barrier(env)
+    t0 = time.perf_counter()
+    eng.run(passes * tsteps)
+    eng.synchronize()
+    dt = (time.perf_counter() - t0) / passes
+    return gdist.allreduce_max(dt, env) * 1e3
+
+
 def probe_child(args, dims, shape, tsteps, graph):
-    """--probe-child: every candidate's bitwise gate on this process grid,
-    then its blocking K-wide exchange of the headline field (mean
-    over --probe-iters, max over ranks), written as JSON to the given path
-    after each candidate.  Fault injection: GMT_PROBE_CRASH=R:KIND makes rank
-    R's child die (status 139, as on a GPU memory fault) when it reaches KIND."""
+    """--probe-child: the candidate's bitwise gate on this process grid, then
+    the cost of its fused passes on the headline field (``pass_ms``: the
+    passes as the job would run them, exchange or inline halo included, mean
+    over --probe-passes, max over ranks) and, for the exchange transports,
+    the blocking K-wide exchange (mean over --probe-iters), written as JSON
+    to the given path.  Fault injection: GMT_PROBE_CRASH=R:KIND makes rank R's
+    child die (status 139, as on a GPU memory fault) when it reaches KIND."""
     from gpu_mpi_tests_amd.engine import NativeJacobi
 
     env = gdist.init(device=args.device)
     crash = os.environ.get("GMT_PROBE_CRASH", "").split(":")
     out = {}
-    for t in args.probe_kinds.split(","):
-        mark(env, f"transport probe: {t}")
-        if len(crash) == 2 and crash[0] == str(env.rank) and crash[1] == t:
-            print(f"GMT FAULT INJECTION: rank {env.rank} transport probe child dies at {t}", file=sys.stderr,
+    for plane in args.probe_kinds.split(","):
+        mark(env, f"transport probe: {plane}")
+        if len(crash) == 2 and crash[0] == str(env.rank) and crash[1] == plane:
+            print(f"GMT FAULT INJECTION: rank {env.rank} transport probe child dies at {plane}", file=sys.stderr,
                   flush=True)
             os._exit(139)
+        t, push = _plane(plane)
         rec = {}
         try:
-            rec["gate_max_diff"] = check_engine(env, dims, tsteps, graph, "analytic", 0, transport=t)
+            rec["gate_max_diff"] = check_engine(env, dims, tsteps, graph, "analytic", 0, transport=plane)
             if rec["gate_max_diff"] == 0.0:
-                eng = NativeJacobi(shape[0], shape[1], env, dims=dims, overlap=False, graph=False,
-                                   tblock=tsteps if tsteps > 1 else False, transport=t, calibrate=False)
+                eng = NativeJacobi(shape[0], shape[1], env, dims=dims, overlap=False if push else "auto",
+                                   graph=False, tblock=tsteps if tsteps > 1 else False, transport=t, push=push,
+                                   calibrate=False)
                 try:
-                    rec["exchange_us"] = round(halo_latency(env, eng, args.probe_iters) * 1e6, 2)
-                    rec["label"] = eng.transport
+                    if push and not eng.push_active:
+                        raise RuntimeError("the inline halo exchange does not apply to this share")
+                    rec["pass_ms"] = round(probe_pass_ms(env, eng, max(tsteps, 1), args.probe_passes), 4)
+                    if not push:
+                        rec["exchange_us"] = round(halo_latency(env, eng, args.probe_iters) * 1e6, 2)
+                    rec["label"] = eng.transport + (" inline halo" if push else "")
+                    rec["overlap"] = eng.overlap
                 finally:
                     eng.close()
         except Exception as ex:  # a failing candidate is data, not a crash
             rec["error"] = f"{type(ex).__name__}: {ex}"[:300]
-        out[t] = rec
+        out[plane] = rec
         with open(args.probe_child, "w") as f:
             json.dump(out, f)
     gdist.shutdown()
@@ -428,8 +461,9 @@ def probe_child(args, dims, shape, tsteps, graph):
 
 def agree_transport(env, probe, kinds, margin=0.97):
     """Every rank's probe -> one choice for all: a candidate counts if it
-    passed the gate and timed on EVERY rank; its exchange time is the max over
-    ranks; IPC replaces RCCL only when it is faster by more than 3%.  Every
+    passed the gate and timed on EVERY rank; its pass time is the max over
+    ranks; another plane replaces RCCL only when its passes are faster by
+    more than 3%.  Every
     rank calls this (world > 1), probed or not, so ranks whose environments
     disagree on probing (device counts, LOCAL_WORLD_SIZE) cannot leave one
     side waiting in the collective: only kinds that every rank probed count.
@@ -446,10 +480,12 @@ def agree_transport(env, probe, kinds, margin=0.97):
         cands["_mismatch"] = {"gate": "fail", "error": f"ranks probed different kinds: {sorted(allp_kinds)}"}
     for t in common:
         recs = [(p.get(t) or {}) for p in allp]
-        ok = all(r.get("gate_max_diff") == 0.0 and r.get("exchange_us") for r in recs)
+        ok = all(r.get("gate_max_diff") == 0.0 and r.get("pass_ms") for r in recs)
         c = {"gate": "pass" if ok else "fail"}
         if ok:
-            c["exchange_us"] = max(r["exchange_us"] for r in recs)
+            c["pass_ms"] = max(r["pass_ms"] for r in recs)
+            if all(r.get("exchange_us") for r in recs):
+                c["exchange_us"] = max(r["exchange_us"] for r in recs)
             c["label"] = recs[0].get("label", t)
         else:
             whys = []
@@ -463,7 +499,7 @@ def agree_transport(env, probe, kinds, margin=0.97):
                     whys.append(f"rank {i}: {', '.join(why)}")
             c["error"] = "; ".join(whys[:4])[:600]
         cands[t] = c
-    passing = {t: c["exchange_us"] for t, c in cands.items() if c["gate"] == "pass" and not t.startswith("_")}
+    passing = {t: c["pass_ms"] for t, c in cands.items() if c["gate"] == "pass" and not t.startswith("_")}
     choice = "auto"
     if passing:
         choice = min(passing, key=passing.get)
@@ -558,7 +594,9 @@ def run_extras(args, env, solver, info, shape, points, tsteps, overlap, dims, gr
     def halo():
         if env.world_size > 1:
             extras["halo_exchange_us"] = round(halo_latency(env, solver, iters) * 1e6, 2)
-            extras["halo_exchange_kind"] = (f"{info['transport']}, {info['tsteps']}-wide faces + corners "
+            inline = info["transport"].endswith("inline halo")
+            extras["halo_exchange_kind"] = (f"{_plane(transport)[0]}{' blocking exchange (the fused passes exchange inline)' if inline else ''}, "
+                                            f"{info['tsteps']}-wide faces + corners "
                                             f"of the {shape[0]}x{shape[1]} field, process grid "
                                             f"{info['dims'][0]}x{info['dims'][1]}")
         extras["residual_l2"] = solver.residual()
@@ -610,7 +648,7 @@ def run_extras(args, env, solver, info, shape, points, tsteps, overlap, dims, gr
         extra("small-domain stencil run", small)
     if env.world_size > 1:
         def refh():
-            extras.update(ref_halo(env, args.ref_n_local, args.ref_n_other, args.ref_iters, transport))
+            extras.update(ref_halo(env, args.ref_n_local, args.ref_n_other, args.ref_iters, _plane(transport)[0]))
             bad = (extras["ref_halo_dim0_bad_ghosts"], extras["ref_halo_dim1_bad_ghosts"])
             if any(bad):
                 raise RuntimeError(f"wrong ghost cells after an exchange (dim 0: {bad[0]}, dim 1: {bad[1]})")
@@ -627,7 +665,7 @@ def run_extras(args, env, solver, info, shape, points, tsteps, overlap, dims, gr
     extra("daxpy", daxpy)
 
     def allred():
-        extras.update(daxpy_allreduce(env, args.daxpy_n, iters=20, transport=transport))
+        extras.update(daxpy_allreduce(env, args.daxpy_n, iters=20, transport=_plane(transport)[0]))
         if not extras["daxpy_allsum_rel_err"] <= 1e-9:
             raise RuntimeError(f"DAXPY ALLSUM {extras['daxpy_allsum']} differs from the closed form "
                                f"{extras['daxpy_allsum_exact']} (rel err {extras['daxpy_allsum_rel_err']:.3e})")
@@ -685,13 +723,16 @@ def main(argv=None):
                     help="hang watchdog: seconds without progress before the job fails naming the rank and "
                          "phase (GMT_TIMEOUT overrides; 0 = off)")
     ap.add_argument("--transport", choices=("auto",) + PROBE_KINDS, default="auto",
-                    help="engine data plane at N > 1 (auto: timed at start-up, see --transport-probe)")
+                    help="engine data plane at N > 1: rccl, ipc, or push (ipc mappings, every fused pass "
+                         "stores its faces into the neighbours' ghost cells; auto: timed at start-up, see "
+                         "--transport-probe)")
     ap.add_argument("--transport-probe", choices=("auto", "on", "off"), default="auto",
                     help="auto: with one rank per GPU, time RCCL and IPC (xGMI peer mappings) on the real "
                          "faces in an isolated child process group and keep the faster that passes the "
                          "bitwise gate; on: also on the CPU backend; off: RCCL")
     ap.add_argument("--probe-timeout", type=float, default=150.0, help="seconds for the transport probe")
     ap.add_argument("--probe-iters", type=int, default=50, help="timed exchanges per probed transport")
+    ap.add_argument("--probe-passes", type=int, default=6, help="timed fused passes per probed data plane")
     ap.add_argument("--probe-port", type=int, default=0, help="the probe's rendezvous port (0: MASTER_PORT+101)")
     ap.add_argument("--probe-child", type=str, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--probe-kinds", type=str, default="", help=argparse.SUPPRESS)

@@ -19,6 +19,9 @@
 //                           counts above 10 round down)
 //   --wg-strips=N --seg-rows=L   gmt_tb_opts launch shape (0 = default)
 //   --halo-iters=K          K blocking halo exchanges -> latency line
+//   --push                  inline halo exchange of the fused passes (JacobiConfig::push: the
+//                           pass stores its faces into the neighbours' ghost cells; ipc or
+//                           a single rank)
 //   --check                 rank 0 re-runs the whole problem serially on the host
 //   --json=FILE
 #include <mpi.h>
@@ -111,6 +114,7 @@ int main(int argc, char** argv) {
   if (c.tblock) c.tsteps = static_cast<int>(cli.geti("tsteps", 2));
   c.wg_waves = static_cast<int>(cli.geti("wg-strips", 0));
   c.seg_rows = static_cast<int>(cli.geti("seg-rows", 0));
+  c.push = cli.flag("push");
   // with one rank and no periodic wrap there is nothing to exchange; with a
   // periodic wrap a single rank exchanges with itself
   comm::Kind kind = comm::parse_kind(cli.get("transport", "auto"));
@@ -118,7 +122,7 @@ int main(int argc, char** argv) {
   auto tr = comm::make_transport(comm::resolve(kind, b), MPI_COMM_WORLD, b);
 
   double t_step = 0, resid = 0, halo_us = 0, max_diff = -1;
-  bool graph = false, overlap = false, band = false;
+  bool graph = false, overlap = false, band = false, push = false;
   size_t hbytes = 0, hmsgs = 0;
   int64_t lnx = 0, lny = 0;
   {
@@ -126,6 +130,7 @@ int main(int argc, char** argv) {
     graph = solver.graph_active();
     overlap = solver.overlap_active();
     band = solver.band_first();
+    push = solver.push_active();
     hbytes = solver.bytes_per_exchange();
     hmsgs = solver.messages();
     lnx = solver.nx();
@@ -189,7 +194,8 @@ int main(int argc, char** argv) {
     std::printf("global    = %lld x %lld\n", (long long)c.ny_global, (long long)c.nx_global);
     std::printf("local     = %lld x %lld (rank 0)\n", (long long)lny, (long long)lnx);
     std::printf("transport = %s overlap=%d%s graph=%d periodic=%d tblock=%d backend=%s\n", tr->name(),
-                overlap, band ? " (band-first)" : "", graph, c.periodic, c.tblock, gmt_rt_backend_name());
+                overlap, band ? " (band-first)" : (push ? " (inline halo)" : ""), graph, c.periodic, c.tblock,
+                gmt_rt_backend_name());
     std::printf("steps     = %d (warmup %d)\n", n_iter, n_warmup);
     std::printf("TIME step : %0.6f ms\n", t_step * 1e3);
     std::printf("MLUPS     : %0.1f (per GPU %0.1f, %0.1f GB/s per GPU at 16 B/pt)\n", mlups,
@@ -202,7 +208,7 @@ int main(int argc, char** argv) {
     JsonRecord j;
     j.add("app", "mpi_jacobi2d").add("ranks", world).add("py", c.py).add("px", c.px)
         .add("ny", (long long)c.ny_global).add("nx", (long long)c.nx_global).add("transport", tr->name())
-        .add("overlap", overlap).add("graph", graph).add("tblock", c.tblock).add("steps", n_iter).add("ms_per_step", t_step * 1e3)
+        .add("overlap", overlap).add("band_first", band).add("push", push).add("graph", graph).add("tblock", c.tblock).add("steps", n_iter).add("ms_per_step", t_step * 1e3)
         .add("MLUPS", mlups).add("halo_us", halo_us).add("halo_bytes", hbytes).add("residual", resid)
         .add("check_max_diff", max_diff);
     j.append_to(cli.get("json", ""));

@@ -134,7 +134,7 @@ void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank,
   if (opts) o = *opts;
   if (o.tsteps < 0 || o.tsteps > GMT_TB_MAX_SWEEPS || o.overlap < 0 || o.overlap > 2 || o.wg_waves < 0 ||
       o.wg_waves > 8 || o.seg_rows < 0 || o.exact < -1 || o.exact > 1 || o.init < 0 || o.init > 1 ||
-      o.calibrate < 0 || o.calibrate > 1 || o.seed < 0 || o.seed >= (int64_t(1) << 53))
+      o.calibrate < 0 || o.calibrate > 1 || o.seed < 0 || o.seed >= (int64_t(1) << 53) || o.push < 0 || o.push > 1)
     return nullptr;
   auto* h = new Handle();
   h->t = gmt::engine_transport(rank, world, transport, ccl_id);
@@ -160,6 +160,7 @@ void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank,
   c.init = o.init;
   c.seed = static_cast<uint64_t>(o.seed);
   c.calibrate = o.calibrate != 0;
+  c.push = o.push != 0;
   h->py = py;
   h->px = px;
   h->s = std::make_unique<gmt::JacobiSolver>(*h->t, c);
@@ -209,6 +210,7 @@ int gmt_engine_jacobi_info(void* p, int64_t* out) {
   out[12] = static_cast<int64_t>(s.tuned_serial_s() * 1e9);
   out[13] = s.exact();
   out[14] = s.band_first();
+  out[15] = s.push_active();
   return 0;
 }
 int gmt_engine_jacobi_plan(void* p, int steps, int* out, int max) {

@@ -1,12 +1,16 @@
 // Native distributed Jacobi engine (gmt/jacobi.hpp).
 #include "gmt/jacobi.hpp"
+#include "gmt/control.hpp"
 #include "gmt/kernels.h"
 #include "gmt/util.hpp"
 
 #include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -85,7 +89,10 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   g_ = ks_;
   yo_ = g_;
   xo_ = round_up(g_, 8);  // ghost columns fit left of the interior; 64-B aligned interior
-  ld_ = round_up(xo_ + nx_ + g_, 64);
+  // one row pitch on every rank (the largest share's): the inline halo
+  // exchange addresses a neighbour's cells with this rank's pitch
+  const int64_t nx_max = (c.nx_global + c.px - 1) / c.px;
+  ld_ = round_up(xo_ + nx_max + g_, 64);
   const size_t elems = static_cast<size_t>(ld_) * (ny_ + 2 * g_);
   GMT_CHECK("stream", gmt_rt_stream_create(&s_, 0));
   // exchange stream priority: high by default; GMT_COMM_PRIORITY=0 for A/B
@@ -117,9 +124,10 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
     halo_[b] = std::make_unique<Halo2D>(t_, f, g_, g_, nb_, false, GMT_SPACE_DEVICE, ks_ > 1);
   }
   if (const char* e = std::getenv("GMT_PACK_WGS")) beside_pack_wgs_ = std::max(0, std::atoi(e));
-  if (ks_ > 1 && halo_[0]->active() && (c.overlap || c.overlap_auto)) split_cus();
+  if (c.push && ks_ > 1 && halo_[0]->active()) setup_push();
+  if (!push_on_ && ks_ > 1 && halo_[0]->active() && (c.overlap || c.overlap_auto)) split_cus();
   watchdog_kick("jacobi: halo plans ready");
-  if (c.overlap_auto) autotune_overlap();
+  if (c.overlap_auto && !push_on_) autotune_overlap();
   if (c.graph) capture_graphs();
   watchdog_kick("jacobi: ready");
 }
@@ -207,7 +215,7 @@ void JacobiSolver::calibrate_costs() {
   watchdog_kick("jacobi: pass-cost calibration");
   std::vector<int> ks;
   for (int K = 1; K <= ks_; ++K)
-    if (K == 1 || gmt_jacobi5tb_supported(K)) ks.push_back(K);
+    if (K == 1 || (push_on_ ? gmt_jacobi5tb_push_supported(K) : gmt_jacobi5tb_supported(K))) ks.push_back(K);
   Buffer<double> d(ks.size(), GMT_SPACE_DEVICE);
   std::vector<double> host(ks.size(), 1e300);
   constexpr int kSweeps = 2;
@@ -296,6 +304,7 @@ void JacobiSolver::autotune_overlap() {
 
 JacobiSolver::~JacobiSolver() {
   if (s_) gmt_rt_stream_synchronize(s_);
+  for (void* b : push_opened_) GMT_WARN("ipc close", gmt_rt_ipc_close(b));
   if (cs_) gmt_rt_stream_synchronize(cs_);
   if (sb_) gmt_rt_stream_synchronize(sb_);
   for (auto& g : graph_) gmt_rt_graph_destroy(g);
@@ -410,6 +419,10 @@ void JacobiSolver::exchange_now(int parity) {
 // segments): no frame pass, no redundant work (the core/frame scheme of
 // round 1 cost 2-11 % per pass, profiles/r02_shares.md).
 void JacobiSolver::enqueue_block(int parity, int K) {
+  if (push_on_) {
+    push_block(parity, K);
+    return;
+  }
   Halo2D& h = *halo_[parity];
   const int64_t dom[4] = {xo_, nx_, yo_, ny_};
   if (!h.active()) {
@@ -446,6 +459,137 @@ void JacobiSolver::enqueue_block(int parity, int K) {
   hn.set_pack_wgs(0);
   GMT_CHECK("event", gmt_rt_event_record(ev_halo_, cs_));
   GMT_CHECK("wait", gmt_rt_stream_wait_event(s_, ev_halo_));
+  fresh_[parity ^ 1] = true;
+}
+
+// ---- inline halo exchange (cfg_.push) ----
+//
+// Each fused pass stores its output's face cells a second time, straight
+// into the ghost cells of the neighbours' next input buffer
+// (gmt_tb_opts.push, csrc/kernels/jacobi5tb.hpp): the S / N faces (the
+// first / last g_ rows of the interior), W / E faces (the first / last g_
+// columns) and the g_ x g_ corners for the diagonal neighbours.  No pack,
+// exchange or unpack launch: one hand-over launch after the pass
+// (gmt_push_sync) tells every neighbour "my pass is done" and waits for
+// theirs, so the next pass reads complete ghost cells and no rank writes a
+// buffer its neighbour still reads (a neighbour pushes into this rank's
+// buffer b^1 only during its pass p, which starts after this rank's pass
+// p - 1 — the last reader of b^1 — handed over).  The round-4 traces showed
+// why an exchange cannot hide beside a pass that holds every CU: its
+// kernels only get registers as the pass drains (profiles/r04_overlap.md).
+// Written by the pass itself, the faces cost a few store instructions per
+// step of the boundary strips and segments.
+namespace {
+constexpr int kPushOpp[8] = {GMT_PUSH_N, GMT_PUSH_S, GMT_PUSH_E, GMT_PUSH_W,
+                             GMT_PUSH_NE, GMT_PUSH_NW, GMT_PUSH_SE, GMT_PUSH_SW};
+constexpr int kPushTag = 40000;  // + the direction, seen from the sender
+struct PushWire {
+  gmt_ipc_handle h[3];  // buf_[0], buf_[1], the flag slots
+  uint64_t off[3];
+  int64_t nx, ny, ld;
+};
+}  // namespace
+
+void JacobiSolver::setup_push() {
+  const JacobiConfig& c = cfg_;
+  const int me = t_.rank();
+  const int nbr[8] = {nb_.south, nb_.north, nb_.west, nb_.east, nb_.sw, nb_.se, nb_.nw, nb_.ne};
+  // The kernel's rules (gmt_tb_opts.push) on the smallest share, so every
+  // rank takes the same decision: an even face width, two segments clear of
+  // each other's face, two strips (wider than any pass's strip output).
+  const int64_t ny_min = c.ny_global / c.py, nx_min = c.nx_global / c.px;
+  if ((g_ & 1) || g_ > 64 || ny_min < 2 * g_ + 2 || nx_min <= 256 || !gmt_jacobi5tb_push_supported(ks_)) return;
+  bool remote = false;
+  for (int d = 0; d < 8; ++d) remote = remote || (nbr[d] >= 0 && nbr[d] != me);
+  comm::Control* ctl = t_.control();
+  // no control plane for the mappings (rccl): the transport's exchange (the
+  // same on every rank: one transport kind per job)
+  if (remote && !ctl) return;
+  push_flags_ = Buffer<uint64_t>(8, GMT_SPACE_FLAGS);
+  GMT_CHECK("push flags", gmt_rt_memset_async(push_flags_.data(), 0, push_flags_.bytes(), s_));
+  GMT_CHECK("push flags", gmt_rt_stream_synchronize(s_));
+  push_err_ = Buffer<unsigned>(1, GMT_SPACE_PINNED);
+  *push_err_.data() = 0;
+  PushWire mine;
+  std::memset(&mine, 0, sizeof(mine));
+  void* own[3] = {buf_[0].data(), buf_[1].data(), push_flags_.data()};
+  if (remote)
+    for (int i = 0; i < 3; ++i) {
+      size_t off = 0;
+      GMT_CHECK("ipc handle", gmt_rt_ipc_get_handle(&mine.h[i], &off, own[i]));
+      mine.off[i] = off;
+    }
+  mine.nx = nx_;
+  mine.ny = ny_;
+  mine.ld = ld_;
+  std::vector<PushWire> in(8);
+  std::vector<comm::HostMsg> rs, ss;
+  for (int d = 0; d < 8; ++d) {
+    if (nbr[d] < 0 || nbr[d] == me) continue;
+    rs.push_back({&in[d], sizeof(PushWire), nbr[d], kPushTag + kPushOpp[d]});
+    ss.push_back({&mine, sizeof(PushWire), nbr[d], kPushTag + d});
+  }
+  if (!rs.empty()) ctl->exchange(rs, ss);
+  std::map<std::string, void*> opened;  // a handle maps once per process
+  auto open = [&](const gmt_ipc_handle& h, uint64_t off) -> char* {
+    const std::string k(reinterpret_cast<const char*>(h.bytes), sizeof(h.bytes));
+    auto it = opened.find(k);
+    if (it == opened.end()) {
+      void* base = nullptr;
+      GMT_CHECK("ipc open", gmt_rt_ipc_open(&base, &h));
+      push_opened_.push_back(base);
+      it = opened.emplace(k, base).first;
+    }
+    return static_cast<char*>(it->second) + off;
+  };
+  for (int d = 0; d < 8; ++d) {
+    if (nbr[d] < 0) continue;
+    const bool self = nbr[d] == me;
+    if (!self && in[d].ld != ld_) {
+      std::printf("JacobiSolver: rank %d's row pitch %lld differs from rank %d's %lld\n", nbr[d],
+                  static_cast<long long>(in[d].ld), me, static_cast<long long>(ld_));
+      abort_job(EXIT_FAILURE);
+    }
+    const int64_t onx = self ? nx_ : in[d].nx, ony = self ? ny_ : in[d].ny;
+    // this rank's face cell (x, y) -> the neighbour's ghost cell (x + tx, y + ty)
+    const bool wside = d == GMT_PUSH_W || d == GMT_PUSH_SW || d == GMT_PUSH_NW;
+    const bool eside = d == GMT_PUSH_E || d == GMT_PUSH_SE || d == GMT_PUSH_NE;
+    const bool sside = d == GMT_PUSH_S || d == GMT_PUSH_SW || d == GMT_PUSH_SE;
+    const bool nside = d == GMT_PUSH_N || d == GMT_PUSH_NW || d == GMT_PUSH_NE;
+    const int64_t tx = wside ? onx : (eside ? -nx_ : 0);
+    const int64_t ty = sside ? ony : (nside ? -ny_ : 0);
+    for (int b = 0; b < 2; ++b) {
+      // a pass reading buffer b writes b ^ 1: its faces go to the
+      // neighbour's b ^ 1, the neighbour's input of the next pass
+      const char* t = self ? reinterpret_cast<const char*>(buf_[b ^ 1].data()) : open(in[d].h[b ^ 1], in[d].off[b ^ 1]);
+      push_base_[b][d] = reinterpret_cast<const double*>(
+          reinterpret_cast<uintptr_t>(t) + static_cast<uintptr_t>((ty * ld_ + tx) * static_cast<int64_t>(sizeof(double))));
+    }
+    if (!self) {
+      push_remote_[d] = reinterpret_cast<uint64_t*>(open(in[d].h[2], in[d].off[2])) + kPushOpp[d];
+      push_mask_ |= 1 << d;
+    }
+  }
+  push_on_ = true;
+  cfg_.overlap = false;  // no band-first passes: the exchange is inline
+}
+
+void JacobiSolver::push_block(int parity, int K) {
+  if (!fresh_[parity]) exchange_now(parity);
+  const int64_t dom[4] = {xo_, nx_, yo_, ny_};
+  gmt_tb_opts o{};
+  o.sweeps = K;
+  o.wg_waves = cfg_.wg_waves;
+  o.exact = exact_ ? 1 : 0;
+  for (int d = 0; d < 8; ++d) o.push[d] = push_base_[parity][d];
+  o.push_w = g_;
+  GMT_CHECK("jacobi tb (inline halo)", gmt_jacobi5tb(&o, 1, dom, dom, halo_mask(), buf_[parity].data(),
+                                                     buf_[parity ^ 1].data(), ld_, ny_ + 2 * g_, s_));
+  if (push_mask_) {
+    ++push_epoch_;
+    GMT_CHECK("push hand-over", gmt_push_sync(push_flags_.data(), push_remote_, push_mask_, push_epoch_,
+                                             push_err_.data(), s_));
+  }
   fresh_[parity ^ 1] = true;
 }
 
@@ -506,7 +650,7 @@ double JacobiSolver::table_pass_ms(int K) const {
   const PassCosts& tab = std::fabs(std::log(pts / kCostLarge.points)) < std::fabs(std::log(pts / kCostSmall.points))
                              ? kCostLarge
                              : kCostSmall;
-  if (tab.ms[K] <= 0) return 0.0;
+  if (tab.ms[K] <= 0 || (push_on_ && K > 1 && !gmt_jacobi5tb_push_supported(K))) return 0.0;
   const bool exchanges = t_.size() > 1 || c.periodic;  // the same on every rank
   const double over = kLaunchMs + (exchanges && !c.overlap ? kExchangeMs : 0.0);
   return tab.ms[K] * pts / tab.points + over;
@@ -588,7 +732,7 @@ void JacobiSolver::capture_graphs() {
   GMT_CHECK("sync", gmt_rt_stream_synchronize(cs_));
   const bool saved[2] = {fresh_[0], fresh_[1]};
   for (int p = 0; p < 4; ++p) {
-    if (p >= 2 && ks_ < 2) break;
+    if (p >= 2 && (ks_ < 2 || push_on_)) break;  // inline-halo passes carry a per-pass epoch: eager
     // serial passes capture their exchange, band-first ones start from a
     // current halo (step_block makes sure of it)
     fresh_[0] = fresh_[1] = p >= 2 && band_mode(ks_);
@@ -641,6 +785,11 @@ void JacobiSolver::synchronize() {
       abort_job(EXIT_FAILURE);
     }
     band_ran_ = false;
+  }
+  if (push_on_ && push_mask_ && *push_err_.data() != 0) {
+    std::printf("JacobiSolver: an inline-halo hand-over timed out waiting for the neighbours in directions "
+                "0x%x (GMT_WAIT_TIMEOUT_MS); ghost cells are stale\n", *push_err_.data());
+    abort_job(EXIT_FAILURE);
   }
   // a halo exchange that timed out (IPC) left stale ghost cells: fail loudly
   for (auto& h : halo_)

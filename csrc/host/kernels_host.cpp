@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <sched.h>
+#include <thread>
 
 #include <cstring>
 #include <vector>
@@ -257,6 +258,7 @@ static int host_xk(int K, int n_rect, const int64_t* rects, const int64_t* dom, 
 }
 
 int gmt_jacobi5tb_supported(int K) { return (K >= 1 && K <= 10) || (K > 10 && K <= GMT_TB_MAX_SWEEPS && K % 2 == 0); }
+int gmt_jacobi5tb_push_supported(int K) { return gmt_jacobi5tb_supported(K) && gmt::tb::tb_push_built(K); }
 int gmt_jacobi5tb_max_sweeps(int exact) { return exact ? 18 : GMT_TB_MAX_SWEEPS; }  // as the gfx950 build
 
 // CPU backend of csrc/kernels/jacobi5tb.hip: same argument checks, reference loops
@@ -281,9 +283,61 @@ int gmt_jacobi5tb(const gmt_tb_opts* o, int n_rect, const int64_t* rects, const 
     const int rb = ((mask & 4) ? 1 : 0) + ((mask & 8) ? 1 : 0);
     if (rb == 0 || rects[4 * o->signal_rects + 3] < rb * std::max<int64_t>(32, o->signal_rows)) return 1;
   }
+  const int64_t w = o->push_w;
+  if (w < 0) return 1;
+  if (w > 0) {  // inline halo exchange: the GPU launcher's rules (jacobi5tb.hpp launch_tb)
+    bool ok = gmt::tb::tb_push_built(K) && n_rect == 1 && w <= 64 && (w & 1) == 0 && !sig && o->seg_rows == 0 && dom[1] >= w && dom[3] >= 2 * w + 2;
+    for (int j = 0; ok && j < 4; ++j) ok = rects[j] == dom[j];
+    const int64_t wout = gmt::tb::tb_strip_out(K);
+    if (ok && o->push[GMT_PUSH_W] && o->push[GMT_PUSH_E] && (dom[1] + wout - 1) / wout < 2) ok = false;
+    if (ok && dom[1] < wout && (dom[1] & 1)) ok = false;  // the GPU kernel's odd-edge stores
+    if (!ok) return 1;
+  }
   const int rc = host_xk(K, n_rect, rects, dom, mask, u, un, ld);
+  if (rc == 0 && w > 0) {
+    // the faces of the output, a second time, into the neighbours' ghost cells
+    const int64_t x0 = dom[0], x1 = dom[0] + dom[1], y0 = dom[2], y1 = dom[2] + dom[3];
+    auto put = [&](int d, int64_t xa, int64_t xb, int64_t ya, int64_t yb) {
+      double* t = const_cast<double*>(o->push[d]);
+      if (!t) return;
+      for (int64_t y = ya; y < yb; ++y)
+        for (int64_t x = xa; x < xb; ++x) t[y * ld + x] = un[y * ld + x];
+    };
+    put(GMT_PUSH_S, x0, x1, y0, y0 + w);
+    put(GMT_PUSH_N, x0, x1, y1 - w, y1);
+    put(GMT_PUSH_W, x0, x0 + w, y0, y1);
+    put(GMT_PUSH_E, x1 - w, x1, y0, y1);
+    put(GMT_PUSH_SW, x0, x0 + w, y0, y0 + w);
+    put(GMT_PUSH_SE, x1 - w, x1, y0, y0 + w);
+    put(GMT_PUSH_NW, x0, x0 + w, y1 - w, y1);
+    put(GMT_PUSH_NE, x1 - w, x1, y1 - w, y1);
+  }
   if (rc == 0 && sig) __atomic_fetch_add(o->signal, uint64_t{1}, __ATOMIC_RELEASE);
   return rc;
+}
+
+// CPU backend of gmt_push_sync (csrc/kernels/ipc.hip): the same hand-over on
+// memfd-shared flag words, waits bounded by GMT_WAIT_TIMEOUT_MS of wall clock
+int gmt_push_sync(const uint64_t* local, uint64_t* const remote[8], int mask, uint64_t epoch, unsigned* err, void*) {
+  if (!local || !err || mask < 0 || mask > 255) return 1;
+  for (int d = 0; d < 8; ++d)
+    if (((mask >> d) & 1) && (!remote || !remote[d])) return 1;
+  for (int d = 0; d < 8; ++d)
+    if ((mask >> d) & 1) __atomic_store_n(remote[d], epoch, __ATOMIC_RELEASE);
+  const char* e = std::getenv("GMT_WAIT_TIMEOUT_MS");
+  const double limit = (e && std::atof(e) > 0 ? std::atof(e) : 10000.0) / 1e3;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int d = 0; d < 8; ++d) {
+    if (!((mask >> d) & 1)) continue;
+    while (__atomic_load_n(local + d, __ATOMIC_ACQUIRE) < epoch) {
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+        __atomic_fetch_or(err, 1u << d, __ATOMIC_RELAXED);
+        break;
+      }
+      std::this_thread::yield();
+    }
+  }
+  return 0;
 }
 
 int64_t gmt_jacobi5tb_group_cols(int sweeps, int wg_waves) {

@@ -44,6 +44,7 @@ typedef struct gmt_engine_opts {
   int calibrate; /* 1: prepare() times every fused-pass size on the real share and the
                     planner uses those costs instead of the built-in table */
   int64_t seed;
+  int push;     /* 1: inline halo exchange of the fused passes (JacobiConfig::push) */
 } gmt_engine_opts;
 /* id: 128 bytes (RCCL unique id / control id) or NULL (local); NULL on invalid options */
 void* gmt_engine_jacobi_create(int64_t ny, int64_t nx, int py, int px, int rank, int world,
@@ -53,8 +54,9 @@ int gmt_engine_jacobi_run(void* h, int steps); /* enqueue `steps` steps */
 int gmt_engine_jacobi_sync(void* h);
 double gmt_engine_jacobi_residual(void* h);
 int gmt_engine_jacobi_exchange(void* h); /* one blocking halo exchange */
-/* out[14]: nx, ny, off_x, off_y, bytes_per_exchange, messages, graph, overlap, py, px, tsteps,
- * overlap_auto ns per pass with overlap, without (0 if not tuned), exact arithmetic in use */
+/* out[16]: nx, ny, off_x, off_y, bytes_per_exchange, messages, graph, overlap, py, px, tsteps,
+ * overlap_auto ns per pass with overlap, without (0 if not tuned), exact arithmetic in use,
+ * band-first passes, inline halo exchange in use */
 int gmt_engine_jacobi_info(void* h, int64_t* out);
 /* The fused passes (sweeps per pass, in launch order) that run(steps) enqueues:
  * writes min(n, max) entries, returns n. */

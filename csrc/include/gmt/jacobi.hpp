@@ -75,6 +75,15 @@ struct JacobiConfig {
   // share (max over ranks) and plan_passes uses those costs instead of the
   // built-in table (measured on one box for one kernel revision)
   bool calibrate = false;
+  // Inline halo exchange (fused passes; gmt_tb_opts.push): every pass
+  // stores its output faces straight into the neighbours' ghost cells of
+  // their next input (IPC mappings traded over the transport's control
+  // plane; this rank's own buffers on a periodic axis), then one small
+  // hand-over launch (gmt_push_sync) replaces the halo exchange.  Needs a
+  // transport with a control plane (ipc) unless every neighbour is this
+  // rank; off (the transport's exchange as before) when the share is too
+  // small for the kernel's push rules.
+  bool push = false;
 };
 
 class JacobiSolver {
@@ -112,7 +121,9 @@ class JacobiSolver {
   bool tblock() const { return ks_ > 1; }
   int tsteps() const { return ks_; }
   int ghost() const { return g_; }
-  bool overlap_active() const { return cfg_.overlap && halo_[0] && halo_[0]->active(); }
+  bool overlap_active() const { return push_on_ || (cfg_.overlap && halo_[0] && halo_[0]->active()); }
+  // the fused passes exchange their halo inline (cfg_.push took effect)
+  bool push_active() const { return push_on_; }
   // the fused passes overlap band-first (enqueue_block)
   bool band_first() const { return ks_ > 1 && band_mode(ks_); }
   const Neighbors& neighbors() const { return nb_; }
@@ -145,6 +156,8 @@ class JacobiSolver {
   double measure_max_abs();
   int halo_mask() const;
   void split_cus();
+  void setup_push();
+  void push_block(int parity, int k);  // one inline-halo pass + its hand-over
 
   comm::Transport& t_;
   JacobiConfig cfg_;
@@ -182,6 +195,18 @@ class JacobiSolver {
   double meas_ms_[GMT_TB_MAX_SWEEPS + 1] = {};
   bool calibrated_ = false;
   double umax_ = 0.0;  // max |u| of the initial field over every rank
+  // inline halo exchange (setup_push): per parity of the pass's INPUT, the
+  // push targets (gmt_tb_opts.push) — the neighbours' other buffer with the
+  // face translation folded in; the neighbours' flag slots for this rank;
+  // the directions that are other ranks; the hand-over epoch
+  bool push_on_ = false;
+  const double* push_base_[2][8] = {};
+  uint64_t* push_remote_[8] = {};
+  int push_mask_ = 0;
+  uint64_t push_epoch_ = 0;
+  Buffer<uint64_t> push_flags_;  // [d]: written by the neighbour in direction d
+  Buffer<unsigned> push_err_;    // host-visible: bit d = the wait for direction d expired
+  std::vector<void*> push_opened_;
 };
 
 // Balanced block split of n over p parts: offset and length of part i.

@@ -181,8 +181,29 @@ typedef struct gmt_tb_opts {
      are ready after the first round of workgroups, with no band rects of
      their own (no extra strips, segments or pipeline warm-ups). */
   int signal_cols;
+  /* Inline halo exchange ("push", 0 = off): the pass stores its output's
+     face cells a second time, straight into the ghost cells of the
+     neighbours' NEXT input field — no pack, copy or exchange kernel.  For
+     direction d (GMT_PUSH_S .. GMT_PUSH_NE), output cell (x, y) of a face
+     goes to push[d] + (y * ld + x) doubles (the engine folds the
+     neighbour's buffer and the translation into push[d]; IPC-mapped memory
+     of another process or device, or this rank's own other buffer on a
+     periodic axis); NULL = no neighbour that way.  Faces: rows [y0, y0 +
+     push_w) to S, [y1 - push_w, y1) to N, columns [x0, x0 + push_w) to W,
+     [x1 - push_w, x1) to E, their w x w intersections to the diagonals, of
+     the one rect (which must be `dom`).  Needs: push_w even and <= 64;
+     two strips or more when both W and E are pushed (a strip pushes one
+     x face); the segment planner keeps every segment clear of one of the
+     S / N faces; no completion signal options; rects of even width or
+     wider than a strip (no odd-edge stores). */
+  const double* push[8];
+  int push_w;
 } gmt_tb_opts;
+enum { GMT_PUSH_S = 0, GMT_PUSH_N = 1, GMT_PUSH_W = 2, GMT_PUSH_E = 3,
+       GMT_PUSH_SW = 4, GMT_PUSH_SE = 5, GMT_PUSH_NW = 6, GMT_PUSH_NE = 7 };
 int gmt_jacobi5tb_supported(int sweeps);
+/* gmt_jacobi5tb_supported and an inline-halo (gmt_tb_opts.push) kernel is built */
+int gmt_jacobi5tb_push_supported(int sweeps);
 /* Largest sweep count whose kernel runs without scratch: GMT_TB_MAX_SWEEPS
  * for the scaled form, 18 with exact = 1 (planners stay at or below it). */
 int gmt_jacobi5tb_max_sweeps(int exact);
@@ -203,6 +224,17 @@ int gmt_jacobi5tb_plan(const gmt_tb_opts* opts, int n_rect, const int64_t* rects
  * GMT_WAIT_TIMEOUT_MS of device wall clock (default 10 s) and sets bit 2 of
  * *err.  All three in GMT_SPACE_FLAGS memory. */
 int gmt_signal_wait(const uint64_t* signal, uint64_t* seen, unsigned* err, void* stream);
+
+/* Hand-over between two inline-halo passes (gmt_tb_opts.push), one launch
+ * on `stream` after the pushing pass: for every direction d set in `mask`,
+ * stores `epoch` into *remote[d] (this rank's flag slot in the neighbour's
+ * memory, IPC-mapped; system-scope release), then waits until local[d] >=
+ * epoch (the neighbour's faces are in this rank's ghost cells) and acquires
+ * on every XCD.  Each wait is bounded by GMT_WAIT_TIMEOUT_MS of device wall
+ * clock (default 10 s); an expired one ORs 1 << d into *err (host-visible)
+ * and gives up.  local / remote: GMT_SPACE_FLAGS memory. */
+int gmt_push_sync(const uint64_t* local, uint64_t* const remote[8], int mask, uint64_t epoch, unsigned* err,
+                  void* stream);
 
 /* ---- Stream-ordered IPC exchange (csrc/kernels/ipc.hip), one launch per
  *      exchange of a persistent plan: e = *epoch + 1.  Send channel: wait

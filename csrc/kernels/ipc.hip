@@ -170,6 +170,49 @@ __global__ __launch_bounds__(kWave) void signal_wait_kernel(const uint64_t* sign
   __hip_atomic_store(seen, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// gmt_push_sync: the hand-over between two inline-halo passes (the pass
+// kernel stored its output faces straight into the neighbours' ghost cells,
+// gmt_tb_opts.push).  One workgroup per XCD (workgroups are dealt to the 8
+// XCDs round robin): workgroup 0 tells every neighbour that this rank's
+// pass, faces included, is complete; every workgroup then waits for every
+// neighbour's word and acquires at system scope, so no XCD's L2 keeps a
+// stale copy of the ghost cells the neighbours just wrote.  Why push and
+// not pull: a strided W / E face would need its own exchange launch between
+// the passes (pack or copy kernel, the 9-10% of round 4); written by the
+// pass itself it costs a few store instructions and this launch.
+struct PushSyncArgs {
+  const uint64_t* local;
+  uint64_t* remote[8];
+  uint64_t epoch;
+  unsigned* err;
+  uint64_t ticks;
+  int mask;
+};
+
+__global__ __launch_bounds__(kWave) void push_sync_kernel(PushSyncArgs a) {
+  const int d = threadIdx.x;
+  const bool mine = d < 8 && ((a.mask >> d) & 1);
+  if (blockIdx.x == 0 && mine) {
+    // the pass's face stores are complete: its waves drained vmcnt and the
+    // pass finished before this launch (stream order)
+    __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope
+    __hip_atomic_store(a.remote[d], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (mine) {
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(const_cast<uint64_t*>(a.local + d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) <
+           a.epoch) {
+      __builtin_amdgcn_s_sleep(2);
+      if (wall_clock64() - t0 > a.ticks) {
+        __hip_atomic_fetch_or(a.err, 1u << d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope, on this workgroup's XCD
+}
+
 // per-wait bound in device wall-clock ticks (GMT_WAIT_TIMEOUT_MS, default 10 s)
 uint64_t timeout_ticks() {
   static int dev_cached = -1;
@@ -257,5 +300,24 @@ extern "C" int gmt_ipc_exchange(const gmt_ipc_plan* p, void* stream) {
   a.rb = p->recv_chunks < ipc::kMaxRoleBlocks ? p->recv_chunks : ipc::kMaxRoleBlocks;
   if (a.sb + a.rb < 1) return static_cast<int>(hipErrorInvalidValue);
   ipc::ipc_exchange_kernel<<<grid_1d(a.sb + a.rb), kBlock, 0, static_cast<hipStream_t>(stream)>>>(a);
+  GMT_RET_LAUNCH();
+}
+
+extern "C" int gmt_push_sync(const uint64_t* local, uint64_t* const remote[8], int mask, uint64_t epoch, unsigned* err,
+                             void* stream) {
+  using namespace gmt;
+  if (!local || !err || mask < 0 || mask > 255) return static_cast<int>(hipErrorInvalidValue);
+  ipc::PushSyncArgs a{};
+  a.local = local;
+  for (int d = 0; d < 8; ++d) {
+    a.remote[d] = remote ? remote[d] : nullptr;
+    if (((mask >> d) & 1) && !a.remote[d]) return static_cast<int>(hipErrorInvalidValue);
+  }
+  a.epoch = epoch;
+  a.err = err;
+  a.ticks = ipc::timeout_ticks();
+  a.mask = mask;
+  if (mask == 0) return 0;
+  ipc::push_sync_kernel<<<kNumXcd, kWave, 0, static_cast<hipStream_t>(stream)>>>(a);
   GMT_RET_LAUNCH();
 }

@@ -98,6 +98,7 @@ extern "C" int gmt_jacobi5tb_supported(int sweeps) {
 // The exact (1/4 per level) K = 20 kernel needs one VGPR more than the 256 of
 // 2 waves per SIMD and spills 8 B per lane (tests/test_kernel_resources.py):
 // it exists for the kernel-level API, but planners use at most 18 exact sweeps.
+extern "C" int gmt_jacobi5tb_push_supported(int K) { return gmt_jacobi5tb_supported(K) && tb_push_built(K); }
 extern "C" int gmt_jacobi5tb_max_sweeps(int exact) { return exact ? 18 : GMT_TB_MAX_SWEEPS; }
 
 namespace {

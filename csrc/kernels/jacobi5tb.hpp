@@ -121,7 +121,17 @@ struct Args {
   // sig_wgs leading workgroups)
   int cb_rect;                   // -1: none
   int cb_lo, cb_hi;
+  // inline halo exchange (gmt_tb_opts.push, the PUSH kernels): output cell
+  // (x, y) of a face is stored a second time at push[d] + y * ld + x, in the
+  // ghost cells of the neighbour's next input; nullptr: no neighbour that way
+  const double* push[8];
+  int64_t push_w;                // face width
 };
+
+// cache policy of the face stores into a neighbour's memory: system scope
+// (sc0 | sc1: written through to the memory that owns them, complete when
+// the wave's vmcnt drains) and streaming (nt)
+constexpr int kPushAux = 1 | 2 | 16;
 
 // NC doubles of one strip row held by a lane (its columns c0 .. c0+NC-1)
 template <int NC>
@@ -218,10 +228,10 @@ __device__ __forceinline__ u2 pack1(double a) {
 // runtime one costs the unrolled body its register allocation,
 // tests/test_kernel_resources.py); sig_step >= 0: once that step's row is
 // stored, this (output) wave publishes a row-band arrival (Args::rb_rect).
-template <int K, int J, bool EXACT, bool EDGE, bool RULE, bool UP>
+template <int K, int J, bool EXACT, bool EDGE, bool RULE, bool UP, bool PUSH>
 __device__ __forceinline__ void run_stage(const Args& a, const double* __restrict__ u, double* __restrict__ un,
                                           char* ring, int lane, int64_t xs, int64_t xe, int64_t ys, int64_t ye,
-                                          int nsteps, int sig_step) {
+                                          int nsteps, int sig_step, int xd) {
   using C = Cfg<K>;
   constexpr int NC = C::NC;
   constexpr int PB = J * C::NL + 1, PE = (J + 1) * C::NL;
@@ -232,7 +242,9 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   constexpr int kP = C::P, kRS = C::RS, kHS = C::HS;
   constexpr uint32_t kRow = C::ROW;
   constexpr int D = C::DLAG * J;                     // step lag behind stage 0
-  constexpr int SPS = kOut ? (EDGE ? NC : NC / 2) : 0;  // global stores per step
+  // global stores per step (PUSH: three face groups more, see below)
+  constexpr int SPS = kOut ? (EDGE ? NC : (PUSH ? 4 : 1) * (NC / 2)) : 0;
+  static_assert(!(PUSH && EDGE), "inline halo exchange: no odd-edge stores");
   // DMAs per step.  Narrow strips: stage 0 loads the whole row.  Wide strips:
   // stage q < NDMA loads the row's q-th 1-KB piece (an LDS-DMA costs ~60
   // issue cycles: three on one wave made stage 0 the pole of every step
@@ -338,6 +350,50 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
     stp[q] = (ina && inb) ? static_cast<uint32_t>(ca - xs) * 8u : kDrop;
     sts[q] = (ina && !inb) ? static_cast<uint32_t>(ca - xs) * 8u : kDrop;
   }
+  // Inline halo exchange (PUSH, output stage; gmt_tb_opts.push): the face
+  // cells of this strip's output are stored a second time, into the
+  // neighbours' ghost cells — the y face this segment holds (S or N rows),
+  // the x face this strip holds (xd: W or E columns; per-lane offsets xp),
+  // and their corner (diagonal neighbour).  All three store groups are
+  // issued every step: a descriptor with nothing of this wave's output in
+  // range (a face this wave does not hold, a row outside the face) drops
+  // them in the buffer unit, with no branch in the unrolled step.
+  __amdgpu_buffer_rsrc_t prs_y = row_rsrc(un, 0), prs_x = row_rsrc(un, 0), prs_c = row_rsrc(un, 0);
+  uint32_t psh = 0;  // the y face's first row relative to ys, in bytes
+  uint32_t xp[NC / 2];
+  if constexpr (PUSH && kOut) {
+    const int64_t w = a.push_w;
+    int yd = -1;
+    int64_t fy0 = 0, fy1 = 0;
+    if (a.push[GMT_PUSH_S] && ys < dy0 + w) {
+      yd = GMT_PUSH_S;
+      fy0 = ys > dy0 ? ys : dy0;
+      fy1 = ye < dy0 + w ? ye : dy0 + w;
+    } else if (a.push[GMT_PUSH_N] && ye > dy1 - w) {
+      yd = GMT_PUSH_N;
+      fy0 = ys > dy1 - w ? ys : dy1 - w;
+      fy1 = ye < dy1 ? ye : dy1;
+    }
+    auto face = [&](int d, int64_t row0, int64_t rows) {
+      return row_rsrc(a.push[d] + row0 * ld + xs, static_cast<uint32_t>(rows) * ld8);
+    };
+    if (yd >= 0) {
+      prs_y = face(yd, fy0, fy1 - fy0);
+      psh = static_cast<uint32_t>(fy0 - ys) * ld8;
+    }
+    if (xd >= 0) {
+      prs_x = face(xd, ys, L);
+      const int cd = yd < 0 ? -1 : (yd == GMT_PUSH_S ? (xd == GMT_PUSH_W ? GMT_PUSH_SW : GMT_PUSH_SE)
+                                                      : (xd == GMT_PUSH_W ? GMT_PUSH_NW : GMT_PUSH_NE));
+      if (cd >= 0 && a.push[cd]) prs_c = face(cd, fy0, fy1 - fy0);
+    }
+    const int64_t fx0 = xd == GMT_PUSH_W ? dx0 : dx1 - w;
+#pragma unroll
+    for (int q = 0; q < NC / 2; ++q) {
+      const int64_t ca = c0 + 2 * q;
+      xp[q] = (xd >= 0 && ca >= fx0 && ca + 1 < fx0 + w) ? stp[q] : kDrop;
+    }
+  }
   auto store_step = [&](int s, const dv<NC>& v) {  // level K of step s = output row s - D - 2K of the walk
     if constexpr (kOut) {
       const uint32_t ro = sbase + static_cast<uint32_t>(s - D - 2 * K) * rstep;  // warm-up rows: out of range
@@ -345,6 +401,18 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
         constexpr int q = decltype(Q)::value;
         __builtin_amdgcn_raw_buffer_store_b128(pack2(v.c[2 * q], v.c[2 * q + 1]), srs, stp[q] + ro, 0, 2 /* nt */);
       });
+      if constexpr (PUSH) {
+        // (rows before the face wrap to offsets far past the range: the
+        // segment's rows times ld8 stay below 2^31, launch_tb's lmax)
+        const uint32_t ry = ro - psh;
+        static_for<0, NC / 2>([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          const u4 d = pack2(v.c[2 * q], v.c[2 * q + 1]);
+          __builtin_amdgcn_raw_buffer_store_b128(d, prs_y, stp[q] + ry, 0, kPushAux);
+          __builtin_amdgcn_raw_buffer_store_b128(d, prs_x, xp[q] + ro, 0, kPushAux);
+          __builtin_amdgcn_raw_buffer_store_b128(d, prs_c, xp[q] + ry, 0, kPushAux);
+        });
+      }
       if constexpr (EDGE) {
         static_for<0, NC / 2>([&](auto Q) {
           constexpr int q = decltype(Q)::value;
@@ -578,7 +646,7 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
 // A workgroup = nw adjacent strips of one segment row, S waves per strip
 // (adjacent strips share their overlap columns in the CU's L1 / the XCD's
 // L2).  S == 1: every wave is independent (no barrier).
-template <int K, bool EXACT, bool EDGE>
+template <int K, bool EXACT, bool EDGE, bool PUSH>
 __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict__ u, double* __restrict__ un,
                                          int64_t t) {
   using C = Cfg<K>;
@@ -690,9 +758,13 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   char* ring = reinterpret_cast<char*>(lds_dyn) + sl * strip_lds<K>();
   // one instantiation per (stage, rule path, direction); the direction is
   // bottom-up only for the N row bands
+  // the x face this strip pushes (PUSH): the first strip holds the W one,
+  // the last the E one (launch_tb: at least two strips when both are pushed)
+  const int xd = !PUSH ? -1 : (strip == 0 && a.push[GMT_PUSH_W]) ? GMT_PUSH_W
+                            : (strip == a.nstrip[k] - 1 && a.push[GMT_PUSH_E]) ? GMT_PUSH_E : -1;
   auto go = [&](auto jc, auto rule_c, auto up_c, int sstep) {
-    run_stage<K, decltype(jc)::value, EXACT, EDGE, decltype(rule_c)::value, decltype(up_c)::value>(
-        a, u, un, ring, lane, xs, xe, ys, ye, nsteps, sstep);
+    run_stage<K, decltype(jc)::value, EXACT, EDGE, decltype(rule_c)::value, decltype(up_c)::value, PUSH>(
+        a, u, un, ring, lane, xs, xe, ys, ye, nsteps, sstep, xd);
   };
   using T = std::true_type;
   using F = std::false_type;
@@ -723,7 +795,7 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   }
 }
 
-template <int K, bool EXACT, bool EDGE>
+template <int K, bool EXACT, bool EDGE, bool PUSH>
 __global__ __launch_bounds__(kMaxThreads) __attribute__((amdgpu_waves_per_eu(2)))
 void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__ un, int64_t nblocks) {
   const int64_t ns = a.sig_wgs, nd = a.sig_dispatch;
@@ -731,7 +803,7 @@ void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__
   // signalling workgroups (and row bands) first, in dispatch order over all
   // XCDs; the rest XCD-contiguous
   const int64_t t = b < nd ? b : nd + xcd_swizzle(b - nd, nblocks - nd);
-  tb_block<K, EXACT, EDGE>(a, u, un, t);
+  tb_block<K, EXACT, EDGE, PUSH>(a, u, un, t);
   if (t < ns) {
     // every wave's stores written back past its XCD's L2, then one arrival
     // per workgroup (vector atomics on uncached memory)
@@ -777,8 +849,11 @@ struct SegPlan {
 // interior segments per strip group, each at least rb_min rows long, so its
 // S and N bands are separate segments that finish early.
 template <int K>
+// push_ns (inline halo exchange with both S and N faces pushed): every
+// segment holds at most one of the two faces (launch_tb: ny >= 2 w + 2), so
+// at least two segments per strip group.
 SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t resident_wgs, int sig_rects, int rb_rect = -1,
-                      int rb = 0, int64_t rb_min = 0) {
+                      int rb = 0, int64_t rb_min = 0, bool push_ns = false) {
   SegPlan p{};
   const int64_t edge = std::max<int64_t>(64, K);
   auto fill = [&](int64_t L0, int64_t* wgs) {
@@ -803,6 +878,7 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
       }
       const int64_t mid = ny - p.e0[k] - p.e1[k];
       if (k == rb_rect && rb > 0) L = std::min<int64_t>(L, std::max<int64_t>(rb_min, mid / rb));
+      if (push_ns) L = std::min<int64_t>(L, (mid + 1) / 2);
       p.nmid[k] = (mid + L - 1) / L;
       p.lmid[k] = (mid + p.nmid[k] - 1) / p.nmid[k];  // balanced lengths
       // strip groups that can reach a Dirichlet column run the rule path
@@ -813,6 +889,7 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
                                            (rx1 + Cfg<K>::KL > a.dom[0] + a.dom[1] && !(a.mask & 2)));
       int64_t lb = xrule ? std::max<int64_t>(64, p.lmid[k] / 2) : p.lmid[k];
       if (k == rb_rect && rb > 0) lb = std::min<int64_t>(lb, std::max<int64_t>(rb_min, mid / rb));
+      if (push_ns) lb = std::min<int64_t>(lb, (mid + 1) / 2);
       p.nmid_b[k] = (mid + lb - 1) / lb;
       p.lmid_b[k] = (mid + p.nmid_b[k] - 1) / p.nmid_b[k];
       const int64_t groups = (a.nstrip[k] + a.nw - 1) / a.nw, nbnd = groups < 2 ? groups : 2;
@@ -910,7 +987,7 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
 // Fills the kernel arguments and the launch shape; info (optional) gets
 // {workgroups, resident workgroups, threads per workgroup, rows per interior
 // segment and interior segments of the first rect, VGPRs per lane}.
-template <int K, bool EXACT, bool EDGE>
+template <int K, bool EXACT, bool EDGE, bool PUSH>
 int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int64_t* dom, int mask, const double* u,
               double* un, int64_t ld, int64_t nrows, hipStream_t s, int64_t* info = nullptr) {
   using C = Cfg<K>;
@@ -923,6 +1000,22 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   a.mask = mask;
   a.quarter = 0.25;
   for (int j = 0; j < 4; ++j) a.dom[j] = dom[j];
+  bool push_ns = false;
+  if constexpr (PUSH) {
+    // gmt_tb_opts.push: the one rect is the interior, an even face width,
+    // room for two segments clear of each other's face, no signals
+    const int64_t w = o.push_w;
+    bool ok = n_rect == 1 && w > 0 && w <= 64 && (w & 1) == 0 && o.signal_rects == 0 && o.signal_rows == 0 &&
+              o.signal_cols == 0 && o.seg_rows == 0 && dom[1] >= w && dom[3] >= 2 * w + 2;
+    for (int j = 0; ok && j < 4; ++j) ok = rects[j] == dom[j];
+    if (!ok) return static_cast<int>(hipErrorInvalidValue);
+    for (int d = 0; d < 8; ++d) a.push[d] = o.push[d];
+    a.push_w = w;
+    push_ns = o.push[GMT_PUSH_S] && o.push[GMT_PUSH_N];
+    // a strip pushes one x face
+    if (o.push[GMT_PUSH_W] && o.push[GMT_PUSH_E] && (dom[1] + C::WOUT - 1) / C::WOUT < 2)
+      return static_cast<int>(hipErrorInvalidValue);
+  }
   constexpr int64_t wout = C::WOUT;
   int64_t maxh = 0;
   for (int k = 0; k < n_rect; ++k) {
@@ -945,7 +1038,7 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   (void)maxh;
   const size_t smem = static_cast<size_t>(a.nw * strip_lds<K>());
   if (smem > 65536) {  // above the default dynamic-LDS limit (gfx950 has 160 KB per CU)
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE>),
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE, PUSH>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem));
     if (e != hipSuccess) return static_cast<int>(e);
   }
@@ -960,7 +1053,7 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   int per_cu = slot ? slot->load(std::memory_order_relaxed) : 0;
   if (per_cu <= 0) {
     int occ = 0, cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE>),
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE, PUSH>),
                                                      a.nw * G * kWave, smem) != hipSuccess || occ < 1)
       occ = 1;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -987,7 +1080,7 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   // search costs milliseconds; the engine launches the same passes over and over)
   SegPlan sp;
   {
-    std::vector<int64_t> key = {a.n, a.nw, a.mask, o.seg_rows, lmax, per_cu, sig_rects, rbk, rbs + rbn, rb_min};
+    std::vector<int64_t> key = {a.n, a.nw, a.mask, o.seg_rows, lmax, per_cu, sig_rects, rbk, rbs + rbn, rb_min, push_ns};
     for (int k = 0; k < a.n; ++k) key.insert(key.end(), a.r[k], a.r[k] + 4);
     key.insert(key.end(), a.dom, a.dom + 4);
     static std::mutex mu;
@@ -996,7 +1089,7 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     auto it = cache.find(key);
     if (it == cache.end()) {
       if (cache.size() > 256) cache.clear();
-      it = cache.emplace(key, plan_segments<K>(a, o.seg_rows, lmax, per_cu, sig_rects, rbk, rbs + rbn, rb_min)).first;
+      it = cache.emplace(key, plan_segments<K>(a, o.seg_rows, lmax, per_cu, sig_rects, rbk, rbs + rbn, rb_min, push_ns)).first;
     }
     sp = it->second;
   }
@@ -1056,12 +1149,12 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   a.signal = o.signal;
   if (info) {
     hipFuncAttributes fa{};
-    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE>));
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE, PUSH>));
     const int64_t v[6] = {nb, per_cu, a.nw * G * kWave, a.lmid[0], a.nmid[0], fa.numRegs};
     for (int j = 0; j < 6; ++j) info[j] = v[j];
     return 0;
   }
-  jacobi5tb_kernel<K, EXACT, EDGE><<<grid_1d(nb), a.nw * G * kWave, smem, s>>>(a, u, un, nb);
+  jacobi5tb_kernel<K, EXACT, EDGE, PUSH><<<grid_1d(nb), a.nw * G * kWave, smem, s>>>(a, u, un, nb);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -1080,11 +1173,20 @@ int dispatch_k(const gmt_tb_opts& o, bool exact, int n_rect, const int64_t* rect
   for (int k = 0; k < n_rect; ++k)
     if (rects[4 * k + 1] > 0 && rects[4 * k + 3] > 0 && rects[4 * k + 1] < tb_strip_out(K) && rects[4 * k + 1] % 2 == 1)
       edge = true;
+  if (o.push_w > 0) {  // inline halo exchange: no odd-edge stores (checked in launch_tb)
+    if constexpr (tb_push_built(K)) {
+      if (edge) return static_cast<int>(hipErrorInvalidValue);
+      return exact ? launch_tb<K, true, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
+                   : launch_tb<K, false, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
+    } else {
+      return static_cast<int>(hipErrorInvalidValue);
+    }
+  }
   if (edge)
-    return exact ? launch_tb<K, true, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
-                 : launch_tb<K, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
-  return exact ? launch_tb<K, true, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
-               : launch_tb<K, false, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
+    return exact ? launch_tb<K, true, true, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
+                 : launch_tb<K, false, true, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
+  return exact ? launch_tb<K, true, false, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
+               : launch_tb<K, false, false, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
 }
 
 }  // namespace tb

@@ -69,6 +69,8 @@ class TbOpts(ctypes.Structure):
         ("signal_rows", c_int),
         ("reserved_cus", c_int),
         ("signal_cols", c_int),
+        ("push", c_vp * 8),
+        ("push_w", c_int),
     ]
 
 _SIGS = {

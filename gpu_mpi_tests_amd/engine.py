@@ -48,7 +48,7 @@ class EngineOpts(ctypes.Structure):
     """gmt_engine_opts (csrc/include/gmt/engine.h)."""
     _fields_ = [(n, ctypes.c_int) for n in
                 ("periodic", "overlap", "graph", "tsteps", "wg_waves", "seg_rows", "exact", "init",
-                 "calibrate")] + [("seed", ctypes.c_int64)]
+                 "calibrate")] + [("seed", ctypes.c_int64), ("push", ctypes.c_int)]
 
 
 class EngineError(RuntimeError):
@@ -280,7 +280,13 @@ class NativeJacobi:
                  dims: tuple[int, int] | None = None, periodic: bool = False,
                  overlap: "bool | str" = True, graph: bool = True,
                  tblock: bool | int = False, wg_waves: int = 0, seg_rows: int = 0, exact: int = -1,
-                 transport: str = "auto", init: str = "analytic", seed: int = 0, calibrate: bool = False):
+                 transport: str = "auto", init: str = "analytic", seed: int = 0, calibrate: bool = False,
+                 push: bool = False):
+        """push: the fused passes exchange their halo inline (each pass stores
+        its output faces straight into the neighbours' ghost cells over IPC
+        mappings, then one hand-over launch; gmt/jacobi.hpp JacobiConfig::push).
+        Needs the IPC transport when a neighbour is another rank; silently the
+        transport's exchange when the share is too small (``push_active``)."""
         from .parallel.decomp import choose_dims
 
         self.env = env or gdist.get()
@@ -317,16 +323,17 @@ class NativeJacobi:
         opts = EngineOpts(periodic=int(bool(periodic)), overlap=2 if auto else int(bool(overlap)),
                           graph=int(bool(graph)), tsteps=ks, wg_waves=int(wg_waves),
                           seg_rows=int(seg_rows), exact=int(exact), init=INITS[init],
-                          calibrate=int(bool(calibrate)), seed=int(seed))
+                          calibrate=int(bool(calibrate)), seed=int(seed), push=int(bool(push)))
         with _StdoutToStderr():
             self.h = self.lib.gmt_engine_jacobi_create(ny, nx, py, px, e.rank, e.world_size, transport,
                                                        cid, ctypes.byref(opts))
         if not self.h:
             raise EngineError("gmt_engine_jacobi_create failed")
-        info = (ctypes.c_int64 * 15)()
+        info = (ctypes.c_int64 * 16)()
         self.lib.gmt_engine_jacobi_info(self.h, info)
         (self.nx, self.ny, self.off_x, self.off_y, self.halo_bytes, self.halo_msgs,
-         graph_on, overlap_on, _, _, tb, t_ov, t_ser, exact_on, band_on) = list(info)
+         graph_on, overlap_on, _, _, tb, t_ov, t_ser, exact_on, band_on, push_on) = list(info)
+        self.push_active = bool(push_on)
         # overlapped fused passes run band-first (boundary bands signal, the
         # output halo travels under the interior)
         self.band_first = bool(band_on)

@@ -316,7 +316,7 @@ def _check_xk_bounds(k: int, u: torch.Tensor, un: torch.Tensor, rects) -> None:
 
 def jacobi5tb(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, int, int, int]],
               dom: tuple[int, int, int, int], halo_mask: int = 0, *, wg_waves: int = 0, seg_rows: int = 0,
-              exact: bool = False) -> None:
+              exact: bool = False, push: "dict | None" = None, push_w: int = 0) -> None:
     """``k`` fused Laplace sweeps per memory pass with the temporal-blocking kernel
     (csrc/kernels/jacobi5tb.hip): ``un = J^k(u)`` on up to 8 output rects (absolute
     coordinates, each with its k-wide ring inside the array); the rest of ``un``
@@ -325,7 +325,10 @@ def jacobi5tb(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[i
     Dirichlet rings).  ``k``: see :func:`tb_supported`.  ``wg_waves``: 256-column
     strips per workgroup (0 = default), ``seg_rows``: output rows per strip (0 =
     default), ``exact``: 1/4 multiply per level instead of power-of-two scaled
-    levels."""
+    levels.  ``push`` ({direction: tensor}, directions "S" "N" "W" "E" "SW" "SE"
+    "NW" "NE") with ``push_w``: the inline halo exchange (gmt_tb_opts.push) —
+    the output's face cells are also stored into each tensor at the same
+    coordinates (a tensor with ``un``'s row pitch)."""
     rects = [tuple(int(v) for v in r) for r in rects if r[1] > 0 and r[3] > 0]
     if not tb_supported(k):
         raise ValueError(f"jacobi5tb: {k} sweeps per pass is not built (1..10 or even 12..{TB_MAX_SWEEPS})")
@@ -343,6 +346,13 @@ def jacobi5tb(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[i
     arr = (ctypes.c_int64 * (4 * len(rects)))(*[v for r in rects for v in r])
     d = (ctypes.c_int64 * 4)(*[int(v) for v in dom])
     o = _native.TbOpts(int(k), int(wg_waves), int(seg_rows), int(bool(exact)))
+    if push:
+        order = ("S", "N", "W", "E", "SW", "SE", "NW", "NE")
+        for d, t in push.items():
+            if t.stride(0) != un.stride(0) or t.shape[0] < un.shape[0] or t.dtype != un.dtype:
+                raise ValueError("jacobi5tb: a push target needs un's row pitch, rows and dtype")
+            o.push[order.index(d)] = t.data_ptr()
+        o.push_w = int(push_w)
     _native.check(L.gmt_jacobi5tb(ctypes.byref(o), len(rects), ctypes.cast(arr, ctypes.c_void_p),
                                   ctypes.cast(d, ctypes.c_void_p), int(halo_mask), u.data_ptr(),
                                   un.data_ptr(), u.stride(0), u.shape[0], _stream(u)),

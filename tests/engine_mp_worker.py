@@ -20,7 +20,8 @@ def main():
     dims = tuple(int(v) for v in sys.argv[7].split("x")) if len(sys.argv) > 7 else None
     env = gd.init(device=os.environ.get("GMT_TEST_DEVICE", "cpu"))
     e = engine.NativeJacobi(ny, nx, env, dims=dims, periodic=periodic, overlap=overlap,
-                            graph=os.environ.get("GMT_TEST_GRAPH", "1") == "1", tblock=tblock)
+                            graph=os.environ.get("GMT_TEST_GRAPH", "1") == "1", tblock=tblock,
+                            push=os.environ.get("GMT_TEST_PUSH", "0") == "1")
     e.run(steps)
     e.synchronize()
     e.exchange()  # a blocking exchange on its own (bench.py's latency probe)
@@ -38,7 +39,7 @@ def main():
         bad = np.argwhere(np.abs(full - ref) > 0)
         print(json.dumps(dict(diff=float(np.abs(full - ref).max()), transport=e.transport, nbad=int(len(bad)),
                               first_bad=bad[:4].tolist(), overlap=e.overlap, band_first=e.band_first,
-                              dims=[e.py, e.px], tsteps=e.tsteps, halo=e.halo_bytes,
+                              dims=[e.py, e.px], tsteps=e.tsteps, halo=e.halo_bytes, push=e.push_active,
                               resid_same=len(set(resids)) == 1)), flush=True)
     e.close()
     gd.shutdown()

@@ -197,15 +197,17 @@ def test_bench_transport_probe_cpu():
     port, pport = str(free_port()), str(free_port())
     rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
-                "--device", "cpu", "--size", "192", "--steps", "3", "--warmup", "1", "--skip-extras",
-                "--transport-probe", "on", "--probe-port", pport, "--probe-iters", "5"])
+                "--device", "cpu", "--size", "600", "--steps", "3", "--warmup", "1", "--skip-extras",
+                "--transport-probe", "on", "--probe-port", pport, "--probe-iters", "5", "--probe-passes", "2"])
     cands = rec["transport_candidates"]
-    assert set(cands) == {"rccl", "ipc"}, cands
+    assert set(cands) == {"rccl", "ipc", "push"}, cands
     for c in cands.values():
-        assert c["gate"] == "pass" and c["exchange_us"] > 0, cands
-    best = min(cands, key=lambda t: cands[t]["exchange_us"])
-    chosen = rec["config"]["transport"].replace("-host", "")
-    assert chosen == best or (chosen == "rccl" and cands["ipc"]["exchange_us"] > 0.97 * cands["rccl"]["exchange_us"])
+        assert c["gate"] == "pass" and c["pass_ms"] > 0, cands
+    assert cands["rccl"]["exchange_us"] > 0 and cands["ipc"]["exchange_us"] > 0
+    assert "inline halo" in cands["push"]["label"]
+    best = min(cands, key=lambda t: cands[t]["pass_ms"])
+    chosen = {"rccl-host": "rccl", "ipc-host": "ipc", "ipc-host inline halo": "push"}[rec["config"]["transport"]]
+    assert chosen == best or (chosen == "rccl" and cands[best]["pass_ms"] > 0.97 * cands["rccl"]["pass_ms"])
     assert rec["check_max_diff"] == 0.0 and rec["transport_probe_s"] > 0
 
 
@@ -220,9 +222,9 @@ def test_bench_transport_probe_drops_a_crashing_candidate_cpu():
                 "--transport-probe", "on", "--probe-port", pport, "--probe-iters", "5", "--probe-timeout", "20"],
                GMT_PROBE_CRASH="1:ipc")
     cands = rec["transport_candidates"]
-    assert cands["rccl"]["gate"] == "pass" and cands["rccl"]["exchange_us"] > 0, cands
+    assert cands["rccl"]["gate"] == "pass" and cands["rccl"]["pass_ms"] > 0, cands
     assert cands["ipc"]["gate"] == "fail" and "probe exit" in cands["ipc"]["error"], cands
-    assert rec["config"]["transport"] == "rccl-host" and rec["check_max_diff"] == 0.0
+    assert rec["config"]["transport"] in ("rccl-host", "ipc-host inline halo") and rec["check_max_diff"] == 0.0
 
 
 def test_bench_probe_drops_rccl_every_extra_on_ipc_cpu():
@@ -233,14 +235,14 @@ def test_bench_probe_drops_rccl_every_extra_on_ipc_cpu():
     port, pport = str(free_port()), str(free_port())
     rec = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
-                "--device", "cpu", "--size", "192", "--steps", "3", "--warmup", "1",
+                "--device", "cpu", "--size", "600", "--steps", "3", "--warmup", "1",
                 "--daxpy-n", "20000", "--ref-n-local", "32", "--ref-n-other", "300", "--ref-iters", "4",
                 "--small-size", "96", "--transport-probe", "on", "--probe-port", pport, "--probe-iters", "5",
-                "--probe-timeout", "30"], GMT_PROBE_CRASH="1:rccl")
+                "--probe-passes", "2", "--probe-timeout", "60"], GMT_PROBE_CRASH="1:rccl")
     cands = rec["transport_candidates"]
     assert cands["rccl"]["gate"] == "fail" and "probe exit 139" in cands["rccl"]["error"], cands
-    assert cands["ipc"]["gate"] == "pass", cands
-    assert rec["config"]["transport"] == "ipc-host"
+    assert cands["ipc"]["gate"] == "pass" and cands["push"]["gate"] == "pass", cands
+    assert rec["config"]["transport"] in ("ipc-host", "ipc-host inline halo"), rec["config"]["transport"]
     assert rec["ref_halo_config"].endswith("ipc-host") and rec["daxpy_allreduce_kind"] == "ipc-host"
     assert rec["ref_halo_dim0_bad_ghosts"] == 0 and rec["daxpy_allsum_rel_err"] <= 1e-9
     assert not [k for k in rec if k.endswith("_error")], rec
