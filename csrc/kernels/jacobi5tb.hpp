@@ -32,17 +32,15 @@ constexpr uint32_t kDrop = 0x80000000u;       // buffer offset past num_records:
 // back edge).
 constexpr int unroll_for(int NL) { return NL > 1 ? 2 * (NL - 1) + 1 : 2; }
 
-// Per-K shape (gmt/tb_geom.h).  Narrow strips re-read their three level-0
-// rows from LDS every step (the round-2/3 kernel); wide strips slide them
-// (SLIDE: one new row per step, read in the middle of the step into the
-// registers of the row level PB no longer needs), which makes the ring and
-// hand-off slots compile-time constants of the unrolled step (RS = U, HS = 3
-// divide U).
+// Per-K shape (gmt/tb_geom.h): every step re-reads the three input rows of
+// the stage's first level from LDS.  (The round-4 six-column strip with four
+// stages that slid its rows — 14% less VALU, 9-10% slower at two waves per
+// SIMD, profiles/r04_wide.md — lives in git history: scripts/build_variant.sh
+// wide git:09d882f with GEOM='s/kWideK20 = false/kWideK20 = true/'.)
 template <int K>
 struct Cfg {
   static constexpr int NC = tb_nc(K);           // columns per lane
   static constexpr int S = tb_stages(K);        // waves (stages) per strip
-  static constexpr bool SLIDE = tb_wide(K);
   static constexpr int COLS = NC * kWave;
   static constexpr uint32_t ROW = COLS * 8;     // bytes of one strip row
   static constexpr int NDMA = NC / 2;           // 1-KB full-wave DMAs per row
@@ -50,33 +48,23 @@ struct Cfg {
   static constexpr int WOUT = tb_strip_out(K);
   static constexpr int NL = K / S;              // levels per stage
   static constexpr int U = unroll_for(NL);
-  static constexpr int P = SLIDE ? 7 : 6;       // input rows in flight
-  static constexpr int RS = P + 2;              // DMA ring slots (compile-time slot indices when U % RS == 0)
-  // FLOW (wide strips): stages synchronise through per-ring progress
-  // counters in LDS instead of one workgroup barrier per step, so a stage
-  // stalls only for its own producer / consumer (hand-off rings of 5 slots:
-  // up to three steps of slack)
-  static constexpr bool FLOW = false;
-  static constexpr int HS = SLIDE ? (FLOW ? 5 : 3) : 6;  // hand-off ring slots
-  // step lag of each stage behind the previous one: narrow strips 2 (the
-  // hand-off rows of step s are requested before the barrier that ends step
-  // s); wide strips 3 (a writer leaves its newest hand-off row in flight
-  // across the step barrier: waiting for the three ds_write_b128 a wave has
-  // just issued cost every step ~a fifth, profiles/r04_wide.md)
-  static constexpr int DLAG = SLIDE ? 3 : 2;
+  static constexpr int P = 6;                   // input rows in flight
+  static constexpr int RS = P + 2;              // DMA ring slots
+  static constexpr int HS = 6;                  // hand-off ring slots
+  // step lag of each stage behind the previous one: 2 (the hand-off rows of
+  // step s are requested before the barrier that ends step s)
+  static constexpr int DLAG = 2;
   static constexpr int LAG = DLAG * (S - 1);    // the output stage's step lag
   static_assert(K % S == 0, "equal stages");
   static_assert(NC % 2 == 0 && KL % 2 == 0, "column pairs");
-  static_assert(!SLIDE || (U % 3 == 0 && (FLOW || U % HS == 0)), "compile-time register and hand-off slots");
-  static constexpr int CTL = FLOW ? 64 : 0;     // bytes of progress counters per strip
-  static_assert(SLIDE || HS >= 5, "hand ring: rows of steps s-4..s");
+  static_assert(HS >= 5, "hand ring: rows of steps s-4..s");
 };
 
 // LDS per strip: the DMA ring, plus S - 1 hand-off rings
 template <int K>
 __host__ __device__ constexpr int64_t strip_lds() {
   using C = Cfg<K>;
-  return static_cast<int64_t>(C::RS) * C::ROW + static_cast<int64_t>(C::S - 1) * C::HS * C::ROW + C::CTL;
+  return static_cast<int64_t>(C::RS) * C::ROW + static_cast<int64_t>(C::S - 1) * C::HS * C::ROW;
 }
 
 struct Args {
@@ -238,59 +226,18 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   constexpr bool kIn = J == 0;
   constexpr bool kOut = J == C::S - 1;
   constexpr bool SYNC = C::S > 1;
-  constexpr bool SLIDE = C::SLIDE;
   constexpr int kP = C::P, kRS = C::RS, kHS = C::HS;
   constexpr uint32_t kRow = C::ROW;
   constexpr int D = C::DLAG * J;                     // step lag behind stage 0
   // global stores per step (PUSH: three face groups more, see below)
   constexpr int SPS = kOut ? (EDGE ? NC : (PUSH ? 4 : 1) * (NC / 2)) : 0;
   static_assert(!(PUSH && EDGE), "inline halo exchange: no odd-edge stores");
-  // DMAs per step.  Narrow strips: stage 0 loads the whole row.  Wide strips:
-  // stage q < NDMA loads the row's q-th 1-KB piece (an LDS-DMA costs ~60
-  // issue cycles: three on one wave made stage 0 the pole of every step
-  // barrier, profiles/r04_wide.md) and waits for it before the barrier that
-  // publishes the row to stage 0.
-  constexpr bool kDma = SLIDE ? J < C::NDMA : kIn;
-  constexpr int DPS = kDma ? (SLIDE ? 1 : C::NDMA) : 0;
-  static_assert(!SLIDE || (C::S > C::NDMA && SPS * DPS == 0), "wide strips: the output stage loads nothing");
+  // DMAs per step: stage 0 loads the whole row
+  constexpr bool kDma = kIn;
+  constexpr int DPS = kDma ? C::NDMA : 0;
   // hand-off rings: read ring J - 1, write ring J
   char* const hand_rd = ring + kRS * kRow + (J > 0 ? J - 1 : 0) * kHS * kRow;
   char* const hand_wr = ring + kRS * kRow + J * kHS * kRow;
-  // FLOW progress counters (after the hand-off rings): [j] rows < v that
-  // stage j wrote to its ring are complete; [4 + j] rows < v of ring j were
-  // read by stage j + 1; [8 + q] rows < v of DMA piece q landed; [12] rows
-  // < v of the DMA ring were read by stage 0.  Every spin is bounded (a
-  // protocol error yields wrong results, never a hung GPU).
-  constexpr bool FLOW = SLIDE && C::FLOW;
-  int* const ctl = reinterpret_cast<int*>(ring + kRS * kRow + (C::S - 1) * kHS * kRow);
-  auto ctl_put = [&](int i, int v) {
-    if (lane == 0) __atomic_store_n(ctl + i, v, __ATOMIC_RELAXED);
-  };
-  // the spin is one asm block: a loop in the unrolled step's control flow
-  // costs its register allocation dozens of copies per step
-  const uint32_t ctl_lds = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ctl));
-  auto wait_ge = [&](int i, int want) {
-    int v, cnt;
-    uint32_t sv;
-    asm volatile(
-        "s_mov_b32 %2, 0x10000\n"
-        "1:\n\t"
-        "ds_read_b32 %0, %3\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "v_readfirstlane_b32 %1, %0\n\t"
-        "s_cmp_ge_i32 %1, %4\n\t"
-        "s_cbranch_scc1 2f\n\t"
-        "s_sleep 1\n\t"
-        "s_sub_u32 %2, %2, 1\n\t"
-        "s_cbranch_scc0 1b\n"
-        "2:"
-        : "=&v"(v), "=&s"(sv), "=&s"(cnt)
-        : "v"(ctl_lds + 4u * static_cast<uint32_t>(i)), "s"(__builtin_amdgcn_readfirstlane(want))
-        : "memory", "scc");
-    (void)v;
-    (void)sv;
-    (void)cnt;
-  };
   // every kernel argument the loop needs, as values: the asm memory clobbers
   // below would otherwise force a reload of the kernarg segment per use
   const int64_t ld = a.ld;
@@ -325,15 +272,10 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
     if constexpr (kDma) {
       char* dst = ring + slot * kRow;
       const uint32_t o = dbase + static_cast<uint32_t>(s) * rstep;
-      if constexpr (SLIDE) {
-        constexpr uint32_t q = J;
+      static_for<0, C::NDMA>([&](auto Q) {
+        constexpr uint32_t q = decltype(Q)::value;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + q * 1024u, 16, loff + q * kPieceStride + o, 0, 0, 0);
-      } else {
-        static_for<0, C::NDMA>([&](auto Q) {
-          constexpr uint32_t q = decltype(Q)::value;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + q * 1024u, 16, loff + q * kPieceStride + o, 0, 0, 0);
-        });
-      }
+      });
     }
   };
   //  stores: rows [ys, ye) from column xs.  The left output edge is a column
@@ -465,22 +407,7 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   // prologue: rows 0..P-1 in flight, each preceded by the (dropped) stores a
   // steady-state step issues, so every wait below counts the same younger
   // memory operations
-  if constexpr (SLIDE) {
-    // wide strips: every loading stage issues its piece of rows 0..P-1 and
-    // waits for rows 0 and 1; one extra barrier publishes them (every wave of
-    // the workgroup takes it, idle ones included) and the FLOW counters
-    if constexpr (kDma) {
-      static_for<0, kP>([&](auto I) { dma(decltype(I)::value, decltype(I)::value); });
-      wait_vmcnt<DPS * (kP - 2)>();
-    }
-    if constexpr (FLOW) {
-      if constexpr (kDma) ctl_put(8 + J, 2);
-      if constexpr (!kOut) ctl_put(J, 0);
-      if constexpr (J > 0) ctl_put(4 + J - 1, 0);
-      if constexpr (kIn) ctl_put(12, 0);
-    }
-    step_barrier();
-  } else if constexpr (kIn) {
+  if constexpr (kIn) {
     // (each dummy store gets its own out-of-range row so the compiler cannot
     // merge identical stores)
     static_for<0, kP>([&](auto I) {
@@ -489,19 +416,14 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
     });
   }
 
-  // level PB-1 input rows.  Narrow strips: r0, r1, r2 = the rows of step s,
-  // read one step ahead so the ds_reads are in flight across the step
-  // barrier.  Wide strips (SLIDE): R[i % 3] holds input row i; the row step s
-  // adds is read in the middle of step s - 1.
+  // level PB-1 input rows: r0, r1, r2 = the rows of step s, read one step
+  // ahead so the ds_reads are in flight across the step barrier.
   //   stage 0: input row i = DMA'd window row i, step s uses rows s-2, s-1, s;
   //   stage J > 0: input row i = the row stage J-1 wrote at its step i, step
-  //   s uses rows s-2-RD .. s-RD (RD = DLAG: row i is complete once the
-  //   writer has waited for it at the end of its step i + 1, and published by
-  //   that step's barrier).
-  constexpr int RD = kIn ? 0 : C::DLAG;  // step s's newest input row is s - RD
+  //   s uses rows s-2-DLAG .. s-DLAG (published by the barrier of the
+  //   writer's step that wrote it).
   dv<NC> r0, r1, r2;
-  dv<NC> R[3];
-  auto load_rows = [&](int s) {  // narrow strips: the three rows of step s
+  auto load_rows = [&](int s) {  // the three rows of step s
     if constexpr (kIn) {
       // the DMA of row s (issued at the end of step s-P) has landed once at
       // most (SPS + DPS)(P - 1) younger memory operations are outstanding
@@ -515,61 +437,15 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
       r2 = lds_row<NC>(hand_rd + ((s + kHS - 2) % kHS) * kRow, lane);
     }
   };
-  // wide strips: input row i (i = s0 + j, s0 a multiple of U: every slot
-  // index is a constant of the unrolled step)
-  constexpr bool kRingFixed = C::U % kRS == 0;  // DMA ring slot of a row: a constant of the unrolled step
-  auto load_one = [&](auto Jc, int s) {  // the newest input row of step s + 1 (s = s0 + Jc)
-    constexpr int i = decltype(Jc)::value + 1 - RD;  // its index mod U (+ a multiple of U)
-    constexpr int im = ((i % 3) + 3) % 3;
-    if constexpr (kIn) {
-      // row s+1: every piece landed before the barrier that ended step s-1
-      const int slot = kRingFixed ? (i % kRS) : (s + 1) % kRS;
-      R[im] = lds_row<NC>(ring + slot * kRow, lane);
-    } else {
-      // FLOW rings (5 slots) do not divide the unroll: the slot of the
-      // absolute row s + 1 - RD
-      const int slot = C::FLOW ? ((s + 1 - RD) % kHS + kHS) % kHS : ((i % kHS) + kHS) % kHS;
-      R[im] = lds_row<NC>(hand_rd + slot * kRow, lane);
-    }
-  };
-  if constexpr (SLIDE) {
-    // rows -RD-2, -RD-1 (warm-up: never in an output cone) and -RD
-    static_for<0, 3>([&](auto Q) {
-      constexpr int i = decltype(Q)::value - 2 - RD;
-      constexpr int im = ((i % 3) + 3) % 3;
-      if constexpr (kIn) R[im] = lds_row<NC>(ring + (((i % kRS) + kRS) % kRS) * kRow, lane);
-      else R[im] = lds_row<NC>(hand_rd + (((i % kHS) + kHS) % kHS) * kRow, lane);
-    });
-  } else {
-    load_rows(0);
-  }
+  load_rows(0);
 
   // rows of the walk: level p of step s is row rbase(s) - dir * p
   const int64_t yanchor = up ? ye - 1 + K : yl;
   auto step = [&](auto Jc, int s) {
     constexpr int j = decltype(Jc)::value;
     const int64_t rbase = yanchor + dir * (s - D);
-    dv<NC> v;
-    if constexpr (SLIDE) {
-      constexpr int i2 = j - RD;  // newest input row (mod U)
-      constexpr int m0 = (((i2 - 2) % 3) + 3) % 3, m1 = (((i2 - 1) % 3) + 3) % 3, m2 = ((i2 % 3) + 3) % 3;
-      v = level(R[m0], R[m1], R[m2], rbase - dir * PB);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (FLOW) {
-        // the input row is complete; this step's hand-off slot and DMA ring
-        // slot are free (every wait refers to earlier steps of other waves)
-        if constexpr (kIn) {
-          static_for<0, C::NDMA>([&](auto Q) { wait_ge(8 + decltype(Q)::value, s + 2); });
-        } else {
-          wait_ge(J - 1, s + 2 - RD);
-        }
-        if constexpr (!kOut) wait_ge(4 + J, s - kHS + 1);
-        if constexpr (kDma) wait_ge(12, s + kP - kRS + 1);
-      }
-      load_one(Jc, s);  // into R[m0], free now
-    } else {
-      v = level(r0, r1, r2, rbase - dir * PB);
-    }
+    (void)j;
+    dv<NC> v = level(r0, r1, r2, rbase - dir * PB);
     __builtin_amdgcn_sched_barrier(0);
     static_for<PB + 1, PE + 1>([&](auto Q) {
       constexpr int p = decltype(Q)::value;  // PB+1 .. PE, bottom-up
@@ -586,37 +462,15 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
       }
       store_step(s, v);  // issued every step (warm-up rows are out of range)
     } else {
-      const int slot = (SLIDE && !FLOW) ? j % kHS : s % kHS;
-      lds_put<NC>(hand_wr + slot * kRow, lane, v);
+      lds_put<NC>(hand_wr + (s % kHS) * kRow, lane, v);
     }
-    // the ring slot of row s-2 (narrow) / s+P-RS (wide) is free: prefetch row
-    // s+P into it
-    dma(s + kP, (SLIDE && kRingFixed) ? (j + kP) % kRS : (s + kP) % kRS);
-    if constexpr (SLIDE) {
-      // this wave's piece of row s+2 (issued at step s+2-P) has landed once
-      // at most P-2 younger DMAs are outstanding: then the barrier publishes
-      // it to stage 0, which reads row s+2 in the middle of step s+1
-      if constexpr (kDma) wait_vmcnt<DPS * (kP - 2)>();
-      // every LDS access but this step's hand-off writes (issued last) done
-      if constexpr (FLOW) {
-        if constexpr (kOut) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NC / 2) : "memory");
-        if constexpr (kDma) ctl_put(8 + J, s + 3);
-        if constexpr (!kOut) ctl_put(J, s);               // row s - 1 complete
-        if constexpr (J > 0) ctl_put(4 + J - 1, s + 2 - RD);  // row s + 1 - RD read
-        if constexpr (kIn) ctl_put(12, s + 2);            // row s + 1 read
-      } else if constexpr (kOut) {
-        step_barrier();
-      } else {
-        asm volatile("s_waitcnt lgkmcnt(%0)\n\ts_barrier" ::"n"(NC / 2) : "memory");
-      }
-    } else {
-      // hand-off row written (visible to the workgroup after the barrier),
-      // then the next step's rows requested, then the barrier
-      if constexpr (SYNC) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      load_rows(s + 1);
-      if constexpr (SYNC) asm volatile("s_barrier" ::: "memory");
-    }
+    // the ring slot of row s-2 is free: prefetch row s+P into it
+    dma(s + kP, (s + kP) % kRS);
+    // hand-off row written (visible to the workgroup after the barrier),
+    // then the next step's rows requested, then the barrier
+    if constexpr (SYNC) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    load_rows(s + 1);
+    if constexpr (SYNC) asm volatile("s_barrier" ::: "memory");
   };
 
   constexpr int kU = C::U;
@@ -654,10 +508,7 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   extern __shared__ d2 lds_dyn[];
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
-  // wide strips, two per workgroup: the second strip's stages are rotated by
-  // half, so the two waves a SIMD hosts (waves w and w + 4) are stages j and
-  // j + 2 — a loading stage next to a light one
-  const int sl = wave / G, stage = C::SLIDE ? (wave % G + (sl & 1) * (G / 2)) % G : wave % G;
+  const int sl = wave / G, stage = wave % G;  // strip of the workgroup, stage of the strip
   int k = 0;
   while (k + 1 < a.n && t >= a.tstart[k + 1]) ++k;
   const int64_t lt = t - a.tstart[k];
@@ -741,8 +592,8 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   const int64_t strip = gi * a.nw + sl;
   if (strip >= a.nstrip[k]) {  // no strip for this wave
     if constexpr (G > 1) {
-      // the workgroup's per-step barriers (wide strips: and the prologue's)
-      for (int s = 0; s < (C::SLIDE ? (C::FLOW ? 1 : nsteps + 1) : nsteps); ++s) step_barrier();
+      // the workgroup's per-step barriers
+      for (int s = 0; s < nsteps; ++s) step_barrier();
     }
     return;
   }
@@ -855,8 +706,22 @@ template <int K>
 SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t resident_wgs, int sig_rects, int rb_rect = -1,
                       int rb = 0, int64_t rb_min = 0, bool push_ns = false) {
   SegPlan p{};
-  const int64_t edge = std::max<int64_t>(64, K);
+  // A rule segment costs ~kRuleCost times the steps of a plain one (the
+  // loop census: 5837 vs 3218 VALU per 19 steps at K = 20).  Edge segments
+  // (at a Dirichlet row) are either short (64 rows: many of them pack well
+  // into the tail of a multi-round launch) or "balanced" — as long as makes
+  // them cost what an L-row interior segment costs, so a one-round launch
+  // (the N = 8 shares, 8192^2) neither waits for them nor leaves their slots
+  // idle; the makespan search tries both.  Strip groups that reach a
+  // Dirichlet column run the rule path at every step: balanced segments.
+  constexpr double kRuleCost = 1.8;
+  constexpr int64_t kWarm = 2 * K + Cfg<K>::LAG;
+  auto balanced = [](int64_t L) {
+    return std::max<int64_t>(64, static_cast<int64_t>(static_cast<double>(L + kWarm) / kRuleCost) - kWarm);
+  };
+  bool long_edges = false;
   auto fill = [&](int64_t L0, int64_t* wgs) {
+    const int64_t edge = long_edges ? balanced(L0) : std::max<int64_t>(64, K);
     int64_t w = 0;
     for (int k = 0; k < a.n; ++k) {
       int64_t L = L0;
@@ -876,18 +741,29 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
         p.e0[k] = top ? edge : 0;
         p.e1[k] = bot ? edge : 0;
       }
-      const int64_t mid = ny - p.e0[k] - p.e1[k];
+      int64_t mid = ny - p.e0[k] - p.e1[k];
       if (k == rb_rect && rb > 0) L = std::min<int64_t>(L, std::max<int64_t>(rb_min, mid / rb));
       if (push_ns) L = std::min<int64_t>(L, (mid + 1) / 2);
       p.nmid[k] = (mid + L - 1) / L;
       p.lmid[k] = (mid + p.nmid[k] - 1) / p.nmid[k];  // balanced lengths
+      if (long_edges && (p.e0[k] > 0 || p.e1[k] > 0)) {
+        // the edges' length follows the interior segments' final length (a
+        // few fixed-point steps: both depend on each other)
+        for (int it = 0; it < 4; ++it) {
+          const int64_t e = std::min<int64_t>(balanced(p.lmid[k]), (ny - 64) / 2);
+          p.e0[k] = p.e0[k] > 0 ? e : 0;
+          p.e1[k] = p.e1[k] > 0 ? e : 0;
+          mid = ny - p.e0[k] - p.e1[k];
+          p.lmid[k] = (mid + p.nmid[k] - 1) / p.nmid[k];
+        }
+      }
       // strip groups that can reach a Dirichlet column run the rule path
       // (~2x the VALU per step): half-length segments, so they finish with
       // the others instead of ending the launch
       const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
       const bool xrule = seg_rows == 0 && ((rx0 - Cfg<K>::KL < a.dom[0] && !(a.mask & 1)) ||
                                            (rx1 + Cfg<K>::KL > a.dom[0] + a.dom[1] && !(a.mask & 2)));
-      int64_t lb = xrule ? std::max<int64_t>(64, p.lmid[k] / 2) : p.lmid[k];
+      int64_t lb = xrule ? balanced(p.lmid[k]) : p.lmid[k];
       if (k == rb_rect && rb > 0) lb = std::min<int64_t>(lb, std::max<int64_t>(rb_min, mid / rb));
       if (push_ns) lb = std::min<int64_t>(lb, (mid + 1) / 2);
       p.nmid_b[k] = (mid + lb - 1) / lb;
@@ -971,15 +847,20 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
     return end;
   };
   int64_t best_l = 128;
+  bool best_long = false;
   double best = 1e300;
-  for (int64_t L = 128; L <= std::min<int64_t>(2048, lmax); L += 32) {
-    fill(L, &wgs);
-    const double cost = makespan();
-    if (cost < best - 1e-9) {
-      best = cost;
-      best_l = L;
+  for (int le = 0; le < 2; ++le)
+    for (int64_t L = 128; L <= std::min<int64_t>(2048, lmax); L += 16) {
+      long_edges = le == 1;
+      fill(L, &wgs);
+      const double cost = makespan();
+      if (cost < best - 1e-9) {
+        best = cost;
+        best_l = L;
+        best_long = long_edges;
+      }
     }
-  }
+  long_edges = best_long;
   fill(std::min<int64_t>(best_l, lmax), &wgs);
   return p;
 }

@@ -97,6 +97,7 @@ _SIGS = {
         [c_int, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_dbl, c_dbl, c_vp],
     ),
     "gmt_jacobi5tb_supported": (c_int, [c_int]),
+    "gmt_jacobi5tb_push_supported": (c_int, [c_int]),
     "gmt_jacobi5tb": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_vp]),
     "gmt_jacobi5tb_plan": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_i64, c_i64, c_vp]),
     "gmt_jacobi5tb_group_cols": (c_i64, [c_int, c_int]),

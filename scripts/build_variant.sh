@@ -15,18 +15,22 @@ rm -rf $D && mkdir -p $D/src $D/obj
 cp csrc/kernels/*.hpp csrc/kernels/jacobi5tb*.hip $D/src/
 # the strip geometry travels with the kernel (quote includes resolve next to
 # jacobi5tb.hpp first): GEOM='sed expr' edits it, e.g. the wide K = 20 kernel
-#   GEOM='s/kWideK20 = false/kWideK20 = true/' scripts/build_variant.sh wide cur
+#   GEOM='s/kWideK20 = false/kWideK20 = true/' scripts/build_variant.sh wide git:09d882f
+#   (the wide strip left the production header in round 5; with git:REV the
+#   geometry header comes from REV too)
 mkdir -p $D/src/gmt && cp csrc/include/gmt/tb_geom.h $D/src/gmt/
 [ -n "$GEOM" ] && sed -i "$GEOM" $D/src/gmt/tb_geom.h
 case "$expr" in
   git:*) git show "${expr#git:}:csrc/kernels/jacobi5tb.hpp" > $D/src/jacobi5tb.hpp
-         git show "${expr#git:}:csrc/kernels/jacobi5tb.hip" > $D/src/jacobi5tb.hip ;;
+         git show "${expr#git:}:csrc/kernels/jacobi5tb.hip" > $D/src/jacobi5tb.hip
+         git show "${expr#git:}:csrc/include/gmt/tb_geom.h" > $D/src/gmt/tb_geom.h
+         [ -n "$GEOM" ] && sed -i "$GEOM" $D/src/gmt/tb_geom.h ;;
   file:*) cp "${expr#file:}" $D/src/jacobi5tb.hpp ;;
   cur) ;;
   *) sed -i "$expr" $D/src/jacobi5tb.hpp ;;
 esac
 [ "$expr" != cur ] && cmp -s csrc/kernels/jacobi5tb.hpp $D/src/jacobi5tb.hpp && { echo "sed changed nothing"; exit 1; }
-[ -n "$GEOM" ] && cmp -s csrc/include/gmt/tb_geom.h $D/src/gmt/tb_geom.h && { echo "GEOM changed nothing"; exit 1; }
+[ -n "$GEOM" ] && [ "${expr#git:}" = "$expr" ] && cmp -s csrc/include/gmt/tb_geom.h $D/src/gmt/tb_geom.h && { echo "GEOM changed nothing"; exit 1; }
 # ONLY=kf: rebuild only that instantiation unit (+ jacobi5tb.hip) and take
 # the other K from the production build (each unit's device code is its own
 # code object, so the units need not share the edited header)
