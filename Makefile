@@ -148,7 +148,12 @@ asan-host:
 
 # tuning harnesses (standalone, not part of the libraries): stream_sweep, and
 # variant_bench — the A/B kernel variants checked and timed against libgmt
-sweep: $(BUILD)/bench/stream_sweep $(BUILD)/bench/variant_bench $(BUILD)/bench/d1_walk $(BUILD)/bench/sdma_probe
+sweep: $(BUILD)/bench/stream_sweep $(BUILD)/bench/variant_bench $(BUILD)/bench/d1_walk $(BUILD)/bench/sdma_probe \
+       $(BUILD)/bench/plan_model
+# the segment planner on the host (no GPU): plan_model [ny nx mask [resident]] ...
+$(BUILD)/bench/plan_model: csrc/bench/plan_model.hip $(KERNEL_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -Icsrc/include -Icsrc/kernels --cuda-host-only -o $@ $<
 $(BUILD)/bench/sdma_probe: csrc/bench/sdma_probe.hip
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<

@@ -217,10 +217,12 @@ class MpiHostExchange : public Exchange {
     wait_limit_s_ = w && std::atof(w) > 0 ? std::atof(w) / 1e3 : std::max(10.0, wd);
   }
   ~MpiHostExchange() override {
+    if (trace_ && !tr_.empty()) trace_dump();
     for (auto& e : events_) gmt_rt_event_destroy(e);
     for (auto& e : h2d_done_) gmt_rt_event_destroy(e);
   }
   void start(gmt_stream_t s) override {
+    if (trace_) trace_start();
     cur_ ^= 1;
     // the exchange before last drained this staging set with its H2D copies
     if (armed_[cur_]) GMT_CHECK("staging reuse", gmt_rt_event_synchronize(h2d_done_[cur_]));
@@ -272,10 +274,12 @@ class MpiHostExchange : public Exchange {
     auto land = [&](int n) {
       for (int q = 0; q < n; ++q) land_one(static_cast<size_t>(idx[q]));
       pending -= static_cast<size_t>(n);
+      if (trace_) tr_.back().landed.push_back(MPI_Wtime());
     };
     auto send = [&](size_t k) {
       const Chunk& ch = schunks_[k];
       const Msg& m = sends_[ch.msg];
+      if (trace_) tr_.back().staged.push_back(MPI_Wtime());
       sreqs.emplace_back();
       isend(sstage_[ch.msg].data() + ch.off, ch.len, m.peer, m.tag, c_, &sreqs.back());
     };
@@ -284,6 +288,7 @@ class MpiHostExchange : public Exchange {
       return kernel_ ? __atomic_load_n(flags_.data() + k, __ATOMIC_ACQUIRE) >= epoch_
                      : gmt_rt_event_query(events_[k]) == 0;
     };
+    if (trace_) tr_.back().wait = MPI_Wtime();
     double t0 = MPI_Wtime();
     long polls = 0;
     while (next < schunks_.size() || pending > 0) {
@@ -344,10 +349,53 @@ class MpiHostExchange : public Exchange {
         a = b;
       }
     }
+    if (trace_) tr_.back().recvd = MPI_Wtime();
     waitall(sreqs, "mpi-host exchange");
     GMT_CHECK("event", gmt_rt_event_record(h2d_done_[cur_], s));
     armed_[cur_] = true;
+    if (trace_) tr_.back().end = MPI_Wtime();
   }
+
+ private:
+  // GMT_HOST_TRACE=DIR: host timestamps of every exchange (start, wait
+  // entry, each chunk staged and sent, each receive chunk landed, all
+  // received, sends complete), written to DIR/host_trace_r<rank>.txt when
+  // the plan is destroyed — the phases of a slow exchange against a fast one
+  struct Trace {
+    double start = 0, wait = 0, recvd = 0, end = 0;
+    std::vector<double> staged, landed;
+  };
+  void trace_start() {
+    tr_.emplace_back();
+    tr_.back().start = MPI_Wtime();
+  }
+  void trace_dump() {
+    int rank = 0;
+    MPI_Comm_rank(c_, &rank);
+    const std::string path = std::string(trace_) + "/host_trace_r" + std::to_string(rank) + ".txt";
+    FILE* f = std::fopen(path.c_str(), "a");
+    if (!f) return;
+    std::fprintf(f, "# exchange start(s) wait+ first_staged+ last_staged+ first_landed+ last_landed+ recvd+ end+ "
+                    "(us after start) chunks=%zu/%zu bytes=%zu\n", schunks_.size(), rchunks_.size(), total_bytes());
+    for (size_t i = 0; i < tr_.size(); ++i) {
+      const Trace& t = tr_[i];
+      auto us = [&](double v) { return v > 0 ? (v - t.start) * 1e6 : -1.0; };
+      std::fprintf(f, "%zu %.6f %.1f %.1f %.1f %.1f %.1f %.1f %.1f\n", i, t.start, us(t.wait),
+                   us(t.staged.empty() ? 0 : t.staged.front()), us(t.staged.empty() ? 0 : t.staged.back()),
+                   us(t.landed.empty() ? 0 : t.landed.front()), us(t.landed.empty() ? 0 : t.landed.back()),
+                   us(t.recvd), us(t.end));
+    }
+    std::fclose(f);
+  }
+  size_t total_bytes() const {
+    size_t b = 0;
+    for (auto& m : sends_) b += m.bytes;
+    return b;
+  }
+  const char* trace_ = std::getenv("GMT_HOST_TRACE");
+  std::vector<Trace> tr_;
+
+ public:
 
  private:
   struct Chunk {
