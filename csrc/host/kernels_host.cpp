@@ -289,7 +289,10 @@ int gmt_jacobi5tb(const gmt_tb_opts* o, int n_rect, const int64_t* rects, const 
     bool ok = gmt::tb::tb_push_built(K) && n_rect == 1 && w <= 64 && (w & 1) == 0 && !sig && o->seg_rows == 0 && dom[1] >= w && dom[3] >= 2 * w + 2;
     for (int j = 0; ok && j < 4; ++j) ok = rects[j] == dom[j];
     const int64_t wout = gmt::tb::tb_strip_out(K);
-    if (ok && o->push[GMT_PUSH_W] && o->push[GMT_PUSH_E] && (dom[1] + wout - 1) / wout < 2) ok = false;
+    const auto any = [&](int d0, int d1, int d2) { return o->push[d0] || o->push[d1] || o->push[d2]; };
+    if (ok && any(GMT_PUSH_W, GMT_PUSH_SW, GMT_PUSH_NW) && any(GMT_PUSH_E, GMT_PUSH_SE, GMT_PUSH_NE) &&
+        (dom[1] + wout - 1) / wout < 2)
+      ok = false;
     if (ok && dom[1] < wout && (dom[1] & 1)) ok = false;  // the GPU kernel's odd-edge stores
     if (!ok) return 1;
   }

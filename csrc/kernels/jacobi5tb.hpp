@@ -205,6 +205,56 @@ __device__ __forceinline__ u2 pack1(double a) {
   return u2{static_cast<unsigned>(__double2loint(a)), static_cast<unsigned>(__double2hiint(a))};
 }
 
+// The Dirichlet keep of one level (RULE waves): v.c[j] = c.c[j] (exact) or
+// 4 c.c[j] (scaled levels, exact in binary) on the lanes of mask
+// (row kept ? all : kxm[j]); the row is kept iff t < tlo or t >= thi (walk
+// coordinates, run_stage).  One asm block, all scalar but the four writes:
+// the row test (s_cmp / s_cselect: a C++ bool would come back as a VALU
+// select), a branch past the writes when no lane keeps (kor: any ring
+// column in the window; the edge segments of inner strips keep only on the
+// ring rows), EXEC saved, set per column, restored; the s_nop covers the
+// SALU-writes-EXEC -> DPP hazard of the next level's lane shifts (the compiler
+// cannot see EXEC change here).  The round-4 per-cell select (a multiply, two
+// v_cndmask per column and a 64-bit row compare per level) made rule waves
+// ~1.8x the VALU of plain ones.
+template <bool EXACT, int NC>
+__device__ __forceinline__ void keep_cells(dv<NC>& v, const dv<NC>& c, const uint64_t (&kxm)[NC], uint64_t kor, int t,
+                                           int tlo, int thi) {
+  static_assert(NC == 4, "four columns per lane");
+  uint64_t sv, rm;
+#define GMT_KEEP_ASM(OP0, OP1, OP2, OP3)                                                                          \
+  asm("s_cmp_lt_i32 %[t], %[tlo]\n\t"                                                                           \
+      "s_cselect_b64 %[rm], -1, 0\n\t"                                                                           \
+      "s_cmp_ge_i32 %[t], %[thi]\n\t"                                                                           \
+      "s_cselect_b64 %[rm], -1, %[rm]\n\t"                                                                       \
+      "s_or_b64 %[sv], %[rm], %[kor]\n\t"                                                                        \
+      "s_cbranch_scc0 .Lgmt_keep_%=\n\t"                                                                        \
+      "s_mov_b64 %[sv], exec\n\t"                                                                              \
+      "s_or_b64 exec, %[m0], %[rm]\n\t"                                                                         \
+      "s_and_b64 exec, exec, %[sv]\n\t" OP0 "\n\t"                                                             \
+      "s_or_b64 exec, %[m1], %[rm]\n\t"                                                                         \
+      "s_and_b64 exec, exec, %[sv]\n\t" OP1 "\n\t"                                                             \
+      "s_or_b64 exec, %[m2], %[rm]\n\t"                                                                         \
+      "s_and_b64 exec, exec, %[sv]\n\t" OP2 "\n\t"                                                             \
+      "s_or_b64 exec, %[m3], %[rm]\n\t"                                                                         \
+      "s_and_b64 exec, exec, %[sv]\n\t" OP3 "\n\t"                                                             \
+      "s_mov_b64 exec, %[sv]\n\t"                                                                              \
+      "s_nop 4\n"                                                                                               \
+      ".Lgmt_keep_%=:"                                                                                           \
+      : [v0] "+v"(v.c[0]), [v1] "+v"(v.c[1]), [v2] "+v"(v.c[2]), [v3] "+v"(v.c[3]), [sv] "=&s"(sv),           \
+        [rm] "=&s"(rm)                                                                                         \
+      : [c0] "v"(c.c[0]), [c1] "v"(c.c[1]), [c2] "v"(c.c[2]), [c3] "v"(c.c[3]), [m0] "s"(kxm[0]),             \
+        [m1] "s"(kxm[1]), [m2] "s"(kxm[2]), [m3] "s"(kxm[3]), [kor] "s"(kor), [t] "s"(t), [tlo] "s"(tlo),       \
+        [thi] "s"(thi)                                                                                         \
+      : "scc")
+  if constexpr (EXACT)
+    GMT_KEEP_ASM("v_mov_b64 %[v0], %[c0]", "v_mov_b64 %[v1], %[c1]", "v_mov_b64 %[v2], %[c2]", "v_mov_b64 %[v3], %[c3]");
+  else
+    GMT_KEEP_ASM("v_mul_f64 %[v0], %[c0], 4.0", "v_mul_f64 %[v1], %[c1], 4.0", "v_mul_f64 %[v2], %[c2], 4.0",
+                 "v_mul_f64 %[v3], %[c3], 4.0");
+#undef GMT_KEEP_ASM
+}
+
 // One wave = stage J of one strip: levels PB..PE of the K-level pipeline
 // (PB = J NL + 1, PE = (J + 1) NL).  Stage 0 takes level 0 from the DMA
 // ring; stage J > 0 from hand-off ring J - 1 (rows written by stage J - 1;
@@ -254,7 +304,6 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   // (bottom-up: from the last row, a negative step; rows past either end
   // wrap to offsets beyond the buffer range: zero-filled / dropped)
   constexpr bool up = UP;
-  constexpr int dir = UP ? -1 : 1;
   const uint32_t rstep = up ? 0u - ld8 : ld8;
   const uint32_t dbase = up ? static_cast<uint32_t>(L + 2 * K - 1) * ld8 : 0u;
   const uint32_t sbase = up ? static_cast<uint32_t>(L - 1) * ld8 : 0u;
@@ -307,11 +356,14 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
     const int64_t w = a.push_w;
     int yd = -1;
     int64_t fy0 = 0, fy1 = 0;
-    if (a.push[GMT_PUSH_S] && ys < dy0 + w) {
+    // (a face is located even when only its corners are pushed)
+    const bool ps = a.push[GMT_PUSH_S] || a.push[GMT_PUSH_SW] || a.push[GMT_PUSH_SE];
+    const bool pn = a.push[GMT_PUSH_N] || a.push[GMT_PUSH_NW] || a.push[GMT_PUSH_NE];
+    if (ps && ys < dy0 + w) {
       yd = GMT_PUSH_S;
       fy0 = ys > dy0 ? ys : dy0;
       fy1 = ye < dy0 + w ? ye : dy0 + w;
-    } else if (a.push[GMT_PUSH_N] && ye > dy1 - w) {
+    } else if (pn && ye > dy1 - w) {
       yd = GMT_PUSH_N;
       fy0 = ys > dy1 - w ? ys : dy1 - w;
       fy1 = ye < dy1 ? ye : dy1;
@@ -319,12 +371,12 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
     auto face = [&](int d, int64_t row0, int64_t rows) {
       return row_rsrc(a.push[d] + row0 * ld + xs, static_cast<uint32_t>(rows) * ld8);
     };
-    if (yd >= 0) {
+    if (yd >= 0 && a.push[yd]) {
       prs_y = face(yd, fy0, fy1 - fy0);
       psh = static_cast<uint32_t>(fy0 - ys) * ld8;
     }
     if (xd >= 0) {
-      prs_x = face(xd, ys, L);
+      if (a.push[xd]) prs_x = face(xd, ys, L);
       const int cd = yd < 0 ? -1 : (yd == GMT_PUSH_S ? (xd == GMT_PUSH_W ? GMT_PUSH_SW : GMT_PUSH_SE)
                                                       : (xd == GMT_PUSH_W ? GMT_PUSH_NW : GMT_PUSH_NE));
       if (cd >= 0 && a.push[cd]) prs_c = face(cd, fy0, fy1 - fy0);
@@ -368,11 +420,24 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   // ghost ring is fixed keeps its value at every level
   const bool gw = mask & 1, ge = mask & 2, gs = mask & 4, gn = mask & 8;
   auto kept_col = [&](int64_t c) { return (c < dx0 && !gw) || (c >= dx1 && !ge); };
-  bool kx[NC];
+  // per column of the lane: the lanes whose cell is a fixed ring cell (a
+  // wave-uniform 64-bit mask per column, for the exec-masked keep below)
+  uint64_t kxm[NC];
 #pragma unroll
-  for (int j = 0; j < NC; ++j) kx[j] = kept_col(c0 + j);
+  for (int j = 0; j < NC; ++j) kxm[j] = __builtin_amdgcn_ballot_w64(kept_col(c0 + j));
+  const uint64_t kor = kxm[0] | kxm[1] | kxm[2] | kxm[3];  // any ring column in the window
 
-  auto level = [&](const dv<NC>& up_, const dv<NC>& c, const dv<NC>& dn, int64_t row) -> dv<NC> {
+  // fixed ring rows, in walk coordinates t = +-(row - yanchor) (- bottom-up;
+  // the walk's rows: t = s - D - p for level p of step s): kept iff t < tlo
+  // or t >= thi
+  // (32-bit scalar compares; 64-bit row compares would take the VALU)
+  const int64_t yanchor = up ? ye - 1 + K : yl;
+  const auto clamp32 = [](int64_t x) {
+    return static_cast<int>(x < INT32_MIN ? int64_t{INT32_MIN} : x > INT32_MAX ? int64_t{INT32_MAX} : x);
+  };
+  const int tlo = up ? (gn ? INT32_MIN : clamp32(yanchor - dy1 + 1)) : (gs ? INT32_MIN : clamp32(dy0 - yanchor));
+  const int thi = up ? (gs ? INT32_MAX : clamp32(yanchor - dy0 + 1)) : (gn ? INT32_MAX : clamp32(dy1 - yanchor));
+  auto level = [&](const dv<NC>& up_, const dv<NC>& c, const dv<NC>& dn, int t) -> dv<NC> {
 #pragma clang fp contract(off)
     const double w = dpp_from_lower(c.c[NC - 1]), e = dpp_from_upper(c.c[0]);
     dv<NC> v;
@@ -388,10 +453,11 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
       else v.c[j] = (l + r) + (up_.c[j] + dn.c[j]);
     });
     if constexpr (RULE) {
-      const bool rk = (row < dy0 && !gs) || (row >= dy1 && !gn);
-      const double f = EXACT ? 1.0 : 4.0;  // a kept cell: V_p = 4 V_{p-1}
-#pragma unroll
-      for (int j = 0; j < NC; ++j) v.c[j] = (rk || kx[j]) ? c.c[j] * f : v.c[j];
+      // a kept cell: V_p = V_{p-1} (exact) / 4 V_{p-1} (scaled levels),
+      // written under EXEC = the lanes to keep: all lanes on a fixed ring
+      // row, the ring-column lanes otherwise (none in most levels of most
+      // rule waves)
+      keep_cells<EXACT, NC>(v, c, kxm, kor, t, tlo, thi);
     }
     return v;
   };
@@ -439,17 +505,15 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   };
   load_rows(0);
 
-  // rows of the walk: level p of step s is row rbase(s) - dir * p
-  const int64_t yanchor = up ? ye - 1 + K : yl;
+  // rows of the walk: level p of step s is row yanchor +- (s - D - p)
   auto step = [&](auto Jc, int s) {
     constexpr int j = decltype(Jc)::value;
-    const int64_t rbase = yanchor + dir * (s - D);
     (void)j;
-    dv<NC> v = level(r0, r1, r2, rbase - dir * PB);
+    dv<NC> v = level(r0, r1, r2, s - D - PB);
     __builtin_amdgcn_sched_barrier(0);
     static_for<PB + 1, PE + 1>([&](auto Q) {
       constexpr int p = decltype(Q)::value;  // PB+1 .. PE, bottom-up
-      const dv<NC> nv = level(W[p - 1 - PB][0], W[p - 1 - PB][1], v, rbase - dir * p);
+      const dv<NC> nv = level(W[p - 1 - PB][0], W[p - 1 - PB][1], v, s - D - p);
       W[p - 1 - PB][0] = W[p - 1 - PB][1];  // rows of steps s-1 and s become s-2 and s-1
       W[p - 1 - PB][1] = v;
       v = nv;
@@ -611,8 +675,9 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   // bottom-up only for the N row bands
   // the x face this strip pushes (PUSH): the first strip holds the W one,
   // the last the E one (launch_tb: at least two strips when both are pushed)
-  const int xd = !PUSH ? -1 : (strip == 0 && a.push[GMT_PUSH_W]) ? GMT_PUSH_W
-                            : (strip == a.nstrip[k] - 1 && a.push[GMT_PUSH_E]) ? GMT_PUSH_E : -1;
+  const bool pw = PUSH && (a.push[GMT_PUSH_W] || a.push[GMT_PUSH_SW] || a.push[GMT_PUSH_NW]);
+  const bool pe = PUSH && (a.push[GMT_PUSH_E] || a.push[GMT_PUSH_SE] || a.push[GMT_PUSH_NE]);
+  const int xd = !PUSH ? -1 : (strip == 0 && pw) ? GMT_PUSH_W : (strip == a.nstrip[k] - 1 && pe) ? GMT_PUSH_E : -1;
   auto go = [&](auto jc, auto rule_c, auto up_c, int sstep) {
     run_stage<K, decltype(jc)::value, EXACT, EDGE, decltype(rule_c)::value, decltype(up_c)::value, PUSH>(
         a, u, un, ring, lane, xs, xe, ys, ye, nsteps, sstep, xd);
@@ -892,9 +957,12 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     if (!ok) return static_cast<int>(hipErrorInvalidValue);
     for (int d = 0; d < 8; ++d) a.push[d] = o.push[d];
     a.push_w = w;
-    push_ns = o.push[GMT_PUSH_S] && o.push[GMT_PUSH_N];
+    // (a face counts as pushed when only its corners are)
+    const auto any = [&](int d0, int d1, int d2) { return o.push[d0] || o.push[d1] || o.push[d2]; };
+    push_ns = any(GMT_PUSH_S, GMT_PUSH_SW, GMT_PUSH_SE) && any(GMT_PUSH_N, GMT_PUSH_NW, GMT_PUSH_NE);
     // a strip pushes one x face
-    if (o.push[GMT_PUSH_W] && o.push[GMT_PUSH_E] && (dom[1] + C::WOUT - 1) / C::WOUT < 2)
+    if (any(GMT_PUSH_W, GMT_PUSH_SW, GMT_PUSH_NW) && any(GMT_PUSH_E, GMT_PUSH_SE, GMT_PUSH_NE) &&
+        (dom[1] + C::WOUT - 1) / C::WOUT < 2)
       return static_cast<int>(hipErrorInvalidValue);
   }
   constexpr int64_t wout = C::WOUT;

@@ -348,10 +348,10 @@ def jacobi5tb(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[i
     o = _native.TbOpts(int(k), int(wg_waves), int(seg_rows), int(bool(exact)))
     if push:
         order = ("S", "N", "W", "E", "SW", "SE", "NW", "NE")
-        for d, t in push.items():
+        for dirn, t in push.items():
             if t.stride(0) != un.stride(0) or t.shape[0] < un.shape[0] or t.dtype != un.dtype:
                 raise ValueError("jacobi5tb: a push target needs un's row pitch, rows and dtype")
-            o.push[order.index(d)] = t.data_ptr()
+            o.push[order.index(dirn)] = t.data_ptr()
         o.push_w = int(push_w)
     _native.check(L.gmt_jacobi5tb(ctypes.byref(o), len(rects), ctypes.cast(arr, ctypes.c_void_p),
                                   ctypes.cast(d, ctypes.c_void_p), int(halo_mask), u.data_ptr(),

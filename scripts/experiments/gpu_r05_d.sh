@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 5 (d): the planner's balanced edge segments against short ones
-# (build/var/short: the same library with the long-edge search off), same
+# (build/var/short: the same library with the long-edge search off; build/var/head:
+# the committed kernel, per-cell rule select), same
 # box, alternating; then the driver-config bench.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
@@ -11,7 +12,7 @@ mkdir -p $OUT
 B=$R/build/bin/gmt_kernel_bench
 : > $OUT/rates.log
 for rep in 1 2; do
-  for v in new short; do
+  for v in ${VARIANTS:-new head short}; do
     lp=""; [ "$v" != new ] && lp=$R/build/var/$v
     for m in 0 15; do
       for shp in "--jacobi-n=32768 --iters=20" "--jacobi-n=8192 --iters=200" "--jacobi-ny=8192 --jacobi-nx=16384 --iters=60" "--jacobi-ny=16384 --jacobi-nx=8192 --iters=60"; do

@@ -221,10 +221,10 @@ def test_native_engine_push_one_rank_periodic(ny, nx, steps, k):
 
 
 @pytest.mark.parametrize("np_,ny,nx,steps,periodic,tblock,dims", [
-    (2, 100, 600, 23, False, 10, "1x2"),
+    (2, 100, 600, 23, False, 12, "1x2"),
     (2, 140, 300, 41, True, 20, "2x1"),
     (4, 150, 700, 27, False, 6, "2x2"),
-    (4, 120, 1100, 20, True, 10, "2x2"),
+    (4, 120, 1100, 20, True, 12, "2x2"),
     (6, 190, 800, 31, True, 12, "3x2"),
     (8, 210, 1200, 45, False, 20, "2x4"),
 ])
