@@ -162,6 +162,27 @@ int main(int argc, char** argv) {
             std::snprintf(tag, sizeof(tag), "%lldx%lld x%d nw%d P%d seg%d m%d", (long long)ny, (long long)nx, K, nw,
                           P, seg, mask);
             report("jacobi5tb", K, tag, ms, K * 16.0 * ny * nx);
+            if (cli.geti("tb-push", 0) && K % 2 == 0 && gmt_jacobi5tb_push_supported(K)) {
+              // --tb-push=1: the same pass with the inline halo exchange of a
+              // one-rank periodic domain (the engine's layout: every face lands
+              // in the opposite ghost ring of the output), alternated with the
+              // plain pass so clock drift hits both alike
+              gmt_tb_opts op = o;
+              double* bb = b.data();
+              const int64_t dy = ny * ld2, dx = nx;
+              const double* tgt[8] = {bb + dy, bb - dy, bb + dx, bb - dx, bb + dy + dx, bb + dy - dx, bb - dy + dx, bb - dy - dx};
+              for (int d = 0; d < 8; ++d) op.push[d] = tgt[d];  // GMT_PUSH_S, N, W, E, SW, SE, NW, NE
+              op.push_w = g;  // even K: the faces fill the g-wide ghost ring
+              for (int rep = 0; rep < 2; ++rep) {
+                const double mp = time_ms(s, iters, [&] {
+                  GMT_CHECK("tb push", gmt_jacobi5tb(&op, 1, rect, rect, mask, a.data(), b.data(), ld2, rows, s));
+                });
+                const double m0 = time_ms(s, iters, [&] {
+                  GMT_CHECK("tb", gmt_jacobi5tb(&o, 1, rect, rect, mask, a.data(), b.data(), ld2, rows, s));
+                });
+                std::printf("%-10s    %-30s push %.4f ms  plain %.4f ms  ratio %.4f\n", "", tag, mp, m0, mp / m0);
+              }
+            }
             int64_t pi[6] = {};
             GMT_CHECK("plan", gmt_jacobi5tb_plan(&o, 1, rect, rect, mask, ld2, rows, pi));
             std::printf("%-10s    %-30s %9.1f MLUPS  (wgs %lld resident %lld threads %lld seg %lld x %lld vgpr %lld)\n",

@@ -207,45 +207,37 @@ __device__ __forceinline__ u2 pack1(double a) {
 
 // The Dirichlet keep of one level (RULE waves): v.c[j] = c.c[j] (exact) or
 // 4 c.c[j] (scaled levels, exact in binary) on the lanes of mask
-// (row kept ? all : kxm[j]); the row is kept iff t < tlo or t >= thi (walk
-// coordinates, run_stage).  One asm block, all scalar but the four writes:
-// the row test (s_cmp / s_cselect: a C++ bool would come back as a VALU
-// select), a branch past the writes when no lane keeps (kor: any ring
-// column in the window; the edge segments of inner strips keep only on the
-// ring rows), EXEC saved, set per column, restored; the s_nop covers the
-// SALU-writes-EXEC -> DPP hazard of the next level's lane shifts (the compiler
-// cannot see EXEC change here).  The round-4 per-cell select (a multiply, two
-// v_cndmask per column and a 64-bit row compare per level) made rule waves
-// ~1.8x the VALU of plain ones.
+// (row kept ? all : kxm[j]); the row is kept iff x = t - tlo, as unsigned,
+// is >= span = thi - tlo (t: walk coordinate, run_stage).  One asm block,
+// all scalar but the four writes: the row test (s_cmp / s_cselect: a C++
+// bool would come back as a VALU select), EXEC set per column and restored
+// to all lanes — run_stage runs with all 64 lanes active (whole-wave
+// workgroups, no divergent branch around its loop) — and an s_nop for the
+// SALU-writes-EXEC -> DPP hazard of the next level's lane shifts (the
+// compiler cannot see EXEC change here).  The round-4 per-cell select (a
+// multiply, two v_cndmask per column and a 64-bit row compare per level)
+// made rule waves ~1.8x the VALU of plain ones; this is 1.23x the VALU and
+// 7 SALU per level.  (A branch past the four writes when no lane keeps —
+// most levels of the edge segments of inner strips — measured 2-3% slower
+// on the rectangular shares than writing under EXEC = 0:
+// profiles/r05_rule_keep/.)
 template <bool EXACT, int NC>
-__device__ __forceinline__ void keep_cells(dv<NC>& v, const dv<NC>& c, const uint64_t (&kxm)[NC], uint64_t kor, int t,
-                                           int tlo, int thi) {
+__device__ __forceinline__ void keep_cells(dv<NC>& v, const dv<NC>& c, const uint64_t (&kxm)[NC], uint32_t x,
+                                           uint32_t span) {
   static_assert(NC == 4, "four columns per lane");
-  uint64_t sv, rm;
+  uint64_t rm;
 #define GMT_KEEP_ASM(OP0, OP1, OP2, OP3)                                                                          \
-  asm("s_cmp_lt_i32 %[t], %[tlo]\n\t"                                                                           \
+  asm("s_cmp_ge_u32 %[x], %[span]\n\t"                                                                          \
       "s_cselect_b64 %[rm], -1, 0\n\t"                                                                           \
-      "s_cmp_ge_i32 %[t], %[thi]\n\t"                                                                           \
-      "s_cselect_b64 %[rm], -1, %[rm]\n\t"                                                                       \
-      "s_or_b64 %[sv], %[rm], %[kor]\n\t"                                                                        \
-      "s_cbranch_scc0 .Lgmt_keep_%=\n\t"                                                                        \
-      "s_mov_b64 %[sv], exec\n\t"                                                                              \
-      "s_or_b64 exec, %[m0], %[rm]\n\t"                                                                         \
-      "s_and_b64 exec, exec, %[sv]\n\t" OP0 "\n\t"                                                             \
-      "s_or_b64 exec, %[m1], %[rm]\n\t"                                                                         \
-      "s_and_b64 exec, exec, %[sv]\n\t" OP1 "\n\t"                                                             \
-      "s_or_b64 exec, %[m2], %[rm]\n\t"                                                                         \
-      "s_and_b64 exec, exec, %[sv]\n\t" OP2 "\n\t"                                                             \
-      "s_or_b64 exec, %[m3], %[rm]\n\t"                                                                         \
-      "s_and_b64 exec, exec, %[sv]\n\t" OP3 "\n\t"                                                             \
-      "s_mov_b64 exec, %[sv]\n\t"                                                                              \
-      "s_nop 4\n"                                                                                               \
-      ".Lgmt_keep_%=:"                                                                                           \
-      : [v0] "+v"(v.c[0]), [v1] "+v"(v.c[1]), [v2] "+v"(v.c[2]), [v3] "+v"(v.c[3]), [sv] "=&s"(sv),           \
-        [rm] "=&s"(rm)                                                                                         \
+      "s_or_b64 exec, %[m0], %[rm]\n\t" OP0 "\n\t"                                                              \
+      "s_or_b64 exec, %[m1], %[rm]\n\t" OP1 "\n\t"                                                              \
+      "s_or_b64 exec, %[m2], %[rm]\n\t" OP2 "\n\t"                                                              \
+      "s_or_b64 exec, %[m3], %[rm]\n\t" OP3 "\n\t"                                                              \
+      "s_mov_b64 exec, -1\n\t"                                                                                 \
+      "s_nop 4"                                                                                                \
+      : [v0] "+v"(v.c[0]), [v1] "+v"(v.c[1]), [v2] "+v"(v.c[2]), [v3] "+v"(v.c[3]), [rm] "=&s"(rm)            \
       : [c0] "v"(c.c[0]), [c1] "v"(c.c[1]), [c2] "v"(c.c[2]), [c3] "v"(c.c[3]), [m0] "s"(kxm[0]),             \
-        [m1] "s"(kxm[1]), [m2] "s"(kxm[2]), [m3] "s"(kxm[3]), [kor] "s"(kor), [t] "s"(t), [tlo] "s"(tlo),       \
-        [thi] "s"(thi)                                                                                         \
+        [m1] "s"(kxm[1]), [m2] "s"(kxm[2]), [m3] "s"(kxm[3]), [x] "s"(x), [span] "s"(span)                    \
       : "scc")
   if constexpr (EXACT)
     GMT_KEEP_ASM("v_mov_b64 %[v0], %[c0]", "v_mov_b64 %[v1], %[c1]", "v_mov_b64 %[v2], %[c2]", "v_mov_b64 %[v3], %[c3]");
@@ -425,7 +417,6 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   uint64_t kxm[NC];
 #pragma unroll
   for (int j = 0; j < NC; ++j) kxm[j] = __builtin_amdgcn_ballot_w64(kept_col(c0 + j));
-  const uint64_t kor = kxm[0] | kxm[1] | kxm[2] | kxm[3];  // any ring column in the window
 
   // fixed ring rows, in walk coordinates t = +-(row - yanchor) (- bottom-up;
   // the walk's rows: t = s - D - p for level p of step s): kept iff t < tlo
@@ -437,6 +428,8 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   };
   const int tlo = up ? (gn ? INT32_MIN : clamp32(yanchor - dy1 + 1)) : (gs ? INT32_MIN : clamp32(dy0 - yanchor));
   const int thi = up ? (gs ? INT32_MAX : clamp32(yanchor - dy0 + 1)) : (gn ? INT32_MAX : clamp32(dy1 - yanchor));
+  // (mod 2^32: t - tlo in [0, span) <=> tlo <= t < thi, for |t| < 2^30)
+  const uint32_t span = static_cast<uint32_t>(thi) - static_cast<uint32_t>(tlo);
   auto level = [&](const dv<NC>& up_, const dv<NC>& c, const dv<NC>& dn, int t) -> dv<NC> {
 #pragma clang fp contract(off)
     const double w = dpp_from_lower(c.c[NC - 1]), e = dpp_from_upper(c.c[0]);
@@ -457,7 +450,7 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
       // written under EXEC = the lanes to keep: all lanes on a fixed ring
       // row, the ring-column lanes otherwise (none in most levels of most
       // rule waves)
-      keep_cells<EXACT, NC>(v, c, kxm, kor, t, tlo, thi);
+      keep_cells<EXACT, NC>(v, c, kxm, static_cast<uint32_t>(t) - static_cast<uint32_t>(tlo), span);
     }
     return v;
   };
@@ -678,14 +671,30 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   const bool pw = PUSH && (a.push[GMT_PUSH_W] || a.push[GMT_PUSH_SW] || a.push[GMT_PUSH_NW]);
   const bool pe = PUSH && (a.push[GMT_PUSH_E] || a.push[GMT_PUSH_SE] || a.push[GMT_PUSH_NE]);
   const int xd = !PUSH ? -1 : (strip == 0 && pw) ? GMT_PUSH_W : (strip == a.nstrip[k] - 1 && pe) ? GMT_PUSH_E : -1;
-  auto go = [&](auto jc, auto rule_c, auto up_c, int sstep) {
-    run_stage<K, decltype(jc)::value, EXACT, EDGE, decltype(rule_c)::value, decltype(up_c)::value, PUSH>(
-        a, u, un, ring, lane, xs, xe, ys, ye, nsteps, sstep, xd);
-  };
+  // the waves that hold no face (most of them) run the plain output body:
+  // the face stores of the push body are issued every step, in range or not
+  const bool push_here = PUSH && (xd >= 0 ||
+                                  ((a.push[GMT_PUSH_S] || a.push[GMT_PUSH_SW] || a.push[GMT_PUSH_SE]) &&
+                                   ys < a.dom[2] + a.push_w) ||
+                                  ((a.push[GMT_PUSH_N] || a.push[GMT_PUSH_NW] || a.push[GMT_PUSH_NE]) &&
+                                   ye > a.dom[2] + a.dom[3] - a.push_w));
   using T = std::true_type;
   using F = std::false_type;
+  auto go = [&](auto jc, auto rule_c, auto up_c, int sstep) {
+    constexpr int j = decltype(jc)::value;
+    auto run = [&](auto push_c) {
+      run_stage<K, j, EXACT, EDGE, decltype(rule_c)::value, decltype(up_c)::value, decltype(push_c)::value>(
+          a, u, un, ring, lane, xs, xe, ys, ye, nsteps, sstep, xd);
+    };
+    if constexpr (PUSH && j == G - 1) {
+      if (push_here) run(T{});
+      else run(F{});
+    } else {
+      run(F{});
+    }
+  };
   auto stage_go = [&](auto jc, int sstep) {
-    if (dir < 0) {
+    if (!PUSH && dir < 0) {  // (no row bands in an inline-halo pass)
       if (rule) go(jc, T{}, T{}, sstep);
       else go(jc, F{}, T{}, sstep);
     } else {
@@ -764,6 +773,19 @@ struct SegPlan {
 // A row-band rect (rb_rect, gmt_tb_opts.signal_rows) keeps at least `rb`
 // interior segments per strip group, each at least rb_min rows long, so its
 // S and N bands are separate segments that finish early.
+// The step cost of a rule-path wave relative to a plain one (the planner's
+// model).  Loop census at K = 20 per 19 steps: round 4's per-cell select
+// 5837 vs 3218 VALU (1.8); the exec-masked keep 3882 VALU + 1711 SALU vs
+// 3150 VALU + 319 SALU.  GMT_TB_RULE_COST=c overrides it (A/B).
+inline double tb_rule_cost() {
+  static const double c = [] {
+    const char* e = std::getenv("GMT_TB_RULE_COST");
+    const double v = e ? std::atof(e) : 0.0;
+    return v >= 1.0 && v <= 4.0 ? v : 1.3;
+  }();
+  return c;
+}
+
 template <int K>
 // push_ns (inline halo exchange with both S and N faces pushed): every
 // segment holds at most one of the two faces (launch_tb: ny >= 2 w + 2), so
@@ -771,18 +793,21 @@ template <int K>
 SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t resident_wgs, int sig_rects, int rb_rect = -1,
                       int rb = 0, int64_t rb_min = 0, bool push_ns = false) {
   SegPlan p{};
-  // A rule segment costs ~kRuleCost times the steps of a plain one (the
-  // loop census: 5837 vs 3218 VALU per 19 steps at K = 20).  Edge segments
+  // A rule segment costs ~tb_rule_cost() times the steps of a plain one.  Edge segments
   // (at a Dirichlet row) are either short (64 rows: many of them pack well
   // into the tail of a multi-round launch) or "balanced" — as long as makes
   // them cost what an L-row interior segment costs, so a one-round launch
   // (the N = 8 shares, 8192^2) neither waits for them nor leaves their slots
   // idle; the makespan search tries both.  Strip groups that reach a
   // Dirichlet column run the rule path at every step: balanced segments.
-  constexpr double kRuleCost = 1.8;
-  constexpr int64_t kWarm = 2 * K + Cfg<K>::LAG;
-  auto balanced = [](int64_t L) {
-    return std::max<int64_t>(64, static_cast<int64_t>(static_cast<double>(L + kWarm) / kRuleCost) - kWarm);
+  const double fr = tb_rule_cost();
+  constexpr int64_t kWarm = 2 * K + Cfg<K>::LAG, kU = Cfg<K>::U;
+  // a rule segment's rows such that its steps (whole unrolled blocks of kU)
+  // cost at most those of an L-row plain one
+  auto balanced = [fr](int64_t L) {
+    const int64_t st = (L + kWarm + kU - 1) / kU * kU;
+    const int64_t blocks = static_cast<int64_t>(static_cast<double>(st) / (fr * kU) + 1e-9);
+    return std::max<int64_t>(64, blocks * kU - kWarm);
   };
   bool long_edges = false;
   auto fill = [&](int64_t L0, int64_t* wgs) {
@@ -823,8 +848,8 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
         }
       }
       // strip groups that can reach a Dirichlet column run the rule path
-      // (~2x the VALU per step): half-length segments, so they finish with
-      // the others instead of ending the launch
+      // (tb_rule_cost() per step): shorter segments, so they finish with the
+      // others instead of ending the launch
       const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
       const bool xrule = seg_rows == 0 && ((rx0 - Cfg<K>::KL < a.dom[0] && !(a.mask & 1)) ||
                                            (rx1 + Cfg<K>::KL > a.dom[0] + a.dom[1] && !(a.mask & 2)));
@@ -855,8 +880,8 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
   }
   // The launch's time is its makespan: workgroups start in dispatch order
   // on the first free slot (resident_wgs of them) and run (rows + 2K + lag)
-  // steps, rounded up to the unroll, rule-path ones ~1.8x longer per step
-  // (tests the loop census: 5837 vs 3218 VALU per 19 steps at K = 20).
+  // steps, rounded up to the unroll, rule-path ones tb_rule_cost() times
+  // longer per step.
   // Round 3 priced a plan as rounds x (L + 2K), blind to the short edge and
   // boundary-group workgroups that finish early and leave their slots idle
   // for the rest of a round: 15% of a one-round 8192 x 16384 pass
@@ -876,7 +901,6 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
       const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
       const bool xrule = (rx0 - Cfg<K>::KL < a.dom[0] && !(a.mask & 1)) ||
                          (rx1 + Cfg<K>::KL > a.dom[0] + a.dom[1] && !(a.mask & 2));
-      const double fr = 1.8;
       const double fe = yrule ? fr : 1.0;              // an edge segment touches its Dirichlet row
       const double fb = xrule || (yrule && p.e0[k] == 0 && p.e1[k] == 0) ? fr : 1.0;
       const double fm = yrule && p.e0[k] == 0 && p.e1[k] == 0 ? fr : 1.0;
@@ -911,20 +935,44 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
     }
     return end;
   };
+  // GMT_TB_PLAN_DEBUG=1: every candidate on stderr (build/bench/plan_model)
+  static const bool debug = std::getenv("GMT_TB_PLAN_DEBUG") != nullptr;
+  auto eval = [&](int le, int64_t L) {
+    long_edges = le == 1;
+    fill(L, &wgs);
+    const double cost = makespan();
+    if (debug)
+      std::fprintf(stderr, "plan le %d L %lld e %lld/%lld mid %lld x %lld b %lld x %lld wgs %lld cost %.1f\n", le,
+                   (long long)L, (long long)p.e0[0], (long long)p.e1[0], (long long)p.nmid[0], (long long)p.lmid[0],
+                   (long long)p.nmid_b[0], (long long)p.lmid_b[0], (long long)wgs, cost);
+    return cost;
+  };
+  // coarse (16 rows), then every length within 16 rows of each edge mode's
+  // coarse best (segment counts are integers: a plan one segment shorter
+  // can tip a launch into or out of one round)
+  const int64_t lhi = std::min<int64_t>(2048, lmax);
   int64_t best_l = 128;
   bool best_long = false;
   double best = 1e300;
-  for (int le = 0; le < 2; ++le)
-    for (int64_t L = 128; L <= std::min<int64_t>(2048, lmax); L += 16) {
-      long_edges = le == 1;
-      fill(L, &wgs);
-      const double cost = makespan();
+  for (int le = 0; le < 2; ++le) {
+    int64_t c0 = 128;
+    double b0 = 1e300;
+    for (int64_t L = 128; L <= lhi; L += 16) {
+      const double cost = eval(le, L);
+      if (cost < b0 - 1e-9) {
+        b0 = cost;
+        c0 = L;
+      }
+    }
+    for (int64_t L = std::max<int64_t>(128, c0 - 15); L <= std::min(lhi, c0 + 15); ++L) {
+      const double cost = eval(le, L);
       if (cost < best - 1e-9) {
         best = cost;
         best_l = L;
-        best_long = long_edges;
+        best_long = le == 1;
       }
     }
+  }
   long_edges = best_long;
   fill(std::min<int64_t>(best_l, lmax), &wgs);
   return p;

@@ -23,5 +23,6 @@ for rep in 1 2; do
   done
 done
 grep -E "^==|MLUPS" $OUT/rates.log | paste - - | awk '{print $2, $3, $4, $5, $(NF-13), $(NF-12), $(NF-5), $(NF-4), $(NF-3), $(NF-2)}'
+[ -n "$NOBENCH" ] && exit 0
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.out 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
 tail -1 $OUT/bench.out > $OUT/bench.json; cat $OUT/bench.json

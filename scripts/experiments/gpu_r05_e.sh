@@ -20,4 +20,9 @@ for rep in 1 2 3 4 5 6; do
   GMT_HOST_TRACE=$OUT/sycl_$rep timeout -k 10 120 $M -np 2 build/bin/mpi_stencil2d_sycl 1024 1 > $OUT/sycl_$rep.txt 2>&1 || { tail $OUT/sycl_$rep.txt; exit 1; }
   echo "rep $rep: alone $(grep -E '^ *8388608' $OUT/mpi_alone_$rep.txt | head -1) | mpi-host $(grep -E '^ *8388608' $OUT/halo_$rep.txt | head -1) | sycl $(grep 'exchange time' $OUT/sycl_$rep.txt | head -1)"
 done
+# the README's 16-B stream-ordered IPC latency, re-measured (2 ranks, 1 GPU)
+for rep in 1 2 3; do
+  timeout -k 10 120 $M -np 2 build/bin/mpi_halo_bench 16 4096 300 --transport=ipc > $OUT/ipc16_$rep.txt 2>&1 || { tail $OUT/ipc16_$rep.txt; exit 1; }
+done
+head -30 $OUT/ipc16_1.txt
 echo R05E_OK
