@@ -8,6 +8,7 @@
 // argument, 1024 = 4 two-stage K = 20 workgroups per CU on 256 CUs).
 //
 //   build/bench/plan_model [ny nx mask [resident]] ...   (K = 20, one rect = the interior)
+//   GMT_PLAN_PUSH=S: plan as an inline-halo pass pushing faces S (bits 1 W, 2 E, 4 S, 8 N)
 #include <cstdio>
 #include <cstdlib>
 
@@ -45,7 +46,8 @@ int main(int argc, char** argv) {
     a.mask = c.mask;
     const int64_t ld = (x0 + c.nx + K + 63) / 64 * 64;
     const int64_t lmax = std::min<int64_t>(1 << 20, (int64_t(1) << 31) / (ld * 8) - 3 * K - C::LAG - 2 * C::U - C::P);
-    const SegPlan p = plan_segments<K>(a, 0, lmax, c.resident, 0);
+    const char* ps = std::getenv("GMT_PLAN_PUSH");
+    const SegPlan p = plan_segments<K>(a, 0, lmax, c.resident, 0, -1, 0, 0, ps ? std::atoi(ps) : 0);
     const int64_t g = a.nstrip[0], nb = g < 2 ? g : 2;
     const int64_t wgs = g * ((p.e0[0] > 0) + (p.e1[0] > 0)) + nb * p.nmid_b[0] + (g - nb) * p.nmid[0];
     std::printf("%6lld x %6lld mask %2d: edges %lld / %lld rows, interior %lld x %lld rows, rule groups %lld x %lld rows, "

@@ -121,8 +121,9 @@ class MpiTransport : public Transport {
 //          after each; no host wait, so the caller's kernels queue right away.
 //   wait:  send each chunk as soon as its D2H event has completed (MPI keeps
 //          the chunks of one message in order: same peer, tag, communicator),
-//          and enqueue each received chunk's H2D copy as soon as it lands, so
-//          D2H, the wire and H2D of different chunks overlap.
+//          and enqueue each received chunk's H2D copy as soon as it lands (on
+//          the exchange's own receive stream, joined back into the caller's
+//          at the end), so D2H, the wire and H2D of different chunks overlap.
 // Receive staging is double-buffered across exchanges: the next exchange's
 // receives never wait for this one's H2D copies to drain.
 // Device -> host leg (GMT_HOST_STAGE): "kernel" (default) — one gmt_stage_copy
@@ -207,6 +208,11 @@ class MpiHostExchange : public Exchange {
       }
     }
     for (auto& e : h2d_done_) GMT_CHECK("event", gmt_rt_event_create(&e, 0));
+    // the receive leg (H2D copies, scatters) runs on a stream of its own, so
+    // a chunk that lands goes to the device at once instead of queueing
+    // behind the staging kernel on the caller's stream (profiles/r05_xport/)
+    GMT_CHECK("stream", gmt_rt_stream_create(&hs_, 1));
+    GMT_CHECK("event", gmt_rt_event_create(&before_, 0));
     // the staging poll gives up after this long WITHOUT a chunk staged (the
     // clock restarts at every staged chunk).  The first chunk also waits for
     // whatever the stream holds ahead of the staging kernel, so the default
@@ -220,12 +226,18 @@ class MpiHostExchange : public Exchange {
     if (trace_ && !tr_.empty()) trace_dump();
     for (auto& e : events_) gmt_rt_event_destroy(e);
     for (auto& e : h2d_done_) gmt_rt_event_destroy(e);
+    gmt_rt_event_destroy(before_);
+    gmt_rt_stream_destroy(hs_);
   }
   void start(gmt_stream_t s) override {
     if (trace_) trace_start();
     cur_ ^= 1;
     // the exchange before last drained this staging set with its H2D copies
     if (armed_[cur_]) GMT_CHECK("staging reuse", gmt_rt_event_synchronize(h2d_done_[cur_]));
+    // the receive stream writes ghost cells: only after everything the
+    // caller queued before this exchange (which may read them)
+    GMT_CHECK("event", gmt_rt_event_record(before_, s));
+    GMT_CHECK("stream wait", gmt_rt_stream_wait_event(hs_, before_));
     rreqs_.assign(rchunks_.size(), MPI_REQUEST_NULL);
     for (size_t k = 0; k < rchunks_.size(); ++k) {
       const Chunk& ch = rchunks_[k];
@@ -233,7 +245,7 @@ class MpiHostExchange : public Exchange {
       irecv(rstage_[cur_][ch.msg].data() + ch.off, ch.len, m.peer, m.tag, c_, &rreqs_[k]);
     }
     if (kernel_) {
-      // 1 MiB chunks: 32 workgroups each (2 x 16 B in flight per lane)
+      // kStageWgs workgroups sweep the chunks in order (2 x 16 B in flight per lane)
       ++epoch_;
       GMT_CHECK("stage D2H", gmt_stage_copy(static_cast<int>(schunks_.size()), table_.data(), counters_.data(),
                                             flags_.data(), epoch_, kStageWgs, s));
@@ -265,11 +277,11 @@ class MpiHostExchange : public Exchange {
       if (!ch.len) return;
       if (m.block.base) {
         if (any_flat_recv_) deferred.push_back(k);
-        else GMT_CHECK("stage scatter", gmt_stage_scatter(1, rtable_[cur_].data() + k, kScatterWgs, s));
+        else GMT_CHECK("stage scatter", gmt_stage_scatter(1, rtable_[cur_].data() + k, kScatterWgs, hs_));
         return;
       }
       GMT_CHECK("stage H2D", gmt_rt_memcpy_async(static_cast<char*>(m.buf) + ch.off,
-                                                 rstage_[cur_][ch.msg].data() + ch.off, ch.len, s));
+                                                 rstage_[cur_][ch.msg].data() + ch.off, ch.len, hs_));
     };
     auto land = [&](int n) {
       for (int q = 0; q < n; ++q) land_one(static_cast<size_t>(idx[q]));
@@ -345,13 +357,14 @@ class MpiHostExchange : public Exchange {
         size_t b = a + 1;
         while (b < deferred.size() && deferred[b] == deferred[b - 1] + 1) ++b;
         GMT_CHECK("stage scatter", gmt_stage_scatter(static_cast<int>(b - a), rtable_[cur_].data() + deferred[a],
-                                                     kScatterWgs, s));
+                                                     kScatterWgs, hs_));
         a = b;
       }
     }
     if (trace_) tr_.back().recvd = MPI_Wtime();
     waitall(sreqs, "mpi-host exchange");
-    GMT_CHECK("event", gmt_rt_event_record(h2d_done_[cur_], s));
+    GMT_CHECK("event", gmt_rt_event_record(h2d_done_[cur_], hs_));
+    GMT_CHECK("stream wait", gmt_rt_stream_wait_event(s, h2d_done_[cur_]));  // the caller's next work sees the ghosts
     armed_[cur_] = true;
     if (trace_) tr_.back().end = MPI_Wtime();
   }
@@ -413,7 +426,7 @@ class MpiHostExchange : public Exchange {
     }
     return t;
   }
-  static constexpr int kStageWgs = 32;
+  static constexpr int kStageWgs = 256;  // one per CU: enough posted writes in flight to fill the host link
   static constexpr int kScatterWgs = 32;
   MPI_Comm c_;
   std::vector<Msg> recvs_, sends_;
@@ -429,6 +442,8 @@ class MpiHostExchange : public Exchange {
   std::vector<gmt_event_t> events_;
   std::vector<MPI_Request> rreqs_;
   gmt_event_t h2d_done_[2] = {nullptr, nullptr};
+  gmt_stream_t hs_ = nullptr;      // the receive leg's stream
+  gmt_event_t before_ = nullptr;   // the caller's stream at start()
   bool armed_[2] = {false, false};
   int cur_ = 1;
   double wait_limit_s_ = 10.0;

@@ -455,9 +455,9 @@ static void strided_chunk(const gmt_stage_chunk& c, bool gather) {
 }
 
 // CPU backend of csrc/kernels/stage.hip: copy, then publish each chunk's flag
-int gmt_stage_copy(int n_chunks, const gmt_stage_chunk* chunks, unsigned*, uint64_t* flags, uint64_t value,
-                   int wgs_per_chunk, void*) {
-  if (n_chunks < 0 || wgs_per_chunk < 1 || (n_chunks > 0 && (!chunks || !flags))) return 1;
+int gmt_stage_copy(int n_chunks, const gmt_stage_chunk* chunks, unsigned*, uint64_t* flags, uint64_t value, int wgs,
+                   void*) {
+  if (n_chunks < 0 || wgs < 1 || (n_chunks > 0 && (!chunks || !flags))) return 1;
   for (int k = 0; k < n_chunks; ++k) {
     if (chunks[k].rows > 0) strided_chunk(chunks[k], true);
     else if (chunks[k].bytes > 0) std::memcpy(chunks[k].dst, chunks[k].src, static_cast<size_t>(chunks[k].bytes));

@@ -279,7 +279,9 @@ int gmt_ipc_exchange(const gmt_ipc_plan* plan, void* stream);
 
 /* ---- Kernel-driven host staging (csrc/kernels/stage.hip): one launch copies
  *      every chunk src -> dst (device memory -> page-locked host memory the
- *      GPU maps; or the reverse), G workgroups per chunk; once chunk k is
+ *      GPU maps; or the reverse): gmt_stage_copy's `wgs` workgroups each take
+ *      their slice of chunk 0, then of chunk 1, ... (chunks complete in
+ *      order); gmt_stage_scatter runs wgs_per_chunk per chunk.  Once chunk k is
  *      complete and visible system-wide, `value` is stored into flags[k]
  *      (GMT_SPACE_PINNED_COHERENT memory) so the host can hand chunk k to MPI
  *      while later chunks are still being copied.  The chunk table and the
@@ -300,7 +302,7 @@ typedef struct gmt_stage_chunk {
   double* block;
 } gmt_stage_chunk;
 int gmt_stage_copy(int n_chunks, const gmt_stage_chunk* chunks, unsigned* counters, uint64_t* flags,
-                   uint64_t value, int wgs_per_chunk, void* stream);
+                   uint64_t value, int wgs, void* stream);
 int gmt_stage_scatter(int n_chunks, const gmt_stage_chunk* chunks, int wgs_per_chunk, void* stream);
 
 /* One kernel per entry point: the variants the defaults were chosen against

@@ -26,10 +26,11 @@ constexpr int tb_strip_out(int K) { return tb_cols(K) - 2 * tb_left(K); }
 constexpr int tb_max_strips(int K) { return 8 / tb_stages(K); }
 constexpr int tb_default_strips(int K) { return tb_stages(K) == 1 ? 4 : 1; }
 // Sweep counts with an inline-halo (push) kernel: the face stores' two
-// per-lane offsets and three descriptors spill the K = 7-10 one-wave strips
+// per-lane offsets and three descriptors spill the K = 6-10 one-wave strips
 // (253-255 VGPRs without them; K = 10 since the exec-masked Dirichlet keep's
-// column masks took 8 SGPRs) and K = 14; the engine plans around them
-constexpr bool tb_push_built(int K) { return (K < 7 || K > 10) && K != 14; }
+// column masks took 8 SGPRs, K = 6 since the push body is chosen per wave)
+// and K = 14; the engine plans around them
+constexpr bool tb_push_built(int K) { return (K < 6 || K > 10) && K != 14; }
 
 }  // namespace tb
 }  // namespace gmt

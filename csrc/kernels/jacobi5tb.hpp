@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <atomic>
 #include <map>
 #include <mutex>
@@ -114,7 +116,19 @@ struct Args {
   // ghost cells of the neighbour's next input; nullptr: no neighbour that way
   const double* push[8];
   int64_t push_w;                // face width
+  // GMT_TB_WG_TRACE builds (scripts/build_variant.sh): per workgroup, its
+  // tile, start and end (s_memrealtime, 100 MHz) and hardware ids
+  uint64_t* wg_trace;
 };
+
+// Per-workgroup timeline (A/B variant builds only; the production code
+// object has none of it): scripts/build_variant.sh wgt
+//   's/#define GMT_TB_WG_TRACE 0/#define GMT_TB_WG_TRACE 1/', then
+// GMT_TB_WG_TRACE_FILE=path [GMT_TB_WG_TRACE_LAUNCH=n] writes launch n's
+// workgroups (tile, start, end, HW_ID, XCC_ID) and plan to path.
+#ifndef GMT_TB_WG_TRACE
+#define GMT_TB_WG_TRACE 0
+#endif
 
 // cache policy of the face stores into a neighbour's memory: system scope
 // (sc0 | sc1: written through to the memory that owns them, complete when
@@ -258,7 +272,10 @@ __device__ __forceinline__ void keep_cells(dv<NC>& v, const dv<NC>& c, const uin
 // runtime one costs the unrolled body its register allocation,
 // tests/test_kernel_resources.py); sig_step >= 0: once that step's row is
 // stored, this (output) wave publishes a row-band arrival (Args::rb_rect).
-template <int K, int J, bool EXACT, bool EDGE, bool RULE, bool UP, bool PUSH>
+// PUSH (inline halo exchange, output stage): bit 0 = this strip holds an x
+// face (W / E columns), bit 1 = this segment holds y-face rows (S / N); both:
+// the corner too.
+template <int K, int J, bool EXACT, bool EDGE, bool RULE, bool UP, int PUSH>
 __device__ __forceinline__ void run_stage(const Args& a, const double* __restrict__ u, double* __restrict__ un,
                                           char* ring, int lane, int64_t xs, int64_t xe, int64_t ys, int64_t ye,
                                           int nsteps, int sig_step, int xd) {
@@ -271,8 +288,9 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   constexpr int kP = C::P, kRS = C::RS, kHS = C::HS;
   constexpr uint32_t kRow = C::ROW;
   constexpr int D = C::DLAG * J;                     // step lag behind stage 0
-  // global stores per step (PUSH: three face groups more, see below)
-  constexpr int SPS = kOut ? (EDGE ? NC : (PUSH ? 4 : 1) * (NC / 2)) : 0;
+  // global stores per step (PUSH: one face group more per face held, and the corner)
+  constexpr int kGroups = 1 + (PUSH & 1) + ((PUSH >> 1) & 1) + (PUSH == 3 ? 1 : 0);
+  constexpr int SPS = kOut ? (EDGE ? NC : kGroups * (NC / 2)) : 0;
   static_assert(!(PUSH && EDGE), "inline halo exchange: no odd-edge stores");
   // DMAs per step: stage 0 loads the whole row
   constexpr bool kDma = kIn;
@@ -337,14 +355,15 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   // cells of this strip's output are stored a second time, into the
   // neighbours' ghost cells — the y face this segment holds (S or N rows),
   // the x face this strip holds (xd: W or E columns; per-lane offsets xp),
-  // and their corner (diagonal neighbour).  All three store groups are
-  // issued every step: a descriptor with nothing of this wave's output in
-  // range (a face this wave does not hold, a row outside the face) drops
-  // them in the buffer unit, with no branch in the unrolled step.
+  // and their corner (diagonal neighbour).  The groups of the faces this
+  // wave holds (PUSH bits) are issued every step: a descriptor with nothing
+  // of this wave's output in range (a row outside the face, a corner not
+  // pushed) drops them in the buffer unit, with no branch in the unrolled
+  // step.  Waves holding no face run PUSH = 0, the plain body.
   __amdgpu_buffer_rsrc_t prs_y = row_rsrc(un, 0), prs_x = row_rsrc(un, 0), prs_c = row_rsrc(un, 0);
   uint32_t psh = 0;  // the y face's first row relative to ys, in bytes
   uint32_t xp[NC / 2];
-  if constexpr (PUSH && kOut) {
+  if constexpr (PUSH != 0 && kOut) {
     const int64_t w = a.push_w;
     int yd = -1;
     int64_t fy0 = 0, fy1 = 0;
@@ -387,16 +406,16 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
         constexpr int q = decltype(Q)::value;
         __builtin_amdgcn_raw_buffer_store_b128(pack2(v.c[2 * q], v.c[2 * q + 1]), srs, stp[q] + ro, 0, 2 /* nt */);
       });
-      if constexpr (PUSH) {
+      if constexpr (PUSH != 0) {
         // (rows before the face wrap to offsets far past the range: the
         // segment's rows times ld8 stay below 2^31, launch_tb's lmax)
         const uint32_t ry = ro - psh;
         static_for<0, NC / 2>([&](auto Q) {
           constexpr int q = decltype(Q)::value;
           const u4 d = pack2(v.c[2 * q], v.c[2 * q + 1]);
-          __builtin_amdgcn_raw_buffer_store_b128(d, prs_y, stp[q] + ry, 0, kPushAux);
-          __builtin_amdgcn_raw_buffer_store_b128(d, prs_x, xp[q] + ro, 0, kPushAux);
-          __builtin_amdgcn_raw_buffer_store_b128(d, prs_c, xp[q] + ry, 0, kPushAux);
+          if constexpr (PUSH & 2) __builtin_amdgcn_raw_buffer_store_b128(d, prs_y, stp[q] + ry, 0, kPushAux);
+          if constexpr (PUSH & 1) __builtin_amdgcn_raw_buffer_store_b128(d, prs_x, xp[q] + ro, 0, kPushAux);
+          if constexpr (PUSH == 3) __builtin_amdgcn_raw_buffer_store_b128(d, prs_c, xp[q] + ry, 0, kPushAux);
         });
       }
       if constexpr (EDGE) {
@@ -671,13 +690,15 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   const bool pw = PUSH && (a.push[GMT_PUSH_W] || a.push[GMT_PUSH_SW] || a.push[GMT_PUSH_NW]);
   const bool pe = PUSH && (a.push[GMT_PUSH_E] || a.push[GMT_PUSH_SE] || a.push[GMT_PUSH_NE]);
   const int xd = !PUSH ? -1 : (strip == 0 && pw) ? GMT_PUSH_W : (strip == a.nstrip[k] - 1 && pe) ? GMT_PUSH_E : -1;
-  // the waves that hold no face (most of them) run the plain output body:
-  // the face stores of the push body are issued every step, in range or not
-  const bool push_here = PUSH && (xd >= 0 ||
-                                  ((a.push[GMT_PUSH_S] || a.push[GMT_PUSH_SW] || a.push[GMT_PUSH_SE]) &&
-                                   ys < a.dom[2] + a.push_w) ||
-                                  ((a.push[GMT_PUSH_N] || a.push[GMT_PUSH_NW] || a.push[GMT_PUSH_NE]) &&
-                                   ye > a.dom[2] + a.dom[3] - a.push_w));
+  // the output body by the faces this wave holds (the face stores are
+  // issued every step, in range or not): most waves hold none and run the
+  // plain body, the first / last strip an x face, the segments at the S / N
+  // face rows a y face
+  const bool py = PUSH && (((a.push[GMT_PUSH_S] || a.push[GMT_PUSH_SW] || a.push[GMT_PUSH_SE]) &&
+                            ys < a.dom[2] + a.push_w) ||
+                           ((a.push[GMT_PUSH_N] || a.push[GMT_PUSH_NW] || a.push[GMT_PUSH_NE]) &&
+                            ye > a.dom[2] + a.dom[3] - a.push_w));
+  const int pm = (xd >= 0 ? 1 : 0) | (py ? 2 : 0);
   using T = std::true_type;
   using F = std::false_type;
   auto go = [&](auto jc, auto rule_c, auto up_c, int sstep) {
@@ -686,11 +707,15 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
       run_stage<K, j, EXACT, EDGE, decltype(rule_c)::value, decltype(up_c)::value, decltype(push_c)::value>(
           a, u, un, ring, lane, xs, xe, ys, ye, nsteps, sstep, xd);
     };
+    using P0 = std::integral_constant<int, 0>;
     if constexpr (PUSH && j == G - 1) {
-      if (push_here) run(T{});
-      else run(F{});
+      // (two bodies: one per face group — x alone, y alone — spills the
+      // kernel: 71-93 VGPRs of scratch; a wave holding any face runs all
+      // three groups, the ones it does not hold dropped by their descriptors)
+      if (pm != 0) run(std::integral_constant<int, 3>{});
+      else run(P0{});
     } else {
-      run(F{});
+      run(P0{});
     }
   };
   auto stage_go = [&](auto jc, int sstep) {
@@ -728,7 +753,23 @@ void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__
   // signalling workgroups (and row bands) first, in dispatch order over all
   // XCDs; the rest XCD-contiguous
   const int64_t t = b < nd ? b : nd + xcd_swizzle(b - nd, nblocks - nd);
+#if GMT_TB_WG_TRACE
+  const uint64_t wg_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   tb_block<K, EXACT, EDGE, PUSH>(a, u, un, t);
+#if GMT_TB_WG_TRACE
+  __syncthreads();
+  if (threadIdx.x == 0 && a.wg_trace) {
+    const uint64_t wg_t1 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+    const uint64_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    uint64_t* o = a.wg_trace + 4 * b;  // vector stores (a VGPR address)
+    o[0] = static_cast<uint64_t>(t);
+    o[1] = wg_t0;
+    o[2] = wg_t1;
+    o[3] = hw | (xcc << 32);
+  }
+#endif
   if (t < ns) {
     // every wave's stores written back past its XCD's L2, then one arrival
     // per workgroup (vector atomics on uncached memory)
@@ -776,23 +817,43 @@ struct SegPlan {
 // The step cost of a rule-path wave relative to a plain one (the planner's
 // model).  Loop census at K = 20 per 19 steps: round 4's per-cell select
 // 5837 vs 3218 VALU (1.8); the exec-masked keep 3882 VALU + 1711 SALU vs
-// 3150 VALU + 319 SALU.  GMT_TB_RULE_COST=c overrides it (A/B).
+// 3150 VALU + 319 SALU (1.23x the VALU) — yet plans made with 1.2-1.5 run
+// 2-10% slower than with 1.8 on every Dirichlet domain measured
+// (profiles/r05_rule_keep/rule_cost_sweep.txt): a rule wave still takes
+// ~1.8x a plain one's time.  GMT_TB_RULE_COST=c overrides it (A/B).
 inline double tb_rule_cost() {
   static const double c = [] {
     const char* e = std::getenv("GMT_TB_RULE_COST");
     const double v = e ? std::atof(e) : 0.0;
-    return v >= 1.0 && v <= 4.0 ? v : 1.3;
+    return v >= 1.0 && v <= 4.0 ? v : 1.8;
+  }();
+  return c;
+}
+
+// The step cost of a wave running the inline-halo body (three face store
+// groups per step, the ones out of range dropped) relative to a plain one:
+// a one-round pass whose push waves had plain-length segments ran
+// 1.11-1.14x (profiles/r05_overlap/).  GMT_TB_PUSH_COST=c overrides it.
+inline double tb_push_cost() {
+  static const double c = [] {
+    const char* e = std::getenv("GMT_TB_PUSH_COST");
+    const double v = e ? std::atof(e) : 0.0;
+    return v >= 1.0 && v <= 4.0 ? v : 1.15;
   }();
   return c;
 }
 
 template <int K>
-// push_ns (inline halo exchange with both S and N faces pushed): every
-// segment holds at most one of the two faces (launch_tb: ny >= 2 w + 2), so
-// at least two segments per strip group.
+// push_sides (inline halo exchange, the one rect is the interior): the faces
+// pushed, bits 1 W, 2 E, 4 S, 8 N (a corner counts for both its faces).  The
+// waves holding a face run the push body: the S / N face rows get edge
+// segments of their own and the W / E strips' groups shorter segments, both
+// priced at tb_push_cost().  With both S and N pushed every segment holds at
+// most one of the two faces (launch_tb: ny >= 2 w + 2).
 SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t resident_wgs, int sig_rects, int rb_rect = -1,
-                      int rb = 0, int64_t rb_min = 0, bool push_ns = false) {
+                      int rb = 0, int64_t rb_min = 0, int push_sides = 0) {
   SegPlan p{};
+  const bool push_ns = (push_sides & 12) == 12;
   // A rule segment costs ~tb_rule_cost() times the steps of a plain one.  Edge segments
   // (at a Dirichlet row) are either short (64 rows: many of them pack well
   // into the tail of a multi-round launch) or "balanced" — as long as makes
@@ -800,22 +861,29 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
   // (the N = 8 shares, 8192^2) neither waits for them nor leaves their slots
   // idle; the makespan search tries both.  Strip groups that reach a
   // Dirichlet column run the rule path at every step: balanced segments.
-  const double fr = tb_rule_cost();
+  const double fr = tb_rule_cost(), fp = tb_push_cost();
   constexpr int64_t kWarm = 2 * K + Cfg<K>::LAG, kU = Cfg<K>::U;
-  // a rule segment's rows such that its steps (whole unrolled blocks of kU)
-  // cost at most those of an L-row plain one
-  auto balanced = [fr](int64_t L) {
+  // a segment's rows such that its steps (whole unrolled blocks of kU) at
+  // cost factor f cost at most those of an L-row plain one
+  auto balanced = [](int64_t L, double f) {
     const int64_t st = (L + kWarm + kU - 1) / kU * kU;
-    const int64_t blocks = static_cast<int64_t>(static_cast<double>(st) / (fr * kU) + 1e-9);
+    const int64_t blocks = static_cast<int64_t>(static_cast<double>(st) / (f * kU) + 1e-9);
     return std::max<int64_t>(64, blocks * kU - kWarm);
+  };
+  // per-side cost factors of rect k's waves: rule path (Dirichlet side) and
+  // push body (pushed face), out[0..3] = W, E, S, N
+  auto side_cost = [&](int k, double* out) {
+    const int64_t ry0 = a.r[k][2], ry1 = ry0 + a.r[k][3], rx0 = a.r[k][0], rx1 = rx0 + a.r[k][1];
+    const bool rule[4] = {rx0 - Cfg<K>::KL < a.dom[0] && !(a.mask & 1), rx1 + Cfg<K>::KL > a.dom[0] + a.dom[1] && !(a.mask & 2),
+                          ry0 - K < a.dom[2] && !(a.mask & 4), ry1 + K > a.dom[2] + a.dom[3] && !(a.mask & 8)};
+    for (int d = 0; d < 4; ++d) out[d] = (rule[d] ? fr : 1.0) * ((push_sides >> d) & 1 ? fp : 1.0);
   };
   bool long_edges = false;
   auto fill = [&](int64_t L0, int64_t* wgs) {
-    const int64_t edge = long_edges ? balanced(L0) : std::max<int64_t>(64, K);
     int64_t w = 0;
     for (int k = 0; k < a.n; ++k) {
       int64_t L = L0;
-      const int64_t ny = a.r[k][3], ry0 = a.r[k][2], ry1 = ry0 + ny;
+      const int64_t ny = a.r[k][3];
       if (k < sig_rects) {
         const int64_t lb = std::min<int64_t>(std::max<int64_t>(128, L - L / 4), lmax);
         p.e0[k] = p.e1[k] = 0;
@@ -824,12 +892,16 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
         w += (a.nstrip[k] + a.nw - 1) / a.nw * p.nmid[k];
         continue;
       }
-      const bool top = seg_rows == 0 && ry0 - K < a.dom[2] && !(a.mask & 4);
-      const bool bot = seg_rows == 0 && ry1 + K > a.dom[2] + a.dom[3] && !(a.mask & 8);
+      double sc[4];
+      side_cost(k, sc);
+      // edge segments where the row sides cost more (a Dirichlet row, a pushed face)
+      const bool top = seg_rows == 0 && sc[2] > 1.0, bot = seg_rows == 0 && sc[3] > 1.0;
+      const int64_t edge0 = long_edges ? balanced(L0, sc[2]) : std::max<int64_t>(64, K);
+      const int64_t edge1 = long_edges ? balanced(L0, sc[3]) : std::max<int64_t>(64, K);
       p.e0[k] = p.e1[k] = 0;
-      if (ny > 2 * edge + 64) {  // room for edges and an interior
-        p.e0[k] = top ? edge : 0;
-        p.e1[k] = bot ? edge : 0;
+      if (ny > edge0 + edge1 + 64) {  // room for edges and an interior
+        p.e0[k] = top ? edge0 : 0;
+        p.e1[k] = bot ? edge1 : 0;
       }
       int64_t mid = ny - p.e0[k] - p.e1[k];
       if (k == rb_rect && rb > 0) L = std::min<int64_t>(L, std::max<int64_t>(rb_min, mid / rb));
@@ -840,20 +912,18 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
         // the edges' length follows the interior segments' final length (a
         // few fixed-point steps: both depend on each other)
         for (int it = 0; it < 4; ++it) {
-          const int64_t e = std::min<int64_t>(balanced(p.lmid[k]), (ny - 64) / 2);
-          p.e0[k] = p.e0[k] > 0 ? e : 0;
-          p.e1[k] = p.e1[k] > 0 ? e : 0;
+          p.e0[k] = p.e0[k] > 0 ? std::min<int64_t>(balanced(p.lmid[k], sc[2]), (ny - 64) / 2) : 0;
+          p.e1[k] = p.e1[k] > 0 ? std::min<int64_t>(balanced(p.lmid[k], sc[3]), (ny - 64) / 2) : 0;
           mid = ny - p.e0[k] - p.e1[k];
           p.lmid[k] = (mid + p.nmid[k] - 1) / p.nmid[k];
         }
       }
       // strip groups that can reach a Dirichlet column run the rule path
-      // (tb_rule_cost() per step): shorter segments, so they finish with the
-      // others instead of ending the launch
-      const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
-      const bool xrule = seg_rows == 0 && ((rx0 - Cfg<K>::KL < a.dom[0] && !(a.mask & 1)) ||
-                                           (rx1 + Cfg<K>::KL > a.dom[0] + a.dom[1] && !(a.mask & 2)));
-      int64_t lb = xrule ? balanced(p.lmid[k]) : p.lmid[k];
+      // (tb_rule_cost() per step), the W / E strips of a push pass the push
+      // body: shorter segments, so they finish with the others instead of
+      // ending the launch
+      const double fx = seg_rows == 0 ? std::max(sc[0], sc[1]) : 1.0;
+      int64_t lb = fx > 1.0 ? balanced(p.lmid[k], fx) : p.lmid[k];
       if (k == rb_rect && rb > 0) lb = std::min<int64_t>(lb, std::max<int64_t>(rb_min, mid / rb));
       if (push_ns) lb = std::min<int64_t>(lb, (mid + 1) / 2);
       p.nmid_b[k] = (mid + lb - 1) / lb;
@@ -896,17 +966,20 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
     dur.clear();
     for (int k = 0; k < a.n; ++k) {
       const int64_t groups = (a.nstrip[k] + a.nw - 1) / a.nw, nbnd = groups < 2 ? groups : 2;
-      const int64_t ny = a.r[k][3], ry0 = a.r[k][2], ry1 = ry0 + ny;
-      const bool yrule = (ry0 - K < a.dom[2] && !(a.mask & 4)) || (ry1 + K > a.dom[2] + a.dom[3] && !(a.mask & 8));
-      const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
-      const bool xrule = (rx0 - Cfg<K>::KL < a.dom[0] && !(a.mask & 1)) ||
-                         (rx1 + Cfg<K>::KL > a.dom[0] + a.dom[1] && !(a.mask & 2));
-      const double fe = yrule ? fr : 1.0;              // an edge segment touches its Dirichlet row
-      const double fb = xrule || (yrule && p.e0[k] == 0 && p.e1[k] == 0) ? fr : 1.0;
-      const double fm = yrule && p.e0[k] == 0 && p.e1[k] == 0 ? fr : 1.0;
+      double sc[4];
+      side_cost(k, sc);
+      // a workgroup's factor: the rule path if any side it touches is a
+      // Dirichlet one, the push body if it holds any face; without edge
+      // segments the row sides fall to the first / last interior segments
+      // (modelled on all of them)
+      const double fx = std::max(sc[0], sc[1]);
+      const bool edges = p.e0[k] > 0 || p.e1[k] > 0;
+      const double fy = edges ? 1.0 : std::max(sc[2], sc[3]);
+      const double fb = std::max(fx, fy), fm = fy;
       for (int64_t g = 0; g < groups; ++g) {
-        if (p.e0[k] > 0) dur.push_back(fe * steps(p.e0[k]));
-        if (p.e1[k] > 0) dur.push_back(fe * steps(p.e1[k]));
+        const bool bnd = g == 0 || g == groups - 1;
+        if (p.e0[k] > 0) dur.push_back((bnd ? std::max(sc[2], fx) : sc[2]) * steps(p.e0[k]));
+        if (p.e1[k] > 0) dur.push_back((bnd ? std::max(sc[3], fx) : sc[3]) * steps(p.e1[k]));
       }
       for (int64_t g = 0; g < nbnd; ++g)
         for (int64_t m = 0; m < p.nmid_b[k]; ++m) dur.push_back(fb * steps(p.lmid_b[k]));
@@ -994,7 +1067,7 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   a.mask = mask;
   a.quarter = 0.25;
   for (int j = 0; j < 4; ++j) a.dom[j] = dom[j];
-  bool push_ns = false;
+  int push_sides = 0;  // plan_segments: faces pushed, 1 W, 2 E, 4 S, 8 N
   if constexpr (PUSH) {
     // gmt_tb_opts.push: the one rect is the interior, an even face width,
     // room for two segments clear of each other's face, no signals
@@ -1007,7 +1080,8 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     a.push_w = w;
     // (a face counts as pushed when only its corners are)
     const auto any = [&](int d0, int d1, int d2) { return o.push[d0] || o.push[d1] || o.push[d2]; };
-    push_ns = any(GMT_PUSH_S, GMT_PUSH_SW, GMT_PUSH_SE) && any(GMT_PUSH_N, GMT_PUSH_NW, GMT_PUSH_NE);
+    push_sides = (any(GMT_PUSH_W, GMT_PUSH_SW, GMT_PUSH_NW) ? 1 : 0) | (any(GMT_PUSH_E, GMT_PUSH_SE, GMT_PUSH_NE) ? 2 : 0) |
+                 (any(GMT_PUSH_S, GMT_PUSH_SW, GMT_PUSH_SE) ? 4 : 0) | (any(GMT_PUSH_N, GMT_PUSH_NW, GMT_PUSH_NE) ? 8 : 0);
     // a strip pushes one x face
     if (any(GMT_PUSH_W, GMT_PUSH_SW, GMT_PUSH_NW) && any(GMT_PUSH_E, GMT_PUSH_SE, GMT_PUSH_NE) &&
         (dom[1] + C::WOUT - 1) / C::WOUT < 2)
@@ -1077,7 +1151,7 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   // search costs milliseconds; the engine launches the same passes over and over)
   SegPlan sp;
   {
-    std::vector<int64_t> key = {a.n, a.nw, a.mask, o.seg_rows, lmax, per_cu, sig_rects, rbk, rbs + rbn, rb_min, push_ns};
+    std::vector<int64_t> key = {a.n, a.nw, a.mask, o.seg_rows, lmax, per_cu, sig_rects, rbk, rbs + rbn, rb_min, push_sides};
     for (int k = 0; k < a.n; ++k) key.insert(key.end(), a.r[k], a.r[k] + 4);
     key.insert(key.end(), a.dom, a.dom + 4);
     static std::mutex mu;
@@ -1086,7 +1160,7 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     auto it = cache.find(key);
     if (it == cache.end()) {
       if (cache.size() > 256) cache.clear();
-      it = cache.emplace(key, plan_segments<K>(a, o.seg_rows, lmax, per_cu, sig_rects, rbk, rbs + rbn, rb_min, push_ns)).first;
+      it = cache.emplace(key, plan_segments<K>(a, o.seg_rows, lmax, per_cu, sig_rects, rbk, rbs + rbn, rb_min, push_sides)).first;
     }
     sp = it->second;
   }
@@ -1151,7 +1225,46 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     for (int j = 0; j < 6; ++j) info[j] = v[j];
     return 0;
   }
+#if GMT_TB_WG_TRACE
+  static std::atomic<int> trace_launch{0};
+  static uint64_t* trace_buf = nullptr;
+  static int64_t trace_cap = 0;
+  const char* trace_file = std::getenv("GMT_TB_WG_TRACE_FILE");
+  const char* trace_at = std::getenv("GMT_TB_WG_TRACE_LAUNCH");
+  const bool tracing = trace_file && trace_launch++ == (trace_at ? std::atoi(trace_at) : 50);
+  if (tracing) {
+    if (trace_cap < nb) {
+      if (trace_buf) (void)hipFree(trace_buf);
+      if (hipMalloc(&trace_buf, static_cast<size_t>(nb) * 32) != hipSuccess) return static_cast<int>(hipErrorOutOfMemory);
+      trace_cap = nb;
+    }
+    (void)hipMemsetAsync(trace_buf, 0, static_cast<size_t>(nb) * 32, s);
+    a.wg_trace = trace_buf;
+  }
+#endif
   jacobi5tb_kernel<K, EXACT, EDGE, PUSH><<<grid_1d(nb), a.nw * G * kWave, smem, s>>>(a, u, un, nb);
+#if GMT_TB_WG_TRACE
+  if (tracing) {
+    std::vector<uint64_t> h(static_cast<size_t>(nb) * 4);
+    if (hipStreamSynchronize(s) == hipSuccess &&
+        hipMemcpy(h.data(), trace_buf, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      if (FILE* f = std::fopen(trace_file, "w")) {
+        std::fprintf(f, "# K %d nb %lld per_cu %lld nw %d n %d mask %d rect0 %lld %lld %lld %lld nstrip %lld "
+                        "e0 %lld e1 %lld nmid %lld lmid %lld nmid_b %lld lmid_b %lld sig_dispatch %lld\n",
+                     K, (long long)nb, (long long)per_cu, a.nw, a.n, a.mask, (long long)a.r[0][0], (long long)a.r[0][1],
+                     (long long)a.r[0][2], (long long)a.r[0][3], (long long)a.nstrip[0], (long long)a.e0[0],
+                     (long long)a.e1[0], (long long)a.nmid[0], (long long)a.lmid[0], (long long)a.nmid_b[0],
+                     (long long)a.lmid_b[0], (long long)a.sig_dispatch);
+        std::fprintf(f, "# block tile start end hw_id xcc_id\n");
+        for (int64_t i = 0; i < nb; ++i)
+          std::fprintf(f, "%lld %llu %llu %llu %llu %llu\n", (long long)i, (unsigned long long)h[4 * i],
+                       (unsigned long long)h[4 * i + 1], (unsigned long long)h[4 * i + 2],
+                       (unsigned long long)(h[4 * i + 3] & 0xffffffffu), (unsigned long long)(h[4 * i + 3] >> 32));
+        std::fclose(f);
+      }
+    }
+  }
+#endif
   return static_cast<int>(hipGetLastError());
 }
 

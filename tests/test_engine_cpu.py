@@ -199,7 +199,7 @@ def test_ipc_plan_refuses_mismatched_face_layouts():
     assert "disagree on the face layout" in str(ei.value), str(ei.value)[-3000:]
 
 
-@pytest.mark.parametrize("ny,nx,steps,k", [(70, 300, 23, 6), (90, 600, 41, 20), (64, 520, 9, 4)])
+@pytest.mark.parametrize("ny,nx,steps,k", [(70, 300, 23, 4), (90, 600, 41, 20), (64, 520, 9, 2)])
 def test_native_engine_push_one_rank_periodic(ny, nx, steps, k):
     """Inline halo exchange on one rank, periodic on both axes: every pass
     stores its faces straight into the ghost cells of its own next input
@@ -223,7 +223,7 @@ def test_native_engine_push_one_rank_periodic(ny, nx, steps, k):
 @pytest.mark.parametrize("np_,ny,nx,steps,periodic,tblock,dims", [
     (2, 100, 600, 23, False, 12, "1x2"),
     (2, 140, 300, 41, True, 20, "2x1"),
-    (4, 150, 700, 27, False, 6, "2x2"),
+    (4, 150, 700, 27, False, 4, "2x2"),
     (4, 120, 1100, 20, True, 12, "2x2"),
     (6, 190, 800, 31, True, 12, "3x2"),
     (8, 210, 1200, 45, False, 20, "2x4"),

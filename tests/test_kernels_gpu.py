@@ -320,6 +320,14 @@ def test_stage_gather_scatter_field_blocks(rows, cols, chunk):
     packed = face.contiguous().reshape(-1).cpu()   # packed column by column: rows per column contiguous
     assert torch.equal(stage, packed)
     assert (flags == 7).all()
+    # again with more workgroups than a chunk has 16-B pieces (empty slices),
+    # the arrival counters back at zero
+    assert (counters == 0).all()
+    stage.zero_()
+    _native.check(L.gmt_stage_copy(nchunk, table.data_ptr(), counters.data_ptr(), flags.data_ptr(), 8, 300, _stream()),
+                  "stage_copy")
+    torch.cuda.synchronize()
+    assert torch.equal(stage, packed) and (flags == 8).all() and (counters == 0).all()
     # scatter into another field's block
     out = torch.full_like(field, -1.0)
     dst = out[:, 9:9 + rows]

@@ -26,7 +26,7 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
 DIRS = ("S", "N", "W", "E", "SW", "SE", "NW", "NE")
-NO_PUSH = (7, 8, 9, 10, 14)  # gmt::tb::tb_push_built (csrc/include/gmt/tb_geom.h)
+NO_PUSH = (6, 7, 8, 9, 10, 14)  # gmt::tb::tb_push_built (csrc/include/gmt/tb_geom.h)
 
 
 @pytest.fixture(autouse=True, scope="module")
@@ -100,7 +100,7 @@ def env():
     return gd.init(device="cuda")
 
 
-@pytest.mark.parametrize("ny,nx,steps,k", [(300, 700, 43, 20), (257, 1031, 29, 12), (520, 600, 17, 6)])
+@pytest.mark.parametrize("ny,nx,steps,k", [(300, 700, 43, 20), (257, 1031, 29, 12), (520, 600, 17, 4)])
 def test_push_engine_one_rank_periodic(env, ny, nx, steps, k):
     """The engine's inline halo on one GPU rank, periodic on both axes: the
     faces of every pass land in its own next input (no exchange between
@@ -129,7 +129,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     (2, 400, 900, 45, True, 20, "2x1"),
     (2, 300, 1200, 33, False, 12, "1x2"),
     (4, 600, 1100, 60, True, 20, "2x2"),
-    (4, 500, 1300, 29, False, 6, "2x2"),
+    (4, 500, 1300, 29, False, 4, "2x2"),
 ])
 def test_push_engine_ranks_sharing_the_gpu(np_, ny, nx, steps, periodic, k, dims):
     """np_ ranks on cuda:0 (IPC mappings of the same device, socket control
