@@ -121,9 +121,12 @@ class MpiTransport : public Transport {
 //          after each; no host wait, so the caller's kernels queue right away.
 //   wait:  send each chunk as soon as its D2H event has completed (MPI keeps
 //          the chunks of one message in order: same peer, tag, communicator),
-//          and enqueue each received chunk's H2D copy as soon as it lands (on
-//          the exchange's own receive stream, joined back into the caller's
-//          at the end), so D2H, the wire and H2D of different chunks overlap.
+//          and enqueue each received chunk's H2D copy as soon as it lands, so
+//          D2H, the wire and H2D of different chunks overlap.  Flat chunks'
+//          copies run on a stream of their own (8 MiB, ranks bound: 15.8 ->
+//          20 GB/s per rank); field-block scatter kernels stay on the caller's
+//          stream (on a second stream they took mpi_stencil2d_sycl from 1.3 to
+//          1.9 ms: profiles/r05_xport/).
 // Receive staging is double-buffered across exchanges: the next exchange's
 // receives never wait for this one's H2D copies to drain.
 // Device -> host leg (GMT_HOST_STAGE): "kernel" (default) — one gmt_stage_copy
@@ -208,11 +211,16 @@ class MpiHostExchange : public Exchange {
       }
     }
     for (auto& e : h2d_done_) GMT_CHECK("event", gmt_rt_event_create(&e, 0));
-    // the receive leg (H2D copies, scatters) runs on a stream of its own, so
-    // a chunk that lands goes to the device at once instead of queueing
-    // behind the staging kernel on the caller's stream (profiles/r05_xport/)
-    GMT_CHECK("stream", gmt_rt_stream_create(&hs_, 1));
-    GMT_CHECK("event", gmt_rt_event_create(&before_, 0));
+    // flat receive chunks go to the device on a stream of their own (SDMA
+    // copies that start as a chunk lands, instead of queueing behind the
+    // staging kernel on the caller's stream; field blocks keep their scatter
+    // kernels on the caller's stream: profiles/r05_xport/)
+    const char* rs = std::getenv("GMT_HOST_RECV_STREAM");  // A/B: 0 = the caller's stream
+    if (any_flat_recv_ && !(rs && std::atoi(rs) == 0)) {
+      GMT_CHECK("stream", gmt_rt_stream_create(&hs_, 1));
+      GMT_CHECK("event", gmt_rt_event_create(&before_, 0));
+      GMT_CHECK("event", gmt_rt_event_create(&flat_done_, 0));
+    }
     // the staging poll gives up after this long WITHOUT a chunk staged (the
     // clock restarts at every staged chunk).  The first chunk also waits for
     // whatever the stream holds ahead of the staging kernel, so the default
@@ -226,18 +234,21 @@ class MpiHostExchange : public Exchange {
     if (trace_ && !tr_.empty()) trace_dump();
     for (auto& e : events_) gmt_rt_event_destroy(e);
     for (auto& e : h2d_done_) gmt_rt_event_destroy(e);
-    gmt_rt_event_destroy(before_);
-    gmt_rt_stream_destroy(hs_);
+    if (hs_) {
+      gmt_rt_event_destroy(before_);
+      gmt_rt_event_destroy(flat_done_);
+      gmt_rt_stream_destroy(hs_);
+    }
   }
   void start(gmt_stream_t s) override {
     if (trace_) trace_start();
     cur_ ^= 1;
     // the exchange before last drained this staging set with its H2D copies
     if (armed_[cur_]) GMT_CHECK("staging reuse", gmt_rt_event_synchronize(h2d_done_[cur_]));
-    // the receive stream writes ghost cells: only after everything the
-    // caller queued before this exchange (which may read them)
-    GMT_CHECK("event", gmt_rt_event_record(before_, s));
-    GMT_CHECK("stream wait", gmt_rt_stream_wait_event(hs_, before_));
+    if (hs_) {  // the flat copies write device buffers the caller's earlier work may read
+      GMT_CHECK("event", gmt_rt_event_record(before_, s));
+      GMT_CHECK("stream wait", gmt_rt_stream_wait_event(hs_, before_));
+    }
     rreqs_.assign(rchunks_.size(), MPI_REQUEST_NULL);
     for (size_t k = 0; k < rchunks_.size(); ++k) {
       const Chunk& ch = rchunks_[k];
@@ -277,11 +288,11 @@ class MpiHostExchange : public Exchange {
       if (!ch.len) return;
       if (m.block.base) {
         if (any_flat_recv_) deferred.push_back(k);
-        else GMT_CHECK("stage scatter", gmt_stage_scatter(1, rtable_[cur_].data() + k, kScatterWgs, hs_));
+        else GMT_CHECK("stage scatter", gmt_stage_scatter(1, rtable_[cur_].data() + k, kScatterWgs, s));
         return;
       }
       GMT_CHECK("stage H2D", gmt_rt_memcpy_async(static_cast<char*>(m.buf) + ch.off,
-                                                 rstage_[cur_][ch.msg].data() + ch.off, ch.len, hs_));
+                                                 rstage_[cur_][ch.msg].data() + ch.off, ch.len, hs_ ? hs_ : s));
     };
     auto land = [&](int n) {
       for (int q = 0; q < n; ++q) land_one(static_cast<size_t>(idx[q]));
@@ -351,20 +362,23 @@ class MpiHostExchange : public Exchange {
                                  MPI_STATUSES_IGNORE));
       if (n > 0 && n != MPI_UNDEFINED) land(n);
     }
+    if (hs_) {  // the flat copies joined back into the caller's stream
+      GMT_CHECK("event", gmt_rt_event_record(flat_done_, hs_));
+      GMT_CHECK("stream wait", gmt_rt_stream_wait_event(s, flat_done_));
+    }
     if (!deferred.empty()) {  // the field blocks, after every flat copy
       std::sort(deferred.begin(), deferred.end());
       for (size_t a = 0; a < deferred.size();) {  // runs of consecutive chunks: one launch each
         size_t b = a + 1;
         while (b < deferred.size() && deferred[b] == deferred[b - 1] + 1) ++b;
         GMT_CHECK("stage scatter", gmt_stage_scatter(static_cast<int>(b - a), rtable_[cur_].data() + deferred[a],
-                                                     kScatterWgs, hs_));
+                                                     kScatterWgs, s));
         a = b;
       }
     }
     if (trace_) tr_.back().recvd = MPI_Wtime();
     waitall(sreqs, "mpi-host exchange");
-    GMT_CHECK("event", gmt_rt_event_record(h2d_done_[cur_], hs_));
-    GMT_CHECK("stream wait", gmt_rt_stream_wait_event(s, h2d_done_[cur_]));  // the caller's next work sees the ghosts
+    GMT_CHECK("event", gmt_rt_event_record(h2d_done_[cur_], s));
     armed_[cur_] = true;
     if (trace_) tr_.back().end = MPI_Wtime();
   }
@@ -442,8 +456,8 @@ class MpiHostExchange : public Exchange {
   std::vector<gmt_event_t> events_;
   std::vector<MPI_Request> rreqs_;
   gmt_event_t h2d_done_[2] = {nullptr, nullptr};
-  gmt_stream_t hs_ = nullptr;      // the receive leg's stream
-  gmt_event_t before_ = nullptr;   // the caller's stream at start()
+  gmt_stream_t hs_ = nullptr;  // flat receive chunks' H2D copies
+  gmt_event_t before_ = nullptr, flat_done_ = nullptr;
   bool armed_[2] = {false, false};
   int cur_ = 1;
   double wait_limit_s_ = 10.0;

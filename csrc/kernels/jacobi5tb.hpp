@@ -11,6 +11,7 @@
 #include <atomic>
 #include <map>
 #include <mutex>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -1215,6 +1216,18 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   // (Dispatching the rule-path workgroups round-robin over the XCDs instead
   // of XCD-contiguous with the rest cost the Dirichlet 8192 x 16384 and
   // 16384 x 8192 passes 3-6%: profiles/r04_shares.md.)
+  // A/B (GMT_TB_SPECIAL_RR=1): a one-rect pass without signals dispatches its
+  // edge segments and boundary groups round-robin over the XCDs; XCD-contiguous
+  // ranges put them all on XCD 0, which then finished 20-30% early on every
+  // Dirichlet domain traced (profiles/r05_wg_timeline/)
+  static const bool special_rr = [] {
+    const char* e = std::getenv("GMT_TB_SPECIAL_RR");
+    return e && std::atoi(e) > 0;
+  }();
+  if (special_rr && a.n == 1 && a.sig_dispatch == 0) {
+    const int64_t groups = (a.nstrip[0] + a.nw - 1) / a.nw, nbnd = groups < 2 ? groups : 2;
+    a.sig_dispatch = groups * ((sp.e0[0] > 0) + (sp.e1[0] > 0)) + nbnd * sp.nmid_b[0];
+  }
   a.prio = nb <= per_cu ? 1 : 0;
   a.sig_count = o.signal_count;
   a.signal = o.signal;
@@ -1248,7 +1261,8 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     std::vector<uint64_t> h(static_cast<size_t>(nb) * 4);
     if (hipStreamSynchronize(s) == hipSuccess &&
         hipMemcpy(h.data(), trace_buf, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-      if (FILE* f = std::fopen(trace_file, "w")) {
+      const std::string path = std::string(trace_file) + (PUSH ? ".push" : "");
+      if (FILE* f = std::fopen(path.c_str(), "w")) {
         std::fprintf(f, "# K %d nb %lld per_cu %lld nw %d n %d mask %d rect0 %lld %lld %lld %lld nstrip %lld "
                         "e0 %lld e1 %lld nmid %lld lmid %lld nmid_b %lld lmid_b %lld sig_dispatch %lld\n",
                      K, (long long)nb, (long long)per_cu, a.nw, a.n, a.mask, (long long)a.r[0][0], (long long)a.r[0][1],
