@@ -651,14 +651,21 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
     m = rbs + l3 / (ngroups - 2);
     gi = 1 + l3 % (ngroups - 2);
   }
-  const int64_t lmid = (gi == 0 || gi == ngroups - 1) ? a.lmid_b[k] : a.lmid[k];
+  // interior segment m of nm: rows [mid m / nm, mid (m + 1) / nm) of the
+  // interior part — lengths differ by one row at most.  (Round 4 cut
+  // ceil(mid / nm)-row segments and left the rest to the last one: 64
+  // segments of 64 rows over 4036 left 4 rows for the last, a row band
+  // shorter than the rows it signals, and a band-first pass that never
+  // signalled: build/bench/plan_model --check-bands.)
+  const int64_t nm = (gi == 0 || gi == ngroups - 1) ? a.nmid_b[k] : a.nmid[k];
   int64_t ys, ye;
   if (m < 0) {
     ys = edge == 0 ? ry0 : ry1 - e1;
     ye = edge == 0 ? ry0 + e0 : ry1;
   } else {
-    ys = ry0 + e0 + m * lmid;
-    ye = ys + lmid < ry1 - e1 ? ys + lmid : ry1 - e1;
+    const int64_t mid = ry1 - e1 - (ry0 + e0);
+    ys = ry0 + e0 + m * mid / nm;
+    ye = ry0 + e0 + (m + 1) * mid / nm;
   }
   // L + 2K steps (the output stage of a split strip runs LAG steps behind)
   constexpr int kU = C::U;
@@ -1201,8 +1208,10 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     // the band segments exist separately: halo row sides have no edge
     // segments, and the planner kept >= rbs + rbn interior segments of >= rb_min rows
     const int rb = rbs + rbn;
+    // (the shortest segment: floor(mid / n) rows, tb_block's even split)
+    const int64_t mid = a.r[rbk][3] - sp.e0[rbk] - sp.e1[rbk];
     if ((rbs && sp.e0[rbk] > 0) || (rbn && sp.e1[rbk] > 0) || sp.nmid[rbk] < rb || sp.nmid_b[rbk] < rb ||
-        (sp.nmid[rbk] > 1 && sp.lmid[rbk] < o.signal_rows) || (sp.nmid_b[rbk] > 1 && sp.lmid_b[rbk] < o.signal_rows))
+        mid / sp.nmid[rbk] < o.signal_rows || mid / sp.nmid_b[rbk] < o.signal_rows)
       return static_cast<int>(hipErrorInvalidValue);
     a.rb_rect = rbk;
     a.rb_s = rbs;

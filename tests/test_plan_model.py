@@ -1,0 +1,34 @@
+"""The temporal-blocking kernel's segment planner, on the host (CPU-only).
+
+``build/bench/plan_model --check-bands`` plans band-first passes (row bands of
+20 rows on the halo row sides, csrc/engine/jacobi.cpp band_rects) for every
+built sweep count over a sweep of shares, halo masks and resident-slot counts,
+and checks that every row-band segment holds at least the rows it signals:
+a shorter band's output wave never counts its arrival and the pass never
+signals (the round-5 hang of bench.py --overlap on at 2 ranks: 64 segments of
+64 rows over 4036 left 4 rows for the last one).  The kernel now splits an
+interior into segments whose lengths differ by one row at most
+(csrc/kernels/jacobi5tb.hpp tb_block)."""
+import os
+import subprocess
+
+from native_util import ROOT
+
+TOOL = os.path.join(ROOT, "build", "bench", "plan_model")
+
+
+def _tool():
+    subprocess.run(["make", "-C", ROOT, "build/bench/plan_model"], check=True, stdout=subprocess.DEVNULL)
+    return TOOL
+
+
+def test_band_segments_hold_their_signalled_rows():
+    p = subprocess.run([_tool(), "--check-bands"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:]
+    assert "band plans: 0 violations" in p.stdout
+
+
+def test_headline_plans_print():
+    p = subprocess.run([_tool()], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "32768 x  32768 mask  0" in p.stdout and "workgroups on 1024 slots" in p.stdout
