@@ -1035,7 +1035,13 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
   int64_t best_l = 128;
   bool best_long = false;
   double best = 1e300;
+  // A/B: GMT_TB_EDGES=1 plans short edge segments only, 2 balanced ones only
+  static const int edges_mode = [] {
+    const char* e = std::getenv("GMT_TB_EDGES");
+    return e ? std::atoi(e) : 0;
+  }();
   for (int le = 0; le < 2; ++le) {
+    if ((edges_mode == 1 && le == 1) || (edges_mode == 2 && le == 0)) continue;
     int64_t c0 = 128;
     double b0 = 1e300;
     for (int64_t L = 128; L <= lhi; L += 16) {
