@@ -85,6 +85,22 @@ int sweep_bands(bool verbose) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  if (argc > 1 && std::strcmp(argv[1], "--check-swizzle") == 0) {
+    // tail_swizzle is a permutation of the tiles wherever tail_swizzle_ok holds
+    int bad = 0, checked = 0;
+    for (int64_t nb = 2; nb < 4000; nb += (nb < 200 ? 1 : 37))
+      for (int64_t ne = 1; ne < nb; ne += (ne < 40 ? 1 : 13)) {
+        if (!tail_swizzle_ok(nb, ne)) continue;
+        std::vector<char> seen(nb, 0);
+        for (int64_t b = 0; b < nb; ++b) {
+          const int64_t t = tail_swizzle(b, nb, ne);
+          if (t < 0 || t >= nb || seen[t]++) { ++bad; break; }
+        }
+        ++checked;
+      }
+    std::printf("tail_swizzle: %d of %d launch shapes not a permutation\n", bad, checked);
+    return bad ? 1 : 0;
+  }
   if (argc > 1 && std::strcmp(argv[1], "--check-bands") == 0) {
     const bool v = argc > 2;
     int bad = 0;

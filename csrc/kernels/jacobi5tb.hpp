@@ -105,6 +105,11 @@ struct Args {
   int rb_rect;                   // -1: none
   int rb_s, rb_n;                // the rect's first / last segments are row bands
   int64_t sig_rows, sig_total, sig_dispatch;
+  // edges_last > 0 (one-rect pass without signals): the first edges_last
+  // tiles (the edge segments) are dispatched last on every XCD, round-robin
+  // over the XCDs, after each XCD's contiguous range of the other tiles
+  // (tail_swizzle); 0: every tile XCD-contiguous in tile order
+  int64_t edges_last;
   // column bands (gmt_tb_opts.signal_cols): rect cb_rect's first (cb_lo)
   // and last (cb_hi) strip groups — every segment at full length — are
   // dispatched before everything else of the rect, and each of their
@@ -753,6 +758,34 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   }
 }
 
+// Tile of block b for a launch of nb blocks whose first ne tiles (the edge
+// segments) go last: the hardware hands block b to XCD b % 8 as that XCD's
+// (b / 8)-th block; XCD x runs its contiguous share of the nb - ne other
+// tiles (in tile order, as xcd_swizzle), then its share of the edge tiles.
+// Returns -1 when some XCD's block count cannot hold its share (a caller
+// falls back to xcd_swizzle; tail_swizzle_ok checks it on the host).
+__host__ __device__ inline int64_t tail_swizzle(int64_t b, int64_t nb, int64_t ne) {
+  const int64_t nm = nb - ne;
+  const int64_t x = b % kNumXcd, k = b / kNumXcd;
+  const int64_t nx = nb / kNumXcd + (x < nb % kNumXcd ? 1 : 0);        // blocks of XCD x
+  const int64_t qm = nm / kNumXcd, rm = nm % kNumXcd;
+  const int64_t ms = qm + (x < rm ? 1 : 0);                             // its other tiles
+  const int64_t mstart = x * qm + (x < rm ? x : rm);
+  if (k < ms) return ne + mstart + k;
+  // edge tiles: XCD x holds nx - ms of them, after the edge tiles of XCDs < x
+  int64_t estart = 0;
+  for (int64_t y = 0; y < x; ++y)
+    estart += nb / kNumXcd + (y < nb % kNumXcd ? 1 : 0) - (qm + (y < rm ? 1 : 0));
+  return estart + (k - ms);
+}
+inline bool tail_swizzle_ok(int64_t nb, int64_t ne) {
+  if (ne <= 0 || ne >= nb) return false;
+  const int64_t nm = nb - ne;
+  for (int64_t x = 0; x < kNumXcd; ++x)
+    if (nb / kNumXcd + (x < nb % kNumXcd ? 1 : 0) < nm / kNumXcd + (x < nm % kNumXcd ? 1 : 0)) return false;
+  return true;
+}
+
 template <int K, bool EXACT, bool EDGE, bool PUSH>
 __global__ __launch_bounds__(kMaxThreads) __attribute__((amdgpu_waves_per_eu(2)))
 void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__ un, int64_t nblocks) {
@@ -760,7 +793,8 @@ void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__
   const int64_t b = blockIdx.x;
   // signalling workgroups (and row bands) first, in dispatch order over all
   // XCDs; the rest XCD-contiguous
-  const int64_t t = b < nd ? b : nd + xcd_swizzle(b - nd, nblocks - nd);
+  const int64_t t = a.edges_last > 0 ? tail_swizzle(b, nblocks, a.edges_last)
+                    : b < nd ? b : nd + xcd_swizzle(b - nd, nblocks - nd);
 #if GMT_TB_WG_TRACE
   const uint64_t wg_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -970,6 +1004,10 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
   auto steps = [&](int64_t rows) { return static_cast<double>((rows + 2 * K + Cfg<K>::LAG + u - 1) / u * u); };
   std::vector<double> dur;
   std::vector<double> slot;
+  static const bool tail_edges = [] {
+    const char* e = std::getenv("GMT_TB_EDGES_LAST");
+    return e && std::atoi(e) > 0;
+  }();
   auto makespan = [&]() {
     dur.clear();
     for (int k = 0; k < a.n; ++k) {
@@ -984,15 +1022,19 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
       const bool edges = p.e0[k] > 0 || p.e1[k] > 0;
       const double fy = edges ? 1.0 : std::max(sc[2], sc[3]);
       const double fb = std::max(fx, fy), fm = fy;
-      for (int64_t g = 0; g < groups; ++g) {
-        const bool bnd = g == 0 || g == groups - 1;
-        if (p.e0[k] > 0) dur.push_back((bnd ? std::max(sc[2], fx) : sc[2]) * steps(p.e0[k]));
-        if (p.e1[k] > 0) dur.push_back((bnd ? std::max(sc[3], fx) : sc[3]) * steps(p.e1[k]));
-      }
+      auto edge_tiles = [&]() {
+        for (int64_t g = 0; g < groups; ++g) {
+          const bool bnd = g == 0 || g == groups - 1;
+          if (p.e0[k] > 0) dur.push_back((bnd ? std::max(sc[2], fx) : sc[2]) * steps(p.e0[k]));
+          if (p.e1[k] > 0) dur.push_back((bnd ? std::max(sc[3], fx) : sc[3]) * steps(p.e1[k]));
+        }
+      };
+      if (!tail_edges) edge_tiles();
       for (int64_t g = 0; g < nbnd; ++g)
         for (int64_t m = 0; m < p.nmid_b[k]; ++m) dur.push_back(fb * steps(p.lmid_b[k]));
       for (int64_t g = nbnd; g < groups; ++g)
         for (int64_t m = 0; m < p.nmid[k]; ++m) dur.push_back(fm * steps(p.lmid[k]));
+      if (tail_edges) edge_tiles();  // launch_tb's edges_last order (one-rect passes)
     }
     // list scheduling on the resident slots (a min-heap of free times)
     const size_t ns = static_cast<size_t>(std::max<int64_t>(1, resident_wgs));
@@ -1239,6 +1281,17 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     const char* e = std::getenv("GMT_TB_SPECIAL_RR");
     return e && std::atoi(e) > 0;
   }();
+  // GMT_TB_EDGES_LAST=1 (A/B): the edge segments of a one-rect pass without
+  // signals go last on every XCD (tail_swizzle), filling the launch's tail
+  static const bool edges_last = [] {
+    const char* e = std::getenv("GMT_TB_EDGES_LAST");
+    return e && std::atoi(e) > 0;
+  }();
+  if (edges_last && a.n == 1 && a.sig_dispatch == 0) {
+    const int64_t groups = (a.nstrip[0] + a.nw - 1) / a.nw;
+    const int64_t ne = groups * ((sp.e0[0] > 0) + (sp.e1[0] > 0));
+    if (tail_swizzle_ok(nb, ne)) a.edges_last = ne;
+  }
   if (special_rr && a.n == 1 && a.sig_dispatch == 0) {
     const int64_t groups = (a.nstrip[0] + a.nw - 1) / a.nw, nbnd = groups < 2 ? groups : 2;
     a.sig_dispatch = groups * ((sp.e0[0] > 0) + (sp.e1[0] > 0)) + nbnd * sp.nmid_b[0];

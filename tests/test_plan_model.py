@@ -32,3 +32,12 @@ def test_headline_plans_print():
     p = subprocess.run([_tool()], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "32768 x  32768 mask  0" in p.stdout and "workgroups on 1024 slots" in p.stdout
+
+
+def test_tail_swizzle_is_a_permutation():
+    """GMT_TB_EDGES_LAST's block -> tile map (csrc/kernels/jacobi5tb.hpp
+    tail_swizzle): every tile exactly once, on every launch shape the
+    launcher accepts it for."""
+    p = subprocess.run([_tool(), "--check-swizzle"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:]
+    assert " 0 of " in p.stdout
