@@ -146,10 +146,10 @@ int main(int argc, char** argv) {
     const int64_t g = a.nstrip[0], nb = g < 2 ? g : 2;
     const int64_t wgs = g * ((p.e0[0] > 0) + (p.e1[0] > 0)) + nb * p.nmid_b[0] + (g - nb) * p.nmid[0];
     std::printf("%6lld x %6lld mask %2d: edges %lld / %lld rows, interior %lld x %lld rows, rule groups %lld x %lld rows, "
-                "%lld workgroups on %lld slots\n",
+                "%lld workgroups on %lld slots%s\n",
                 (long long)c.ny, (long long)c.nx, c.mask, (long long)p.e0[0], (long long)p.e1[0], (long long)p.nmid[0],
                 (long long)p.lmid[0], (long long)p.nmid_b[0], (long long)p.lmid_b[0], (long long)wgs,
-                (long long)c.resident);
+                (long long)c.resident, p.tail ? ", edges last" : "");
   }
   return 0;
 }

@@ -845,6 +845,7 @@ using namespace gmt::tb;
 // workgroups), over L in [128, 2048].
 struct SegPlan {
   int64_t e0[kMaxRect], e1[kMaxRect], nmid[kMaxRect], lmid[kMaxRect], nmid_b[kMaxRect], lmid_b[kMaxRect];
+  bool tail;  // dispatch the edge segments last on every XCD (launch_tb: Args::edges_last)
 };
 
 // Signalling rects (k < sig_rects: the boundary bands of a pass whose halo
@@ -1004,10 +1005,17 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
   auto steps = [&](int64_t rows) { return static_cast<double>((rows + 2 * K + Cfg<K>::LAG + u - 1) / u * u); };
   std::vector<double> dur;
   std::vector<double> slot;
-  static const bool tail_edges = [] {
+  // The edges-last order (tail_swizzle): one-rect passes without signals
+  // whose other tiles fill at least two rounds — short edge tiles then fill
+  // the last round's tail (32768^2: +1.2%); a one-round launch gets a second
+  // round of edges only and ran 4% slower (profiles/r05_wg_timeline/).
+  // GMT_TB_EDGES_LAST=0 / 1 forbids / forces it (A/B).
+  static const int tail_mode = [] {
     const char* e = std::getenv("GMT_TB_EDGES_LAST");
-    return e && std::atoi(e) > 0;
+    return e ? std::atoi(e) : -1;
   }();
+  const bool tail_possible = a.n == 1 && sig_rects == 0 && rb_rect < 0 && seg_rows == 0 && tail_mode != 0;
+  bool tail_edges = false;
   auto makespan = [&]() {
     dur.clear();
     for (int k = 0; k < a.n; ++k) {
@@ -1063,19 +1071,34 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
   auto eval = [&](int le, int64_t L) {
     long_edges = le == 1;
     fill(L, &wgs);
-    const double cost = makespan();
+    const int64_t groups0 = (a.nstrip[0] + a.nw - 1) / a.nw;
+    const int64_t ne = groups0 * ((p.e0[0] > 0) + (p.e1[0] > 0));
+    const bool can_tail = tail_possible && ne > 0 && wgs - ne >= 2 * resident_wgs;
+    tail_edges = false;
+    double cost = makespan();
+    bool tail = false;
+    if (can_tail && tail_mode == 1) cost = 1e300;  // forced: only the tail order
+    if (can_tail) {
+      tail_edges = true;
+      const double ct = makespan();
+      if (ct < cost - 1e-9) {
+        cost = ct;
+        tail = true;
+      }
+    }
     if (debug)
-      std::fprintf(stderr, "plan le %d L %lld e %lld/%lld mid %lld x %lld b %lld x %lld wgs %lld cost %.1f\n", le,
-                   (long long)L, (long long)p.e0[0], (long long)p.e1[0], (long long)p.nmid[0], (long long)p.lmid[0],
-                   (long long)p.nmid_b[0], (long long)p.lmid_b[0], (long long)wgs, cost);
-    return cost;
+      std::fprintf(stderr, "plan le %d L %lld e %lld/%lld mid %lld x %lld b %lld x %lld wgs %lld tail %d cost %.1f\n",
+                   le, (long long)L, (long long)p.e0[0], (long long)p.e1[0], (long long)p.nmid[0],
+                   (long long)p.lmid[0], (long long)p.nmid_b[0], (long long)p.lmid_b[0], (long long)wgs, tail ? 1 : 0,
+                   cost);
+    return std::make_pair(cost, tail);
   };
   // coarse (16 rows), then every length within 16 rows of each edge mode's
   // coarse best (segment counts are integers: a plan one segment shorter
   // can tip a launch into or out of one round)
   const int64_t lhi = std::min<int64_t>(2048, lmax);
   int64_t best_l = 128;
-  bool best_long = false;
+  bool best_long = false, best_tail = false;
   double best = 1e300;
   // A/B: GMT_TB_EDGES=1 plans short edge segments only, 2 balanced ones only
   static const int edges_mode = [] {
@@ -1087,23 +1110,25 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
     int64_t c0 = 128;
     double b0 = 1e300;
     for (int64_t L = 128; L <= lhi; L += 16) {
-      const double cost = eval(le, L);
+      const double cost = eval(le, L).first;
       if (cost < b0 - 1e-9) {
         b0 = cost;
         c0 = L;
       }
     }
     for (int64_t L = std::max<int64_t>(128, c0 - 15); L <= std::min(lhi, c0 + 15); ++L) {
-      const double cost = eval(le, L);
+      const auto [cost, tail] = eval(le, L);
       if (cost < best - 1e-9) {
         best = cost;
         best_l = L;
         best_long = le == 1;
+        best_tail = tail;
       }
     }
   }
   long_edges = best_long;
   fill(std::min<int64_t>(best_l, lmax), &wgs);
+  p.tail = best_tail;
   return p;
 }
 
@@ -1281,13 +1306,9 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     const char* e = std::getenv("GMT_TB_SPECIAL_RR");
     return e && std::atoi(e) > 0;
   }();
-  // GMT_TB_EDGES_LAST=1 (A/B): the edge segments of a one-rect pass without
-  // signals go last on every XCD (tail_swizzle), filling the launch's tail
-  static const bool edges_last = [] {
-    const char* e = std::getenv("GMT_TB_EDGES_LAST");
-    return e && std::atoi(e) > 0;
-  }();
-  if (edges_last && a.n == 1 && a.sig_dispatch == 0) {
+  // the planner's order: the edge segments of a one-rect pass without
+  // signals last on every XCD (tail_swizzle), filling the launch's tail
+  if (sp.tail && a.n == 1 && a.sig_dispatch == 0) {
     const int64_t groups = (a.nstrip[0] + a.nw - 1) / a.nw;
     const int64_t ne = groups * ((sp.e0[0] > 0) + (sp.e1[0] > 0));
     if (tail_swizzle_ok(nb, ne)) a.edges_last = ne;
