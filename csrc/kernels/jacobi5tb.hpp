@@ -876,12 +876,15 @@ inline double tb_rule_cost() {
 // The step cost of a wave running the inline-halo body (three face store
 // groups per step, the ones out of range dropped) relative to a plain one:
 // a one-round pass whose push waves had plain-length segments ran
-// 1.11-1.14x (profiles/r05_overlap/).  GMT_TB_PUSH_COST=c overrides it.
+// 1.11-1.14x, per-workgroup timelines put push tiles at 1.17x per step, and
+// planning at 1.3 ran the application fastest on both N = 8 shares
+// (profiles/r05_overlap/app_push_cost_sweep.txt).  GMT_TB_PUSH_COST=c
+// overrides it.
 inline double tb_push_cost() {
   static const double c = [] {
     const char* e = std::getenv("GMT_TB_PUSH_COST");
     const double v = e ? std::atof(e) : 0.0;
-    return v >= 1.0 && v <= 4.0 ? v : 1.15;
+    return v >= 1.0 && v <= 4.0 ? v : 1.3;
   }();
   return c;
 }
