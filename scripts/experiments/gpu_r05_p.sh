@@ -6,7 +6,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 export TMPDIR=/tmp
 R=$PWD
-OUT=$R/gpurun_out/r05_p
+OUT=$R/${OUT:-gpurun_out/r05_p}
 mkdir -p $OUT
 for rep in 1 2 3; do
   timeout -k 10 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
