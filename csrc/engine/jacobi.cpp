@@ -665,6 +665,12 @@ std::vector<int> JacobiSolver::plan_passes(int k) const {
   // the job's largest share — the same costs, hence the same plan, on every rank
   std::vector<double> cost(ks_ + 1, 0.0);
   for (int K = 1; K <= ks_; ++K) cost[K] = calibrated_ ? meas_ms_[K] : table_pass_ms(K);
+  // measured costs carry ~1-2% of clock noise: a pass shorter than ks_ must
+  // win by more than that to displace full passes (a 1000-sweep 8192^2 plan
+  // flipped between 50x20 and 5x20+50x18, the latter 1.5% slower:
+  // profiles/r05_final/bench_2.json)
+  if (calibrated_)
+    for (int K = 2; K < ks_; ++K) cost[K] *= 1.02;
   std::vector<double> best(k + 1, 1e300);
   std::vector<int> pick(k + 1, 0);
   best[0] = 0.0;
