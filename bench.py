@@ -134,6 +134,40 @@ def bench_native(env, shape, steps, warmup, overlap, dims, graph, tblock, wg_wav
     return eng, dt, info
 
 
+def timed_check(env, eng, sweeps, init, seed, prefix="timed_check"):
+    """The check of the timed run itself, on the timed domain (reference: the
+    timed field's err_norm, mpi_stencil2d_gt.cc:541-570).  The same initial
+    field is advanced by the same sweeps (warm-up + timed) through an
+    independent path — single sweeps (csrc/kernels/jacobi5.hip) with one plain
+    blocking 1-wide halo exchange per sweep over RCCL (IPC when ranks share a
+    GPU, none at N = 1): no fused passes, no segment plan, no inline halo, no
+    overlap — and the two final interiors are compared bitwise on the device
+    (gmt_diff_bits; max |diff| and differing elements over ranks).  Must be
+    0 / 0: the fused passes are bitwise equal to single sweeps."""
+    from gpu_mpi_tests_amd.engine import NativeJacobi
+
+    t0 = time.perf_counter()
+    if env.world_size == 1:
+        t = "auto"
+    else:
+        t = "ipc" if env.is_gpu and env.ranks_per_device > 1 else "rccl"
+    ref = NativeJacobi(eng.ny_g, eng.nx_g, env, dims=(eng.py, eng.px), overlap=False, graph=False, tblock=False,
+                       init=init, seed=seed, transport=t)
+    try:
+        ref.run(sweeps)
+        ref.synchronize()
+        eng.synchronize()
+        mx, bad = eng.compare(ref)
+        kind = ref.transport
+    finally:
+        ref.close()
+    if env.is_gpu:
+        torch.cuda.empty_cache()
+    return {f"{prefix}_max_diff": mx, f"{prefix}_mismatches": bad,
+            f"{prefix}_path": f"{sweeps} single sweeps + blocking 1-wide exchange ({kind}), bitwise on the device",
+            f"{prefix}_s": round(time.perf_counter() - t0, 3)}
+
+
 def check_engine(env, dims, tsteps, graph, init="analytic", seed=0, transport="auto"):
     """Distributed-correctness gate (reference: mpi_stencil2d_gt.cc:555-570
     err_norm): the engine with this job's process grid and sweeps per pass on
@@ -353,28 +387,38 @@ def probe_kinds(args):
     return list(PROBE_KINDS) if 0 < ndev and lw <= ndev else []
 
 
+def probe_order(kinds):
+    """Interleaved rep order of the probe's candidates: A B C C B A.  The
+    clock drifts over a sustained run (the first of a pair reads high,
+    profiles/r05_overlap/README.md), so every candidate is timed once early
+    and once late, and keeps its better rep."""
+    return [(k, 0) for k in kinds] + [(k, 1) for k in reversed(kinds)]
+
+
 def run_probe(args, argv, kinds):
     """Time every candidate data plane in a CHILD process group of its own
     (this process has not initialised the GPU yet): a candidate that faults,
     hangs or fails the bitwise gate takes only its child down and is
-    dropped, never the job nor the other candidates.  Each candidate's
-    children rendezvous on their own port and are killed as a process group
-    at --probe-timeout.  Returns this rank's candidates (each with its
-    child's exit status) and the probe's wall time."""
+    dropped, never the job nor the other candidates.  Each candidate runs
+    twice, in the interleaved order of probe_order; each child rendezvouses
+    on its own port and is killed as a process group at --probe-timeout.
+    Returns this rank's candidates ({kind: {"reps": [rec, rec]}}, each rec
+    with its child's exit status) and the probe's wall time."""
     import signal
     import subprocess
     import tempfile
 
     rank = int(os.environ.get("RANK", "0") or 0)
     port = int(os.environ.get("MASTER_PORT", "29500") or 29500)
-    base = args.probe_port or (port + 101 if port + 101 + len(kinds) < 65536 else port - 101 - len(kinds))
-    res = {}
+    order = probe_order(kinds)
+    base = args.probe_port or (port + 101 if port + 101 + len(order) < 65536 else port - 101 - len(order))
+    res = {k: {"reps": [None, None]} for k in kinds}
     t0 = time.perf_counter()
-    for i, kind in enumerate(kinds):
+    for i, (kind, rep) in enumerate(order):
         cenv = dict(os.environ, MASTER_PORT=str(base + i), GMT_TIMEOUT=str(min(60.0, args.probe_timeout)))
         # torchrun's agent hosts the store on MASTER_PORT only: the children host their own
         cenv.pop("TORCHELASTIC_USE_AGENT_STORE", None)
-        fd, path = tempfile.mkstemp(prefix=f"gmt_probe_r{rank}_{kind}_", suffix=".json")
+        fd, path = tempfile.mkstemp(prefix=f"gmt_probe_r{rank}_{kind}{rep}_", suffix=".json")
         os.close(fd)
         cmd = [sys.executable, os.path.abspath(__file__), *argv, "--probe-child", path, "--probe-kinds", kind]
         t1 = time.perf_counter()
@@ -396,7 +440,7 @@ def run_probe(args, argv, kinds):
             os.unlink(path)
         rec["_rc"] = rc
         rec["_s"] = round(time.perf_counter() - t1, 2)
-        res[kind] = rec
+        res[kind]["reps"][rep] = rec
     res["_s"] = round(time.perf_counter() - t0, 2)
     return res
 
@@ -459,15 +503,33 @@ def probe_child(args, dims, shape, tsteps, graph):
     gdist.shutdown()
 
 
+SIMPLICITY = ("rccl", "ipc", "push")  # a tie keeps the earlier (simpler) data plane
+
+
+def choose_plane(pass_ms, margin=0.97):
+    """{kind: pass ms} of the candidates that passed -> the job's plane.
+    Candidates are visited from the simplest (RCCL: the library's own
+    collectives, no mappings) to the most involved (push: the pass stores
+    into peer memory); a more involved one replaces the current choice only
+    when its passes are faster by more than 1 - margin (3%) — the run-to-run
+    spread of a probe rep — so a tie keeps the simpler plane."""
+    choice = None
+    for t in sorted(pass_ms, key=lambda k: SIMPLICITY.index(k) if k in SIMPLICITY else len(SIMPLICITY)):
+        if choice is None or pass_ms[t] < margin * pass_ms[choice]:
+            choice = t
+    return choice or "auto"
+
+
 def agree_transport(env, probe, kinds, margin=0.97):
     """Every rank's probe -> one choice for all: a candidate counts if it
-    passed the gate and timed on EVERY rank; its pass time is the max over
-    ranks; another plane replaces RCCL only when its passes are faster by
-    more than 3%.  Every
-    rank calls this (world > 1), probed or not, so ranks whose environments
-    disagree on probing (device counts, LOCAL_WORLD_SIZE) cannot leave one
-    side waiting in the collective: only kinds that every rank probed count.
-    Returns (transport, {kind: record} or None, probe wall seconds)."""
+    passed the gate and timed on EVERY rank in BOTH of its reps; a rep's pass
+    time is the max over ranks, the candidate's the better of its two reps
+    (``pass_ms_reps`` records both); the plane is then choose_plane's.
+    Every rank calls this (world > 1), probed or not, so ranks whose
+    environments disagree on probing (device counts, LOCAL_WORLD_SIZE)
+    cannot leave one side waiting in the collective: only kinds that every
+    rank probed count.  Returns (transport, {kind: record} or None, probe
+    wall seconds)."""
     allp = [None] * env.world_size
     torch.distributed.all_gather_object(allp, {"kinds": list(kinds), "probe": probe or {}}, group=env.host_group)
     common = [t for t in kinds if all(t in (p["kinds"] or []) for p in allp)]
@@ -479,32 +541,33 @@ def agree_transport(env, probe, kinds, margin=0.97):
     if len(allp_kinds) > 1:
         cands["_mismatch"] = {"gate": "fail", "error": f"ranks probed different kinds: {sorted(allp_kinds)}"}
     for t in common:
-        recs = [(p.get(t) or {}) for p in allp]
-        ok = all(r.get("gate_max_diff") == 0.0 and r.get("pass_ms") for r in recs)
+        # per rank, per rep
+        reps = [[r or {} for r in ((p.get(t) or {}).get("reps") or [None, None])] for p in allp]
+        ok = all(r.get("gate_max_diff") == 0.0 and r.get("pass_ms") for rr in reps for r in rr)
         c = {"gate": "pass" if ok else "fail"}
         if ok:
-            c["pass_ms"] = max(r["pass_ms"] for r in recs)
-            if all(r.get("exchange_us") for r in recs):
-                c["exchange_us"] = max(r["exchange_us"] for r in recs)
-            c["label"] = recs[0].get("label", t)
+            c["pass_ms_reps"] = [max(rr[i]["pass_ms"] for rr in reps) for i in range(2)]
+            c["pass_ms"] = min(c["pass_ms_reps"])
+            if all(r.get("exchange_us") for rr in reps for r in rr):
+                c["exchange_us"] = min(max(rr[i]["exchange_us"] for rr in reps) for i in range(2))
+            c["label"] = reps[0][0].get("label", t)
         else:
             whys = []
-            for i, r in enumerate(recs):
-                why = [f"probe exit {r.get('_rc')}"] if r.get("_rc", 0) != 0 else []
-                if r.get("error"):
-                    why.append(r["error"])
-                elif r.get("gate_max_diff"):
-                    why.append(f"gate max diff {r['gate_max_diff']}")
+            for i, rr in enumerate(reps):
+                why = []
+                for j, r in enumerate(rr):
+                    if r.get("_rc", 0) != 0:
+                        why.append(f"rep {j + 1} probe exit {r.get('_rc')}")
+                    if r.get("error"):
+                        why.append(r["error"])
+                    elif r.get("gate_max_diff"):
+                        why.append(f"gate max diff {r['gate_max_diff']}")
                 if why:
                     whys.append(f"rank {i}: {', '.join(why)}")
             c["error"] = "; ".join(whys[:4])[:600]
         cands[t] = c
     passing = {t: c["pass_ms"] for t, c in cands.items() if c["gate"] == "pass" and not t.startswith("_")}
-    choice = "auto"
-    if passing:
-        choice = min(passing, key=passing.get)
-        if choice != "rccl" and "rccl" in passing and passing[choice] > margin * passing["rccl"]:
-            choice = "rccl"
+    choice = choose_plane(passing, margin) if passing else "auto"
     return choice, cands, max(float(p.get("_s", 0.0)) for p in allp)
 
 
@@ -558,7 +621,7 @@ def _epitaph(env, rec):
     dev = "cuda" if env.is_gpu else "cpu"
 
     def update():
-        watchdog_epitaph(json.dumps(rec()) if env.rank == 0 else "", 0, dev)
+        watchdog_epitaph(json.dumps(rec()) if env.rank == 0 else "", EXTRA_HANG_EXIT, dev)
 
     return update
 
@@ -573,6 +636,25 @@ def _maybe_hang(env, phase):
         print(f"GMT FAULT INJECTION: rank {env.rank} hangs in bench phase '{phase}'", file=sys.stderr, flush=True)
         while True:
             time.sleep(3600)
+
+
+class TimedCheckFailed(RuntimeError):
+    pass
+
+
+def checked(extras, rec):
+    """Merges a timed_check record; a mismatch fails the job (after the line
+    is printed, bench.py exits TIMED_CHECK_EXIT)."""
+    extras.update(rec)
+    prefix = next(k for k in rec if k.endswith("_mismatches"))[:-len("_mismatches")]
+    if rec[f"{prefix}_mismatches"] != 0 or rec[f"{prefix}_max_diff"] != 0.0:
+        extras["timed_check_failed"] = sorted(set(extras.get("timed_check_failed", [])) | {prefix})
+        raise TimedCheckFailed(f"{prefix}: {rec[f'{prefix}_mismatches']} lattice points differ from the "
+                               f"single-sweep replay (max |diff| {rec[f'{prefix}_max_diff']})")
+
+
+TIMED_CHECK_EXIT = 6  # a timed field differs from its single-sweep replay
+EXTRA_HANG_EXIT = 5   # the headline stands, an extra hung (the watchdog printed the line)
 
 
 def run_extras(args, env, solver, info, shape, points, tsteps, overlap, dims, graph, transport, extras, epitaph):
@@ -622,7 +704,12 @@ def run_extras(args, env, solver, info, shape, points, tsteps, overlap, dims, gr
             eng3, dt3, info3 = bench_native(env, shape, args.steps, args.warmup, overlap, (hx, hp), graph,
                                             tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows,
                                             args.init, args.seed, not args.no_calibrate, transport)
-            eng3.close()
+            try:
+                if not args.no_timed_check:
+                    checked(extras, timed_check(env, eng3, args.warmup + args.steps, args.init, args.seed,
+                                                "stencil_alt_dims_check"))
+            finally:
+                eng3.close()
             extras["stencil_alt_dims"] = f"{hx}x{hp}"
             extras["stencil_alt_dims_MLUPS"] = round(points * args.steps / dt3 / 1e6, 1)
             extras["stencil_alt_dims_overlap"] = info3["overlap"]
@@ -637,10 +724,16 @@ def run_extras(args, env, solver, info, shape, points, tsteps, overlap, dims, gr
             # 3-4% low, mostly the host round trip and the clock ramp around
             # so short a timed region (profiles/r04_shares.md)
             steps2 = args.small_steps or max(1000 if env.is_gpu else 100, 4 * args.steps)
-            eng2, dt2, info2 = bench_native(env, s2, steps2, max(args.warmup, 10), overlap, dims, graph,
+            w2 = max(args.warmup, 10)
+            eng2, dt2, info2 = bench_native(env, s2, steps2, w2, overlap, dims, graph,
                                             tsteps if tsteps > 1 else False, args.wg_waves, args.seg_rows,
                                             args.init, args.seed, not args.no_calibrate, transport)
-            eng2.close()
+            try:
+                if not args.no_timed_check:
+                    checked(extras, timed_check(env, eng2, w2 + steps2, args.init, args.seed,
+                                                f"stencil_{args.small_size}_check"))
+            finally:
+                eng2.close()
             extras[f"stencil_{args.small_size}_MLUPS"] = round(s2[0] * s2[1] * steps2 / dt2 / 1e6, 1)
             extras[f"stencil_{args.small_size}_ms_per_step"] = round(dt2 / steps2 * 1e3, 5)
             extras[f"stencil_{args.small_size}_pass_plan"] = f"{steps2} steps: {info2['pass_plan']}"
@@ -713,6 +806,9 @@ def main(argv=None):
                     help="second stencil domain (BASELINE single-GPU config 8192^2; 0 = skip)")
     ap.add_argument("--skip-extras", action="store_true", help="headline stencil only")
     ap.add_argument("--skip-check", action="store_true", help="skip the small-domain correctness gate")
+    ap.add_argument("--no-timed-check", action="store_true",
+                    help="skip the check of the timed runs (their final fields against a single-sweep replay, "
+                         "bitwise on the device; a mismatch exits 6)")
     ap.add_argument("--ref-n-local", type=int, default=1024,
                     help="reference halo benchmark (N>1): n_local_deriv (mpi_stencil2d_gt default 1024)")
     ap.add_argument("--ref-n-other", type=int, default=512 * 1024,
@@ -732,7 +828,8 @@ def main(argv=None):
                          "bitwise gate; on: also on the CPU backend; off: RCCL")
     ap.add_argument("--probe-timeout", type=float, default=150.0, help="seconds for the transport probe")
     ap.add_argument("--probe-iters", type=int, default=50, help="timed exchanges per probed transport")
-    ap.add_argument("--probe-passes", type=int, default=6, help="timed fused passes per probed data plane")
+    ap.add_argument("--probe-passes", type=int, default=6,
+                    help="timed fused passes per probed data plane and rep (two reps, interleaved A B C C B A)")
     ap.add_argument("--probe-port", type=int, default=0, help="the probe's rendezvous port (0: MASTER_PORT+101)")
     ap.add_argument("--probe-child", type=str, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--probe-kinds", type=str, default="", help=argparse.SUPPRESS)
@@ -788,18 +885,35 @@ def main(argv=None):
     ms_per_step = dt / args.steps * 1e3
     py, px = info["dims"] if info.get("dims") else gdims
     extras["watchdog_timeout_s"] = watchdog_timeout("cuda" if env.is_gpu else "cpu")
+    if not args.no_timed_check:
+        # before any extra: the halo latency and residual extras advance the field
+        mark(env, "check of the timed run")
+        try:
+            checked(extras, timed_check(env, solver, args.warmup + args.steps, args.init, args.seed))
+        except TimedCheckFailed as ex:
+            extras["timed_check_error"] = str(ex)[:300]
     base = result_record(args, env, shape, mlups, ms_per_step, info, (py, px))
 
     def rec():
         return {**base, **extras}
 
-    # From here on the headline is measured: every later phase is an extra.
-    # An extra that raises becomes an "<extra>_error" field; one that hangs
-    # ends the job through the watchdog, which then prints this line (with
-    # the extras finished so far and a "watchdog" field) and exits 0 on
-    # every rank instead of 124 — the headline is never lost to an extra.
+    # From here on the headline is measured (and checked): every later phase
+    # is an extra.  An extra that raises becomes an "<extra>_error" field; one
+    # that hangs ends the job through the watchdog, which then prints this
+    # line (with the extras finished so far and a "watchdog" field) and exits
+    # EXTRA_HANG_EXIT (5) on every rank instead of 124 — the headline is never
+    # lost to an extra, and the hang stays visible in the exit status.
     epitaph = _epitaph(env, rec)
     epitaph()
+    if extras.get("timed_check_failed"):
+        solver.close()
+        if env.rank == 0:
+            print(json.dumps(rec()), flush=True)
+            print(f"bench.py: the timed field differs from its single-sweep replay: {extras['timed_check_error']}",
+                  file=sys.stderr, flush=True)
+        watchdog_epitaph("", TIMED_CHECK_EXIT, "cuda" if env.is_gpu else "cpu")
+        gdist.shutdown()
+        sys.exit(TIMED_CHECK_EXIT)
     if not args.skip_extras:
         run_extras(args, env, solver, info, shape, points, tsteps, overlap, dims, graph, transport, extras, epitaph)
     else:
@@ -813,6 +927,8 @@ def main(argv=None):
     if failed and env.rank == 0:
         print(f"bench.py: extras failed (the headline stands): {', '.join(failed)}", file=sys.stderr)
     gdist.shutdown()
+    if extras.get("timed_check_failed"):
+        sys.exit(TIMED_CHECK_EXIT)
 
 
 if __name__ == "__main__":

@@ -226,6 +226,12 @@ int gmt_engine_jacobi_copy_interior(void* p, double* host) {
   static_cast<Handle*>(p)->s->copy_interior(host);
   return 0;
 }
+int gmt_engine_jacobi_compare(void* a, void* b, double* out) {
+  if (!a || !b || !out) return 1;
+  gmt::watchdog_kick("engine: compare with the single-sweep replay");
+  static_cast<Handle*>(a)->s->compare(*static_cast<Handle*>(b)->s, out);
+  return 0;
+}
 double gmt_engine_jacobi_stat(void* p, int what) {
   const auto& s = *static_cast<Handle*>(p)->s;
   switch (what) {

@@ -130,6 +130,23 @@ int gmt_abs_max(int64_t nx, int64_t ny, const double* z, int64_t ld, double* out
   return 0;
 }
 
+int gmt_diff_bits(int64_t nx, int64_t ny, const double* a, int64_t lda, const double* b, int64_t ldb,
+                  double* out, double*, void*) {
+  double m = 0.0, n = 0.0;
+  for (int64_t y = 0; y < ny; ++y)
+    for (int64_t x = 0; x < nx; ++x) {
+      const double va = a[y * lda + x], vb = b[y * ldb + x];
+      if (std::memcmp(&va, &vb, sizeof(double)) != 0) {
+        n += 1.0;
+        const double d = std::fabs(va - vb);
+        m = std::max(m, std::isnan(d) ? HUGE_VAL : d);
+      }
+    }
+  out[0] = m;
+  out[1] = n;
+  return 0;
+}
+
 // fill mode 5: the same counter-based hash as reduce.hip lattice_uniform
 static double lattice_uniform(int64_t gx, int64_t gy, uint64_t seed) {
   uint64_t k = (static_cast<uint64_t>(gy + (int64_t(1) << 30)) << 32) ^ static_cast<uint64_t>(gx + (int64_t(1) << 30));

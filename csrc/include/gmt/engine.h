@@ -68,6 +68,10 @@ int gmt_engine_jacobi_copy_interior(void* h, double* host);
 /* what: 0 = max |u| of the initial field (all ranks; drives the exactness
  * guard), 1 = measured ms of a full tsteps pass (0 before a calibrated
  * prepare), 2 = the built-in cost table's ms for that pass on this share */
+/* bitwise comparison of the current interiors of two engines of the same
+ * problem and process grid (collective): out[0] = max |diff| over ranks,
+ * out[1] = elements whose bits differ, summed over ranks */
+int gmt_engine_jacobi_compare(void* a, void* b, double* out);
 double gmt_engine_jacobi_stat(void* h, int what);
 const char* gmt_engine_backend(void);
 

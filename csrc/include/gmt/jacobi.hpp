@@ -110,6 +110,13 @@ class JacobiSolver {
   bool exact() const { return exact_; }
   // local interior, row-major [ny][nx] (host memory)
   void copy_interior(double* host) const;
+  // Bitwise comparison of the current interiors of two solvers of the same
+  // global problem and process grid, on the device (gmt_diff_bits):
+  // out[0] = max |diff| (max over ranks), out[1] = elements whose bits differ
+  // (sum over ranks).  bench.py's check of the timed run replays the timed
+  // sweeps through single sweeps and compares (reference: the err_norm of the
+  // timed field, mpi_stencil2d_gt.cc:541-570).  Collective.
+  void compare(JacobiSolver& o, double out[2]);
 
   int64_t nx() const { return nx_; }
   int64_t ny() const { return ny_; }
@@ -157,6 +164,7 @@ class JacobiSolver {
   int halo_mask() const;
   void split_cus();
   void setup_push();
+  void maybe_corrupt(int parity);  // GMT_CORRUPT_PASS fault injection
   void push_block(int parity, int k);  // one inline-halo pass + its hand-over
 
   comm::Transport& t_;
@@ -191,6 +199,8 @@ class JacobiSolver {
   gmt_graph_t graph_[2] = {nullptr, nullptr};   // single sweep, per parity
   gmt_graph_t graph2_[2] = {nullptr, nullptr};  // fused ks_-sweep block, per parity
   int parity_ = 0;  // buf_[parity_] holds the current u
+  int passes_ = 0;  // fused passes run() enqueued since the field was (re)initialised
+  bool in_run_ = false;
   double tune_s_[2] = {0.0, 0.0};
   double meas_ms_[GMT_TB_MAX_SWEEPS + 1] = {};
   bool calibrated_ = false;

@@ -93,6 +93,15 @@ int gmt_slices_reduce(int op, int64_t n, int nslices, const double* in, double* 
 int gmt_abs_max(int64_t nx, int64_t ny, const double* z, int64_t ld, double* out, double* workspace,
                 void* stream);
 
+/* ---- bitwise comparison of two nx x ny regions: out[0] = max |a - b|
+ *      (NaN -> +inf), out[1] = number of elements whose 64 bits differ (as a
+ *      double: exact to 2^53).  Deterministic two-pass; workspace of
+ *      2 * gmt_diff_sq_workspace(nx, ny) doubles.  bench.py's check of the
+ *      timed run (reference: the err_norm of the timed field,
+ *      mpi_stencil2d_gt.cc:541-570) */
+int gmt_diff_bits(int64_t nx, int64_t ny, const double* a, int64_t lda, const double* b, int64_t ldb,
+                  double* out, double* workspace, void* stream);
+
 /* ---- analytic fill z[y][x] = (x0+i*dx)^3 + (y0+j*dy)^2 over nx x ny (device
  *      side replacement of the reference's host init loops,
  *      mpi_stencil2d_gt.cc:439-497).  mode 0: x^3+y^2 (z), 1: 3x^2 (dz/dx),

@@ -222,6 +222,34 @@ __global__ __launch_bounds__(kBlock) void max_all(const double* __restrict__ ws,
   if (threadIdx.x == 0) out[0] = m;
 }
 
+// ---------------- bitwise comparison (gmt_diff_bits): per tile the max
+// |a - b| (NaN -> +inf) and the count of elements whose bits differ
+__global__ __launch_bounds__(kBlock) void diffbits_pass1(int64_t nx, int64_t ny, const double* __restrict__ a,
+                                                         int64_t lda, const double* __restrict__ b, int64_t ldb,
+                                                         double* __restrict__ ws, int64_t nch) {
+  const int64_t blk = blockIdx.x, nblk = nch * ny;
+  const int64_t c = blk % nch, y = blk / nch;
+  const int64_t x0 = c * kDiffTile;
+  const int64_t x1 = (x0 + kDiffTile) < nx ? (x0 + kDiffTile) : nx;
+  const double* pa = a + y * lda;
+  const double* pb = b + y * ldb;
+  double m = 0.0, n = 0.0;
+  for (int64_t x = x0 + threadIdx.x; x < x1; x += kBlock) {
+    const double va = pa[x], vb = pb[x];
+    if (__double_as_longlong(va) != __double_as_longlong(vb)) {
+      n += 1.0;
+      const double d = fabs(va - vb);
+      m = fmax(m, d != d ? __builtin_inf() : d);
+    }
+  }
+  m = block_max(m);
+  n = block_sum(n);
+  if (threadIdx.x == 0) {
+    ws[blk] = m;
+    ws[nblk + blk] = n;
+  }
+}
+
 // counter-based uniform [0, 1) of an integer lattice point (fill mode 5):
 // splitmix64 of the packed global coordinates — the same value whatever the
 // decomposition, and reproducible on the host (ops/reference.py)
@@ -394,6 +422,19 @@ extern "C" int gmt_abs_max(int64_t nx, int64_t ny, const double* z, int64_t ld, 
   GMT_RET_LAUNCH();
 }
 
+extern "C" int gmt_diff_bits(int64_t nx, int64_t ny, const double* a, int64_t lda, const double* b, int64_t ldb,
+                             double* out, double* ws, void* stream) {
+  using namespace gmt;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (nx <= 0 || ny <= 0) return static_cast<int>(hipMemsetAsync(out, 0, 2 * sizeof(double), s));
+  if (!a || !b || !out || !ws || lda < nx || ldb < nx) return static_cast<int>(hipErrorInvalidValue);
+  const int64_t nch = (nx + kDiffTile - 1) / kDiffTile;
+  diffbits_pass1<<<grid_1d(nch * ny), kBlock, 0, s>>>(nx, ny, a, lda, b, ldb, ws, nch);
+  max_all<<<1, kBlock, 0, s>>>(ws, nch * ny, out);
+  sum_all<<<1, kBlock, 0, s>>>(ws + nch * ny, nch * ny, out + 1);
+  GMT_RET_LAUNCH();
+}
+
 extern "C" int gmt_fill_poly(int mode, int64_t nx, int64_t ny, double x0, double dx, double y0,
                              double dy, double* z, int64_t ld, void* stream) {
   using namespace gmt;
@@ -433,5 +474,5 @@ extern "C" int gmt_device_synchronize(void) { return static_cast<int>(hipDeviceS
 extern "C" const char* gmt_build_info(void) {
   return "libgmt gfx950 (CDNA4) kernels: daxpy, stencil5 1d/2d (dim 1: LDS-DMA pipeline), jacobi5, "
          "jacobi5tb (1-20 fused sweeps, 4 columns per lane), ipc_exchange, signal_wait, "
-         "copy2d_batched, sum_axis, sum, diff_sq, abs_max, fill_poly; built " __DATE__ " " __TIME__;
+         "copy2d_batched, sum_axis, sum, diff_sq, diff_bits, abs_max, fill_poly; built " __DATE__ " " __TIME__;
 }

@@ -102,6 +102,8 @@ def load(device: str = "cuda") -> ctypes.CDLL:
     lib.gmt_engine_jacobi_prepare.restype = c_int
     lib.gmt_engine_jacobi_copy_interior.argtypes = [vp, vp]
     lib.gmt_engine_jacobi_copy_interior.restype = c_int
+    lib.gmt_engine_jacobi_compare.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_double)]
+    lib.gmt_engine_jacobi_compare.restype = c_int
     lib.gmt_engine_jacobi_stat.argtypes = [vp, c_int]
     lib.gmt_engine_jacobi_stat.restype = ctypes.c_double
     lib.gmt_engine_backend.restype = ctypes.c_char_p
@@ -388,6 +390,16 @@ class NativeJacobi:
         out = np.empty((self.ny, self.nx), dtype=np.float64)
         self.lib.gmt_engine_jacobi_copy_interior(self.h, out.ctypes.data)
         return out
+
+    def compare(self, other: "NativeJacobi") -> tuple[float, int]:
+        """Bitwise comparison of this engine's current interior with another
+        engine's (same global problem and process grid), on the device:
+        (max |diff| over ranks, elements whose bits differ over ranks).
+        Collective: every rank calls it."""
+        out = (ctypes.c_double * 2)()
+        if self.lib.gmt_engine_jacobi_compare(self.h, other.h, out):
+            raise EngineError("gmt_engine_jacobi_compare failed")
+        return float(out[0]), int(out[1])
 
     @property
     def points(self) -> int:

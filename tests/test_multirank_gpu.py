@@ -56,6 +56,8 @@ def _need_gpu():
     (4, ["--dims", "2x2"], "n4_dims2x2"),
     # the driver's N = 8 launch: default 4x2 grid, BASELINE's 2x4 timed too
     (8, [], "n8_driver_shape"),
+    # the inline halo through bench.py itself
+    (2, ["--transport", "push", "--small-size", "0"], "n2_push"),
 ])
 def test_bench_oversubscribed_ipc(n, extra, name):
     p = _torchrun(n, ["--size", "8192", "--steps", "20", "--warmup", "5", "--daxpy-n", str(1 << 24),
@@ -66,7 +68,10 @@ def test_bench_oversubscribed_ipc(n, extra, name):
     rec = json.loads(lines[0])
     _record(name, rec)
     assert rec["n_gpus"] == n
-    assert rec["config"]["transport"] == "ipc", rec["config"]
+    push = "push" in extra
+    assert rec["config"]["transport"] == ("ipc inline halo" if push else "ipc"), rec["config"]
+    # the timed run itself, replayed through single sweeps + plain IPC exchanges
+    assert rec["timed_check_mismatches"] == 0 and rec["timed_check_max_diff"] == 0.0, rec
     assert rec["ranks_per_gpu"] == n
     assert rec["check_max_diff"] == 0.0
     # err_norm of the reference's own benchmark at its default per-rank shape
@@ -81,7 +86,7 @@ def test_bench_oversubscribed_ipc(n, extra, name):
     assert rec["value"] > 0 and rec["halo_exchange_us"] > 0
     if "--dims" in extra:
         assert "py2 x px2" in rec["config"]["parallelism"]
-    if "on" in extra:
+    if "--overlap" in extra:
         assert rec["config"]["parallelism"].endswith("overlap")
         # the swapped process grid is timed too (2x1 -> 1x2), same engine path
         assert rec["stencil_alt_dims"] == "1x2" and rec["stencil_alt_dims_MLUPS"] > 0
@@ -102,3 +107,19 @@ def test_bench_ipc_peer_hang_fails_the_job():
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")], p.stdout
     assert "GMT FAULT INJECTION: rank 1" in p.stderr, p.stderr[-4000:]
     assert "timed out waiting for the peer" in p.stdout + p.stderr, (p.stdout + p.stderr)[-4000:]
+
+
+def test_bench_push_corrupt_face_fails_the_job():
+    """Fault injection on the inline halo: rank 1 overwrites one ghost cell
+    its neighbour pushed, at the 2nd fused pass of the timed run
+    (GMT_CORRUPT_PASS=1:2).  The check of the timed run sees the mismatch and
+    the job fails, with the mismatch in the line."""
+    p = _torchrun(2, ["--size", "4096", "--steps", "20", "--warmup", "5", "--skip-extras", "--skip-check",
+                      "--no-calibrate", "--transport", "push"], timeout=200, GMT_CORRUPT_PASS="1:2")
+    assert p.returncode != 0, p.stdout + p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout + p.stderr[-3000:]
+    rec = json.loads(lines[0])
+    assert rec["config"]["transport"] == "ipc inline halo"
+    assert rec["timed_check_mismatches"] > 0 and rec["timed_check_failed"] == ["timed_check"], rec
+    assert "GMT FAULT INJECTION: rank 1" in p.stderr
