@@ -76,11 +76,13 @@ def _sync(env):
         torch.cuda.synchronize(env.device)
 
 
-def _timed(env, fn_run, fn_sync, steps, warmup):
+def _timed(env, fn_run, fn_sync, steps, warmup, on_start=None):
     fn_run(warmup)
     fn_sync()
     gdist.barrier(env)
     _sync(env)
+    if on_start is not None:
+        on_start()  # stream ordered (the engine's clock record reset): after the warm-up
     t0 = time.perf_counter()
     fn_run(steps)
     fn_sync()
@@ -124,8 +126,11 @@ def bench_native(env, shape, steps, warmup, overlap, dims, graph, tblock, wg_wav
     # ranks) -> the plan; then one launch of every pass type of the timed
     # plan; the initial field is restored
     eng.prepare(steps)
-    dt = _timed(env, eng.run, eng.synchronize, steps, warmup)
-    info = {"engine": "native", "graph": eng.graph, "overlap": eng.overlap, "tblock": eng.tblock,
+    dt = _timed(env, eng.run, eng.synchronize, steps, warmup, on_start=eng.clock_reset)
+    clk = eng.clock()
+    # min over ranks: the slowest clock of the job
+    info = {"clock": {"sclk_mhz": -gdist.allreduce_max(-clk["sclk_mhz"], env), "samples": clk["samples"]},
+            "engine": "native", "graph": eng.graph, "overlap": eng.overlap, "tblock": eng.tblock,
             "overlap_tuning": eng.tuned, "tsteps": eng.tsteps, "pass_plan": plan_str(eng.plan(steps)),
             "exact": eng.exact, "max_abs_u0": eng.max_abs_u0, "pass_cost_ms": eng.pass_cost_ms(),
             "transport": (eng.transport + (" inline halo" if eng.push_active else "")
@@ -190,6 +195,11 @@ def check_engine(env, dims, tsteps, graph, init="analytic", seed=0, transport="a
     for ov in ((True,) if push else (True, False)):
         e = NativeJacobi(ny, nx, env, dims=dims, overlap=ov, graph=graph, tblock=k if k > 1 else False,
                          init=init, seed=seed, transport=t, push=push)
+        if push and not e.push_active:
+            # the gate must check the plane the job will run, not the
+            # transport's exchange it would fall back to
+            e.close()
+            raise RuntimeError(f"the inline halo exchange does not apply to the gate's {ny}x{nx} shares")
         e.run(steps)
         e.synchronize()
         part = (e.off_y, e.off_x, e.interior())
@@ -736,6 +746,7 @@ def run_extras(args, env, solver, info, shape, points, tsteps, overlap, dims, gr
                 eng2.close()
             extras[f"stencil_{args.small_size}_MLUPS"] = round(s2[0] * s2[1] * steps2 / dt2 / 1e6, 1)
             extras[f"stencil_{args.small_size}_ms_per_step"] = round(dt2 / steps2 * 1e3, 5)
+            extras[f"stencil_{args.small_size}_sclk_mhz"] = info2["clock"]["sclk_mhz"]
             extras[f"stencil_{args.small_size}_pass_plan"] = f"{steps2} steps: {info2['pass_plan']}"
 
         extra("small-domain stencil run", small)
@@ -885,6 +896,10 @@ def main(argv=None):
     ms_per_step = dt / args.steps * 1e3
     py, px = info["dims"] if info.get("dims") else gdims
     extras["watchdog_timeout_s"] = watchdog_timeout("cuda" if env.is_gpu else "cpu")
+    # the shader clock the timed fused passes ran at (sampled waves' s_memtime
+    # over s_memrealtime; min over ranks): a run's MLUPS against its clock
+    extras["timed_pass_sclk_mhz"] = info["clock"]["sclk_mhz"]
+    extras["timed_pass_clock_samples"] = info["clock"]["samples"]
     if not args.no_timed_check:
         # before any extra: the halo latency and residual extras advance the field
         mark(env, "check of the timed run")

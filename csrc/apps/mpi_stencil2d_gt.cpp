@@ -29,6 +29,10 @@
 //   --timeout=S           hang watchdog (gmt/watchdog.hpp)
 //   --check               compare the ghost rows with the analytic field after EVERY
 //                         exchange (GMT_CORRUPT_GHOST=R:K injects a bad cell); exit 5 on a mismatch
+//   --debug               the reference's DEBUG-build per-rank lines: "%d/%d exchange time
+//                         %0.8f ms" and "%d/%d [%d:0x%08x] err_norm = %.8f" after each
+//                         test_deriv, "%d/%d allreduce time %0.8f ms" after each test_sum
+//                         (mpi_stencil2d_gt.cc:536-539,557-560,635-638)
 #include <mpi.h>
 
 #include <cstdio>
@@ -56,6 +60,7 @@ int main(int argc, char** argv) {
   const bool alloc_per_call = cli.flag("alloc-per-call");
   const std::string tests = cli.get("tests", "deriv,sum");
   const std::string json = cli.get("json", "");
+  const bool debug = cli.flag("debug");
 
   GMT_MPI_CHECK(MPI_Init(&argc, &argv));
   int world_size = 1, world_rank = 0;
@@ -95,6 +100,12 @@ int main(int argc, char** argv) {
     return t;
   };
   auto report = [&](const char* name, int dim, int space, bool buf, const DerivResult& r) {
+    if (debug) {  // every rank, as the reference's DEBUG build (mpi_stencil2d_gt.cc:536-539,557-560)
+      std::printf("%d/%d exchange time %0.8f ms\n", world_rank, world_size, r.total_time / n_iter * 1000);
+      std::printf("%d/%d [%d:0x%08x] err_norm = %.8f\n", world_rank, world_size, b.device, b.info.vendor_id,
+                  r.err_norm);
+      std::fflush(stdout);
+    }
     double time_sum = 0, err_sum = 0;
     MPI_Reduce(&r.total_time, &time_sum, 1, MPI_DOUBLE, MPI_SUM, 0, MPI_COMM_WORLD);
     MPI_Reduce(&r.err_norm, &err_sum, 1, MPI_DOUBLE, MPI_SUM, 0, MPI_COMM_WORLD);
@@ -153,6 +164,10 @@ int main(int argc, char** argv) {
         const int space = m ? GMT_SPACE_MANAGED : GMT_SPACE_DEVICE;
         SumResult r = run_sum(dim, space, n_local_deriv, n_global_other, n_iter, n_warmup, want,
                               b, pool);
+        if (debug) {  // mpi_stencil2d_gt.cc:635-638
+          std::printf("%d/%d allreduce time %0.8f ms\n", world_rank, world_size, r.total_time / n_iter * 1000);
+          std::fflush(stdout);
+        }
         double time_sum = 0, err = r.max_abs_err, err_max = 0;
         MPI_Reduce(&r.total_time, &time_sum, 1, MPI_DOUBLE, MPI_SUM, 0, MPI_COMM_WORLD);
         MPI_Reduce(&err, &err_max, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);

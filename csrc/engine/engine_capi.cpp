@@ -226,10 +226,26 @@ int gmt_engine_jacobi_copy_interior(void* p, double* host) {
   static_cast<Handle*>(p)->s->copy_interior(host);
   return 0;
 }
+int gmt_engine_plan_from_costs(int k, int ks, const double* cost, int measured, int* out, int max) {
+  if (k < 0 || ks < 1 || ks > GMT_TB_MAX_SWEEPS || !cost) return -1;
+  const std::vector<int> plan = gmt::plan_pass_sequence(k, ks, std::vector<double>(cost, cost + ks + 1), measured != 0);
+  for (int i = 0; i < static_cast<int>(plan.size()) && i < max; ++i) out[i] = plan[i];
+  return static_cast<int>(plan.size());
+}
 int gmt_engine_jacobi_compare(void* a, void* b, double* out) {
   if (!a || !b || !out) return 1;
   gmt::watchdog_kick("engine: compare with the single-sweep replay");
   static_cast<Handle*>(a)->s->compare(*static_cast<Handle*>(b)->s, out);
+  return 0;
+}
+int gmt_engine_jacobi_clock(void* p, int reset, double* out) {
+  auto& s = *static_cast<Handle*>(p)->s;
+  if (reset) {
+    s.clock_reset();
+    return 0;
+  }
+  if (!out) return 1;
+  s.clock_read(out);
   return 0;
 }
 double gmt_engine_jacobi_stat(void* p, int what) {

@@ -118,6 +118,13 @@ JacobiSolver::JacobiSolver(comm::Transport& t, const JacobiConfig& c) : t_(t), c
   if (ks_ > 1 && exact_)
     while (ks_ > gmt_jacobi5tb_max_sweeps(1) || !gmt_jacobi5tb_supported(ks_)) --ks_;
   resid_ws_ = Buffer<double>(gmt_jacobi_resid_workspace(nx_, ny_) + 1, GMT_SPACE_DEVICE);
+  {
+    const char* ce = std::getenv("GMT_CLOCK");
+    if (!(ce && ce[0] == '0')) {
+      clk_ = Buffer<uint64_t>(3, GMT_SPACE_DEVICE);
+      clock_reset();
+    }
+  }
   // band-first passes: arrival counter, signal, waiter's count, error word
   sig_ = Buffer<uint64_t>(4, GMT_SPACE_FLAGS);
   for (int b = 0; b < 2; ++b) {
@@ -375,6 +382,7 @@ void JacobiSolver::xk_launch(int K, int n, const int64_t* rects, int parity, int
   const bool sig = sig_rects > 0 || sig_rows > 0 || sig_cols != 0;
   gmt_tb_opts o{K,   cfg_.wg_waves, cfg_.seg_rows, exact_ ? 1 : 0, sig_rects, sig ? count : nullptr,
                 sig ? sig_.data() + 1 : nullptr, sig_rows, st == sb_ && sb_ ? comm_cus_ : 0, sig_cols};
+  o.clock = clk_.data();
   GMT_CHECK("jacobi tb", gmt_jacobi5tb(&o, n, rects, dom, mask, u, un, ld_, ny_ + 2 * g_, st ? st : s_));
 }
 
@@ -514,6 +522,9 @@ void JacobiSolver::setup_push() {
   GMT_CHECK("push flags", gmt_rt_stream_synchronize(s_));
   push_err_ = Buffer<unsigned>(1, GMT_SPACE_PINNED);
   *push_err_.data() = 0;
+  push_stop_ = Buffer<unsigned>(1, GMT_SPACE_DEVICE);
+  GMT_CHECK("push stop", gmt_rt_memset_async(push_stop_.data(), 0, push_stop_.bytes(), s_));
+  GMT_CHECK("push stop", gmt_rt_stream_synchronize(s_));
   PushWire mine;
   std::memset(&mine, 0, sizeof(mine));
   void* own[3] = {buf_[0].data(), buf_[1].data(), push_flags_.data()};
@@ -588,12 +599,15 @@ void JacobiSolver::push_block(int parity, int K) {
   o.exact = exact_ ? 1 : 0;
   for (int d = 0; d < 8; ++d) o.push[d] = push_base_[parity][d];
   o.push_w = g_;
+  o.stop = push_stop_.data();
+  o.clock = clk_.data();
   GMT_CHECK("jacobi tb (inline halo)", gmt_jacobi5tb(&o, 1, dom, dom, halo_mask(), buf_[parity].data(),
                                                      buf_[parity ^ 1].data(), ld_, ny_ + 2 * g_, s_));
   if (push_mask_) {
+    fault_point_exchange(t_.rank());  // GMT_INJECT_HANG: the hand-over is this pass's exchange
     ++push_epoch_;
     GMT_CHECK("push hand-over", gmt_push_sync(push_flags_.data(), push_remote_, push_mask_, push_epoch_,
-                                             push_err_.data(), s_));
+                                             push_err_.data(), push_stop_.data(), s_));
   }
   fresh_[parity ^ 1] = true;
 }
@@ -657,24 +671,33 @@ double JacobiSolver::table_pass_ms(int K) const {
                              : kCostSmall;
   if (tab.ms[K] <= 0 || (push_on_ && K > 1 && !gmt_jacobi5tb_push_supported(K))) return 0.0;
   const bool exchanges = t_.size() > 1 || c.periodic;  // the same on every rank
-  const double over = kLaunchMs + (exchanges && !c.overlap ? kExchangeMs : 0.0);
+  // a push pass exchanges inline (its face stores are in the table's
+  // measured push costs, its hand-over is a launch): no serial exchange
+  const double over = kLaunchMs + (exchanges && !c.overlap && !push_on_ ? kExchangeMs : 0.0);
   return tab.ms[K] * pts / tab.points + over;
 }
 
 std::vector<int> JacobiSolver::plan_passes(int k) const {
-  std::vector<int> plan;
-  if (k <= 0) return plan;
+  if (k <= 0) return {};
   if (ks_ <= 1) return std::vector<int>(k, 1);
   // pass costs: measured on this share (prepare with calibrate; launches and
   // serial exchanges included; max over ranks), else the built-in table for
   // the job's largest share — the same costs, hence the same plan, on every rank
   std::vector<double> cost(ks_ + 1, 0.0);
   for (int K = 1; K <= ks_; ++K) cost[K] = calibrated_ ? meas_ms_[K] : table_pass_ms(K);
-  // measured costs carry ~1-2% of clock noise: a pass shorter than ks_ must
+  return plan_pass_sequence(k, ks_, cost, calibrated_);
+}
+
+std::vector<int> plan_pass_sequence(int k, int ks, std::vector<double> cost, bool measured) {
+  std::vector<int> plan;
+  if (k <= 0) return plan;
+  if (ks <= 1 || static_cast<int>(cost.size()) <= ks) return std::vector<int>(k, 1);
+  const int ks_ = ks;
+  // measured costs carry ~1-2% of clock noise: a pass shorter than ks must
   // win by more than that to displace full passes (a 1000-sweep 8192^2 plan
   // flipped between 50x20 and 5x20+50x18, the latter 1.5% slower:
   // profiles/r05_final/bench_2.json)
-  if (calibrated_)
+  if (measured)
     for (int K = 2; K < ks_; ++K) cost[K] *= 1.02;
   std::vector<double> best(k + 1, 1e300);
   std::vector<int> pick(k + 1, 0);
@@ -893,6 +916,22 @@ void JacobiSolver::compare(JacobiSolver& o, double out[2]) {
   t_.allreduce_sum(res + 1, 1, s_);
   GMT_CHECK("diff bits D2H", gmt_rt_memcpy_async(out, res, 2 * sizeof(double), s_));
   GMT_CHECK("diff bits sync", gmt_rt_stream_synchronize(s_));
+}
+
+void JacobiSolver::clock_reset() {
+  if (clk_.data()) GMT_CHECK("clock reset", gmt_rt_memset_async(clk_.data(), 0, clk_.bytes(), s_));
+}
+
+void JacobiSolver::clock_read(double out[3]) {
+  out[0] = out[1] = out[2] = 0.0;
+  if (!clk_.data()) return;
+  uint64_t c[3] = {0, 0, 0};
+  GMT_CHECK("clock D2H", gmt_rt_memcpy_async(c, clk_.data(), sizeof(c), s_));
+  GMT_CHECK("clock sync", gmt_rt_stream_synchronize(s_));
+  constexpr double kRealtimeMHz = 100.0;  // s_memrealtime: the CDNA constant 100 MHz clock
+  out[0] = c[1] > 0 ? static_cast<double>(c[0]) / static_cast<double>(c[1]) * kRealtimeMHz : 0.0;
+  out[1] = static_cast<double>(c[2]);
+  out[2] = static_cast<double>(c[1]) / (kRealtimeMHz * 1e6);
 }
 
 void JacobiSolver::copy_interior(double* host) const {

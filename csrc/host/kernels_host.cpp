@@ -312,8 +312,12 @@ int gmt_jacobi5tb(const gmt_tb_opts* o, int n_rect, const int64_t* rects, const 
       ok = false;
     if (ok && dom[1] < wout && (dom[1] & 1)) ok = false;  // the GPU kernel's odd-edge stores
     if (!ok) return 1;
+    if (o->stop && __atomic_load_n(o->stop, __ATOMIC_RELAXED) != 0) return 0;  // stopped: the pass does nothing
   }
   const int rc = host_xk(K, n_rect, rects, dom, mask, u, un, ld);
+  if (rc == 0 && o->clock) {  // no shader clock on the CPU: one sample of zero cycles
+    o->clock[2] += 1;
+  }
   if (rc == 0 && w > 0) {
     // the faces of the output, a second time, into the neighbours' ghost cells
     const int64_t x0 = dom[0], x1 = dom[0] + dom[1], y0 = dom[2], y1 = dom[2] + dom[3];
@@ -338,10 +342,12 @@ int gmt_jacobi5tb(const gmt_tb_opts* o, int n_rect, const int64_t* rects, const 
 
 // CPU backend of gmt_push_sync (csrc/kernels/ipc.hip): the same hand-over on
 // memfd-shared flag words, waits bounded by GMT_WAIT_TIMEOUT_MS of wall clock
-int gmt_push_sync(const uint64_t* local, uint64_t* const remote[8], int mask, uint64_t epoch, unsigned* err, void*) {
+int gmt_push_sync(const uint64_t* local, uint64_t* const remote[8], int mask, uint64_t epoch, unsigned* err,
+                  unsigned* stop, void*) {
   if (!local || !err || mask < 0 || mask > 255) return 1;
   for (int d = 0; d < 8; ++d)
     if (((mask >> d) & 1) && (!remote || !remote[d])) return 1;
+  if (stop && __atomic_load_n(stop, __ATOMIC_RELAXED) != 0) return 0;  // stopped: no signal, no wait
   for (int d = 0; d < 8; ++d)
     if ((mask >> d) & 1) __atomic_store_n(remote[d], epoch, __ATOMIC_RELEASE);
   const char* e = std::getenv("GMT_WAIT_TIMEOUT_MS");
@@ -352,6 +358,7 @@ int gmt_push_sync(const uint64_t* local, uint64_t* const remote[8], int mask, ui
     while (__atomic_load_n(local + d, __ATOMIC_ACQUIRE) < epoch) {
       if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
         __atomic_fetch_or(err, 1u << d, __ATOMIC_RELAXED);
+        if (stop) __atomic_fetch_or(stop, 1u << d, __ATOMIC_RELAXED);
         break;
       }
       std::this_thread::yield();
@@ -509,3 +516,10 @@ const char* gmt_build_info(void) {
 }
 
 }  // extern "C"
+
+// the CPU backend has one "XCD": every workgroup on 0
+extern "C" int gmt_xcd_of_workgroups(int n, unsigned* out, void*) {
+  if (n < 1 || n > 4096 || !out) return 1;
+  for (int i = 0; i < n; ++i) out[i] = 0;
+  return 0;
+}

@@ -19,7 +19,9 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <vector>
 
+#include "gmt/numa_bind.hpp"
 #include "gmt/rt.h"
 
 namespace {
@@ -220,6 +222,15 @@ int gmt_rt_stream_create(gmt_stream_t* s, int) {
 int gmt_rt_stream_create_cumask(gmt_stream_t* s, int, const uint32_t*) { return gmt_rt_stream_create(s, 0); }
 int gmt_rt_bind_numa(int, int* node) {
   *node = -1;
+  return kOk;
+}
+// the CPU backend: off by default (the CPU test suite runs many jobs side by
+// side; pinning every job's rank 0 to one core would serialise them)
+int gmt_rt_pin_rank(int local_rank, int local_size, int, int* cpu) {
+  *cpu = -1;
+  if (!gmt::pin_enabled(false) || local_size < 1 || local_rank < 0 || local_rank >= local_size) return kOk;
+  std::vector<int> rank_node(local_size, -1);
+  *cpu = gmt::pin_rank_core(local_rank, local_size, rank_node.data());
   return kOk;
 }
 int gmt_rt_device_cu_count(int* n) {

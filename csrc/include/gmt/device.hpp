@@ -27,6 +27,7 @@ struct RankBinding {
   int device = 0, n_devices = 1, ranks_per_device = 1;
   size_t mem_per_rank = 0;
   int numa_node = -1;  // CPUs bound to this NUMA node (gmt_rt_bind_numa), -1 = unbound
+  int pinned_cpu = -1;  // the core this rank is pinned to (gmt_rt_pin_rank), -1 = not pinned
   gmt_device_info info{};
 };
 
@@ -84,6 +85,8 @@ inline RankBinding set_rank_device(MPI_Comm comm, bool print) {
   GMT_CHECK("set device", gmt_rt_set_device(b.device));
   // the GPU's socket: before any transport allocates its staging buffers
   GMT_CHECK("numa bind", gmt_rt_bind_numa(b.device, &b.numa_node));
+  // one core near the GPU per rank, distinct per local rank (GMT_PIN=0: off)
+  GMT_CHECK("pin rank", gmt_rt_pin_rank(b.local_rank, b.local_size, b.ranks_per_device, &b.pinned_cpu));
   watchdog_start(b.rank, b.device);
   watchdog_kick("device bound");
   return b;

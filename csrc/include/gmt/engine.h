@@ -72,6 +72,12 @@ int gmt_engine_jacobi_copy_interior(void* h, double* host);
  * problem and process grid (collective): out[0] = max |diff| over ranks,
  * out[1] = elements whose bits differ, summed over ranks */
 int gmt_engine_jacobi_compare(void* a, void* b, double* out);
+/* gmt::plan_pass_sequence on given costs (cost[0..ks], ms per K-sweep pass):
+ * the sweeps per pass, written to out[0..max); returns the plan length */
+int gmt_engine_plan_from_costs(int k, int ks, const double* cost, int measured, int* out, int max);
+/* reset != 0: zero the fused passes' clock record (stream ordered); else
+ * out[3] = {shader MHz, samples, seconds sampled} since the last reset */
+int gmt_engine_jacobi_clock(void* h, int reset, double* out);
 double gmt_engine_jacobi_stat(void* h, int what);
 const char* gmt_engine_backend(void);
 

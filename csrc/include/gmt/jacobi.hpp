@@ -117,6 +117,12 @@ class JacobiSolver {
   // sweeps through single sweeps and compares (reference: the err_norm of the
   // timed field, mpi_stencil2d_gt.cc:541-570).  Collective.
   void compare(JacobiSolver& o, double out[2]);
+  // Shader clock of the fused passes since the last clock_reset() (stream
+  // ordered): one sampled wave per 256 workgroups stamps s_memtime and
+  // s_memrealtime (gmt_tb_opts.clock).  out = {MHz (0 without samples or on
+  // the CPU backend), samples, seconds sampled}.  GMT_CLOCK=0: no stamps.
+  void clock_reset();
+  void clock_read(double out[3]);
 
   int64_t nx() const { return nx_; }
   int64_t ny() const { return ny_; }
@@ -216,6 +222,8 @@ class JacobiSolver {
   uint64_t push_epoch_ = 0;
   Buffer<uint64_t> push_flags_;  // [d]: written by the neighbour in direction d
   Buffer<unsigned> push_err_;    // host-visible: bit d = the wait for direction d expired
+  Buffer<unsigned> push_stop_;   // device word: a wait expired, later passes return at once
+  Buffer<uint64_t> clk_;         // gmt_tb_opts.clock: cycles, 100 MHz ticks, samples
   std::vector<void*> push_opened_;
 };
 
@@ -225,6 +233,13 @@ inline void block_split(int64_t n, int p, int i, int64_t* off, int64_t* len) {
   *off = i * base + (i < rem ? i : rem);
   *len = base + (i < rem ? 1 : 0);
 }
+
+// The cheapest sequence of fused passes covering k sweeps, passes of at most
+// ks sweeps, cost[K] = ms of a K-sweep pass (0: no such pass; K = 1 a single
+// sweep); measured costs get a 2% handicap on passes shorter than ks (clock
+// noise must not displace full passes).  Full passes first, then the rest,
+// largest first.  JacobiSolver::plan_passes with this rank's costs.
+std::vector<int> plan_pass_sequence(int k, int ks, std::vector<double> cost, bool measured);
 
 // Process grid minimising the halo bytes per rank; strided x faces (which
 // need a pack kernel) are weighted 1.5x a contiguous y face.

@@ -207,6 +207,18 @@ typedef struct gmt_tb_opts {
      wider than a strip (no odd-edge stores). */
   const double* push[8];
   int push_w;
+  /* Inline-halo passes only (push_w > 0): a device word (NULL = none) that a
+     timed-out hand-over sets (gmt_push_sync `stop`); while it is non-zero
+     every workgroup of the pass returns at entry — its ghost cells are
+     stale and a late neighbour may still be writing them — and the job
+     fails at its next synchronisation. */
+  const unsigned* stop;
+  /* Shader-clock record (NULL = none): one sampled wave per 256 workgroups
+     adds its s_memtime delta (shader cycles) to clock[0], its
+     s_memrealtime delta (the 100 MHz constant clock) to clock[1] and 1 to
+     clock[2] (device memory, zeroed by the caller): the clock the pass ran
+     at is clock[0] / clock[1] x 100 MHz. */
+  uint64_t* clock;
 } gmt_tb_opts;
 enum { GMT_PUSH_S = 0, GMT_PUSH_N = 1, GMT_PUSH_W = 2, GMT_PUSH_E = 3,
        GMT_PUSH_SW = 4, GMT_PUSH_SE = 5, GMT_PUSH_NW = 6, GMT_PUSH_NE = 7 };
@@ -241,9 +253,18 @@ int gmt_signal_wait(const uint64_t* signal, uint64_t* seen, unsigned* err, void*
  * epoch (the neighbour's faces are in this rank's ghost cells) and acquires
  * on every XCD.  Each wait is bounded by GMT_WAIT_TIMEOUT_MS of device wall
  * clock (default 10 s); an expired one ORs 1 << d into *err (host-visible)
- * and gives up.  local / remote: GMT_SPACE_FLAGS memory. */
+ * and into *stop (device memory, may be NULL: the gmt_tb_opts.stop word of
+ * the following passes, which then return at once) and gives up.  While
+ * *stop is non-zero the hand-over neither signals nor waits, so a stalled
+ * neighbour stops the whole job within one wait instead of one per pass.
+ * local / remote: GMT_SPACE_FLAGS memory. */
 int gmt_push_sync(const uint64_t* local, uint64_t* const remote[8], int mask, uint64_t epoch, unsigned* err,
-                  void* stream);
+                  unsigned* stop, void* stream);
+
+/* Test hook: the XCD (XCC_ID) each of n one-wave workgroups of a single
+ * launch ran on, out[i] for workgroup i (device memory).  gmt_push_sync's
+ * per-XCD acquire relies on workgroups i < 8 landing on 8 distinct XCDs. */
+int gmt_xcd_of_workgroups(int n, unsigned* out, void* stream);
 
 /* ---- Stream-ordered IPC exchange (csrc/kernels/ipc.hip), one launch per
  *      exchange of a persistent plan: e = *epoch + 1.  Send channel: wait

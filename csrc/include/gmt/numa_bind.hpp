@@ -84,4 +84,113 @@ inline int bind_numa_near(int pci_domain, int pci_bus, int pci_device) {
   return bound > 0 ? node : -1;
 }
 
+// ---- rank pinning (default on the GPU backend; GMT_PIN=0: off)
+//
+// Round 5 traced the host-staged exchange's bimodal slow mode to unpinned
+// ranks: `mpirun -bind-to core` removed it in 12 of 12 runs
+// (profiles/r05_xport/README.md).  The reference's Summit launch binds its
+// resource sets the same way (summit/run.sh:30: jsrun).  So every rank pins
+// itself to ONE physical core (all its hardware threads) near its GPU:
+//   * the candidate CPUs are the GPU's NUMA node's CPUs within the allowed
+//     set (a launcher's binding is only ever narrowed, never widened), all
+//     allowed CPUs when the node is unknown or the intersection is empty;
+//   * the ranks whose GPUs share that node take consecutive physical cores
+//     of it in local-rank order — like `-bind-to core`, which put two ranks
+//     on neighbouring cores (one CCD, one L3).  Spreading them over the node
+//     instead halved the host-staged exchange: 7.1-7.6 GB/s per rank
+//     against 14.9-15.6 unpinned (profiles/r06_pin/);
+//   * nothing changes when the allowed set is already one core.
+// node_of_rank[i]: the NUMA node of local rank i's GPU (-1 unknown).
+// Returns the first CPU of the core pinned to, or -1 (nothing changed).
+inline bool cpu_siblings(int cpu, cpu_set_t* set) {
+  char path[128];
+  std::snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", cpu);
+  FILE* f = std::fopen(path, "r");
+  if (!f) return false;
+  char buf[256] = {0};
+  const bool got = std::fgets(buf, sizeof(buf), f) != nullptr;
+  std::fclose(f);
+  return got && parse_cpulist(buf, set);
+}
+
+inline bool node_cpus(int node, cpu_set_t* set) {
+  char path[128];
+  std::snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+  FILE* f = std::fopen(path, "r");
+  if (!f) return false;
+  char buf[4096] = {0};
+  const bool got = std::fgets(buf, sizeof(buf), f) != nullptr;
+  std::fclose(f);
+  return got && parse_cpulist(buf, set);
+}
+
+inline int pci_numa_node(int pci_domain, int pci_bus, int pci_device) {
+  char path[128];
+  std::snprintf(path, sizeof(path), "/sys/bus/pci/devices/%04x:%02x:%02x.0/numa_node", pci_domain, pci_bus,
+                pci_device);
+  return read_int_file(path, -1);
+}
+
+inline int set_all_threads_affinity(const cpu_set_t& want) {
+  DIR* d = opendir("/proc/self/task");
+  if (!d) return sched_setaffinity(0, sizeof(want), &want) == 0 ? 1 : 0;
+  int bound = 0;
+  while (dirent* e = readdir(d)) {
+    const int tid = std::atoi(e->d_name);
+    if (tid > 0 && sched_setaffinity(tid, sizeof(want), &want) == 0) ++bound;
+  }
+  closedir(d);
+  return bound;
+}
+
+inline int pin_rank_core(int local_rank, int local_size, const int* node_of_rank) {
+  cpu_set_t allowed;
+  if (local_rank < 0 || local_rank >= local_size || sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return -1;
+  const int node = node_of_rank[local_rank];
+  cpu_set_t cand = allowed;
+  if (node >= 0) {
+    cpu_set_t near, both;
+    if (node_cpus(node, &near)) {
+      CPU_AND(&both, &near, &allowed);
+      if (CPU_COUNT(&both) > 0) cand = both;
+    }
+  }
+  // physical cores of the candidates: the first allowed CPU of each sibling set
+  int cores[CPU_SETSIZE];
+  int nc = 0;
+  cpu_set_t seen;
+  CPU_ZERO(&seen);
+  for (int c = 0; c < CPU_SETSIZE; ++c) {
+    if (!CPU_ISSET(c, &cand) || CPU_ISSET(c, &seen)) continue;
+    cpu_set_t sib;
+    if (!cpu_siblings(c, &sib)) {
+      CPU_ZERO(&sib);
+      CPU_SET(c, &sib);
+    }
+    for (int s = 0; s < CPU_SETSIZE; ++s)
+      if (CPU_ISSET(s, &sib)) CPU_SET(s, &seen);
+    cores[nc++] = c;
+  }
+  if (nc == 0) return -1;
+  // this rank's index among the local ranks whose GPUs share its node
+  int idx = 0;
+  for (int r = 0; r < local_rank; ++r) idx += node_of_rank[r] == node ? 1 : 0;
+  const int core = cores[idx % nc];
+  cpu_set_t want, sib;
+  if (!cpu_siblings(core, &sib)) {
+    CPU_ZERO(&sib);
+    CPU_SET(core, &sib);
+  }
+  CPU_AND(&want, &sib, &allowed);
+  if (CPU_COUNT(&want) == 0 || CPU_EQUAL(&want, &allowed)) return -1;
+  return set_all_threads_affinity(want) > 0 ? core : -1;
+}
+
+// GMT_PIN: "0" off, "1" on; unset: on for the GPU backend (default_on)
+inline bool pin_enabled(bool default_on) {
+  const char* e = std::getenv("GMT_PIN");
+  if (!e || !*e) return default_on;
+  return std::atoi(e) != 0;
+}
+
 }  // namespace gmt

@@ -108,6 +108,14 @@ int gmt_rt_device_cu_count(int* n);
    (gmt/numa_bind.hpp; opt-in: GMT_NUMA_BIND=1).  *node = the node, or -1
    when nothing changed (the host backend: always -1). */
 int gmt_rt_bind_numa(int dev, int* node);
+/* Pin every thread of this process to one physical core near its GPU
+   (gmt/numa_bind.hpp pin_rank_core): local ranks map to devices by the
+   reference's block rule (ranks_per_device ranks per GPU, local rank r on
+   device r / ranks_per_device), the ranks sharing a NUMA node take distinct
+   cores.  Default on with the HIP backend, off on the host backend;
+   GMT_PIN=0/1 overrides.  *cpu = the core's first CPU, or -1 when nothing
+   changed. */
+int gmt_rt_pin_rank(int local_rank, int local_size, int ranks_per_device, int* cpu);
 int gmt_rt_stream_destroy(gmt_stream_t s);
 int gmt_rt_stream_synchronize(gmt_stream_t s);
 int gmt_rt_stream_wait_event(gmt_stream_t s, gmt_event_t e);

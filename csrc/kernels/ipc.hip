@@ -180,17 +180,32 @@ __global__ __launch_bounds__(kWave) void signal_wait_kernel(const uint64_t* sign
 // not pull: a strided W / E face would need its own exchange launch between
 // the passes (pack or copy kernel, the 9-10% of round 4); written by the
 // pass itself it costs a few store instructions and this launch.
+//
+// Which mechanism makes the pushed cells visible to the next pass: the
+// writer's system-scope release (above) and, on this side, an acquire on
+// every XCD's L2.  Two acquires cover that: the system-scope fence at the
+// end of this kernel, run by one workgroup on each XCD — the dispatcher
+// deals the workgroups of a launch to the XCDs round robin, starting where
+// the previous launch left off (workgroup i on XCD (x0 + i) mod 8), so the 8
+// workgroups of this launch cover the 8 XCDs whatever x0;
+// tests/test_kernels_gpu.py::test_workgroups_round_robin_over_xcds asserts
+// it with gmt_xcd_of_workgroups — and the acquire fence of the next kernel's
+// dispatch packet.
 struct PushSyncArgs {
   const uint64_t* local;
   uint64_t* remote[8];
   uint64_t epoch;
   unsigned* err;
+  unsigned* stop;
   uint64_t ticks;
   int mask;
 };
 
 __global__ __launch_bounds__(kWave) void push_sync_kernel(PushSyncArgs a) {
   const int d = threadIdx.x;
+  // stopped (an earlier wait expired): no signal, no wait — the passes
+  // return at entry and the host aborts at its next synchronisation
+  if (a.stop && __hip_atomic_load(a.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   const bool mine = d < 8 && ((a.mask >> d) & 1);
   if (blockIdx.x == 0 && mine) {
     // the pass's face stores are complete: its waves drained vmcnt and the
@@ -205,6 +220,7 @@ __global__ __launch_bounds__(kWave) void push_sync_kernel(PushSyncArgs a) {
       __builtin_amdgcn_s_sleep(2);
       if (wall_clock64() - t0 > a.ticks) {
         __hip_atomic_fetch_or(a.err, 1u << d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (a.stop) __hip_atomic_fetch_or(a.stop, 1u << d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
@@ -304,7 +320,7 @@ extern "C" int gmt_ipc_exchange(const gmt_ipc_plan* p, void* stream) {
 }
 
 extern "C" int gmt_push_sync(const uint64_t* local, uint64_t* const remote[8], int mask, uint64_t epoch, unsigned* err,
-                             void* stream) {
+                             unsigned* stop, void* stream) {
   using namespace gmt;
   if (!local || !err || mask < 0 || mask > 255) return static_cast<int>(hipErrorInvalidValue);
   ipc::PushSyncArgs a{};
@@ -315,9 +331,25 @@ extern "C" int gmt_push_sync(const uint64_t* local, uint64_t* const remote[8], i
   }
   a.epoch = epoch;
   a.err = err;
+  a.stop = stop;
   a.ticks = ipc::timeout_ticks();
   a.mask = mask;
   if (mask == 0) return 0;
   ipc::push_sync_kernel<<<kNumXcd, kWave, 0, static_cast<hipStream_t>(stream)>>>(a);
+  GMT_RET_LAUNCH();
+}
+
+namespace gmt {
+namespace ipc {
+__global__ __launch_bounds__(kWave) void xcd_probe_kernel(unsigned* out) {
+  if (threadIdx.x == 0) out[blockIdx.x] = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xfu;  // XCC_ID
+}
+}  // namespace ipc
+}  // namespace gmt
+
+extern "C" int gmt_xcd_of_workgroups(int n, unsigned* out, void* stream) {
+  using namespace gmt;
+  if (n < 1 || n > 4096 || !out) return static_cast<int>(hipErrorInvalidValue);
+  ipc::xcd_probe_kernel<<<n, kWave, 0, static_cast<hipStream_t>(stream)>>>(out);
   GMT_RET_LAUNCH();
 }

@@ -122,6 +122,12 @@ struct Args {
   // ghost cells of the neighbour's next input; nullptr: no neighbour that way
   const double* push[8];
   int64_t push_w;                // face width
+  // PUSH: non-zero *stop (a timed-out hand-over, gmt_push_sync) makes every
+  // workgroup return at entry
+  const unsigned* stop;
+  // shader-clock record (gmt_tb_opts.clock): sampled waves add their
+  // s_memtime / s_memrealtime deltas and a count
+  uint64_t* clk;
   // GMT_TB_WG_TRACE builds (scripts/build_variant.sh): per workgroup, its
   // tile, start and end (s_memrealtime, 100 MHz) and hardware ids
   uint64_t* wg_trace;
@@ -789,8 +795,25 @@ inline bool tail_swizzle_ok(int64_t nb, int64_t ne) {
 template <int K, bool EXACT, bool EDGE, bool PUSH>
 __global__ __launch_bounds__(kMaxThreads) __attribute__((amdgpu_waves_per_eu(2)))
 void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__ un, int64_t nblocks) {
+  if constexpr (PUSH) {
+    // a hand-over that timed out: the ghost cells are stale and a late
+    // neighbour may still write them; the host aborts at its next sync
+    if (a.stop && *a.stop != 0) return;
+  }
   const int64_t ns = a.sig_wgs, nd = a.sig_dispatch;
   const int64_t b = blockIdx.x;
+  // clock record: wave 0 of one workgroup in 256, from the middle of each
+  // 256: its start stamps go to 16 B of LDS past the strips' rings (no
+  // memory operation in front of the pipeline's exact vmcnt waits: start
+  // atomics here cost a one-round 8192^2 pass 1.6%, profiles/r06_clock/),
+  // the deltas go out by vector atomics once the workgroup's work is done
+  extern __shared__ d2 lds_dyn[];
+  uint64_t* stamp = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(lds_dyn) + a.nw * strip_lds<K>());
+  const bool clk = a.clk && (b & 255) == 128 && threadIdx.x == 0;
+  if (clk) {
+    stamp[0] = __builtin_amdgcn_s_memtime();
+    stamp[1] = __builtin_amdgcn_s_memrealtime();
+  }
   // signalling workgroups (and row bands) first, in dispatch order over all
   // XCDs; the rest XCD-contiguous
   const int64_t t = a.edges_last > 0 ? tail_swizzle(b, nblocks, a.edges_last)
@@ -799,6 +822,12 @@ void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__
   const uint64_t wg_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
   tb_block<K, EXACT, EDGE, PUSH>(a, u, un, t);
+  if (clk) {
+    const uint64_t m1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    __hip_atomic_fetch_add(a.clk, m1 - stamp[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(a.clk + 1, r1 - stamp[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(a.clk + 2, uint64_t{1}, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 #if GMT_TB_WG_TRACE
   __syncthreads();
   if (threadIdx.x == 0 && a.wg_trace) {
@@ -1191,7 +1220,8 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   const int64_t lmax = std::min<int64_t>(1 << 20, (int64_t(1) << 31) / (ld * 8) - 3 * K - C::LAG - 2 * C::U - C::P);
   if (lmax < 1) return static_cast<int>(hipErrorInvalidValue);
   (void)maxh;
-  const size_t smem = static_cast<size_t>(a.nw * strip_lds<K>());
+  // + 16 B: the clock record's start stamps (jacobi5tb_kernel)
+  const size_t smem = static_cast<size_t>(a.nw * strip_lds<K>()) + 16;
   if (smem > 65536) {  // above the default dynamic-LDS limit (gfx950 has 160 KB per CU)
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE, PUSH>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem));
@@ -1323,6 +1353,8 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   a.prio = nb <= per_cu ? 1 : 0;
   a.sig_count = o.signal_count;
   a.signal = o.signal;
+  a.stop = PUSH ? o.stop : nullptr;
+  a.clk = o.clock;
   if (info) {
     hipFuncAttributes fa{};
     (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE, PUSH>));

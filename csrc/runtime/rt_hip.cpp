@@ -13,6 +13,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 #include "gmt/numa_bind.hpp"
 #include "gmt/rt.h"
@@ -179,6 +180,23 @@ int gmt_rt_bind_numa(int dev, int* node) {
   const hipError_t e = hipGetDeviceProperties(&p, dev);
   *node = e == hipSuccess ? gmt::bind_numa_near(p.pciDomainID, p.pciBusID, p.pciDeviceID) : -1;
   RT_RET(e);
+}
+int gmt_rt_pin_rank(int local_rank, int local_size, int ranks_per_device, int* cpu) {
+  *cpu = -1;
+  if (!gmt::pin_enabled(true) || local_size < 1 || local_rank < 0 || local_rank >= local_size) return 0;
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev < 1) RT_RET(e);
+  const int per = ranks_per_device > 0 ? ranks_per_device : 1;
+  std::vector<int> dev_node(ndev, -1), rank_node(local_size, -1);
+  for (int d = 0; d < ndev; ++d) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, d) == hipSuccess)
+      dev_node[d] = gmt::pci_numa_node(p.pciDomainID, p.pciBusID, p.pciDeviceID);
+  }
+  for (int r = 0; r < local_size; ++r) rank_node[r] = dev_node[(r / per) % ndev];
+  *cpu = gmt::pin_rank_core(local_rank, local_size, rank_node.data());
+  return 0;
 }
 int gmt_rt_device_cu_count(int* n) {
   int dev = 0;

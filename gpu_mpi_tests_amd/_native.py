@@ -71,6 +71,8 @@ class TbOpts(ctypes.Structure):
         ("signal_cols", c_int),
         ("push", c_vp * 8),
         ("push_w", c_int),
+        ("stop", c_vp),
+        ("clock", c_vp),
     ]
 
 _SIGS = {
@@ -108,6 +110,8 @@ _SIGS = {
     "gmt_add_scalar": (c_int, [c_i64, c_i64, c_dbl, c_vp, c_i64, c_vp]),
     "gmt_error_string": (ctypes.c_char_p, [c_int]),
     "gmt_device_synchronize": (c_int, []),
+    "gmt_xcd_of_workgroups": (c_int, [c_int, c_vp, c_vp]),
+    "gmt_diff_bits": (c_int, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "gmt_build_info": (ctypes.c_char_p, []),
 }
 

@@ -104,6 +104,8 @@ def load(device: str = "cuda") -> ctypes.CDLL:
     lib.gmt_engine_jacobi_copy_interior.restype = c_int
     lib.gmt_engine_jacobi_compare.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_double)]
     lib.gmt_engine_jacobi_compare.restype = c_int
+    lib.gmt_engine_jacobi_clock.argtypes = [vp, c_int, ctypes.POINTER(ctypes.c_double)]
+    lib.gmt_engine_jacobi_clock.restype = c_int
     lib.gmt_engine_jacobi_stat.argtypes = [vp, c_int]
     lib.gmt_engine_jacobi_stat.restype = ctypes.c_double
     lib.gmt_engine_backend.restype = ctypes.c_char_p
@@ -400,6 +402,18 @@ class NativeJacobi:
         if self.lib.gmt_engine_jacobi_compare(self.h, other.h, out):
             raise EngineError("gmt_engine_jacobi_compare failed")
         return float(out[0]), int(out[1])
+
+    def clock_reset(self) -> None:
+        """Zero the fused passes' shader-clock record (stream ordered)."""
+        self.lib.gmt_engine_jacobi_clock(self.h, 1, None)
+
+    def clock(self) -> dict:
+        """The clock the fused passes ran at since clock_reset(): sampled
+        waves' s_memtime / s_memrealtime deltas (gmt_tb_opts.clock).  MHz is
+        0 on the CPU backend or without samples (GMT_CLOCK=0)."""
+        out = (ctypes.c_double * 3)()
+        self.lib.gmt_engine_jacobi_clock(self.h, 0, out)
+        return {"sclk_mhz": round(out[0], 1), "samples": int(out[1]), "sampled_s": round(out[2], 6)}
 
     @property
     def points(self) -> int:

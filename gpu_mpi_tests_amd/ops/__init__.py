@@ -11,7 +11,9 @@ from .kernels import (  # noqa: F401
     copy2d_batched,
     daxpy,
     diff_norm,
+    diff_bits,
     diff_sq,
+    xcd_of_workgroups,
     fill_poly,
     jacobi5,
     jacobi5_rects,

@@ -219,6 +219,39 @@ def diff_sq(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def diff_bits(a: torch.Tensor, b: torch.Tensor) -> tuple[float, int]:
+    """Bitwise comparison of two 2-D fp64 regions (gmt_diff_bits): (max
+    |a - b| with NaN as +inf, number of elements whose 64 bits differ)."""
+    if a.dim() == 1:
+        a, b = a.view(1, -1), b.view(1, -1)
+    _check2d(a, "diff_bits.a")
+    _check2d(b, "diff_bits.b")
+    if tuple(a.shape) != tuple(b.shape):
+        raise ValueError("diff_bits: shape mismatch")
+    if not _is_dev(a):
+        ne = a.view(torch.int64) != b.view(torch.int64)
+        d = (a - b).abs().nan_to_num(nan=float("inf"))[ne]
+        return (float(d.max()) if d.numel() else 0.0), int(ne.sum())
+    ny, nx = a.shape
+    L = _native.lib()
+    ws = torch.empty(max(2, 2 * L.gmt_diff_sq_workspace(nx, ny)), dtype=torch.float64, device=a.device)
+    out = torch.empty(2, dtype=torch.float64, device=a.device)
+    _native.check(L.gmt_diff_bits(nx, ny, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
+                                  out.data_ptr(), ws.data_ptr(), _stream(a)), "gmt_diff_bits")
+    o = out.cpu()
+    return float(o[0]), int(o[1])
+
+
+def xcd_of_workgroups(n: int, device: str = "cuda") -> list[int]:
+    """The XCD each workgroup of one n-workgroup launch ran on (test hook of
+    gmt_push_sync's per-XCD acquire)."""
+    out = torch.zeros(n, dtype=torch.int32, device=device)
+    _native.check(_native.lib().gmt_xcd_of_workgroups(int(n), out.data_ptr(),
+                                                      torch.cuda.current_stream(out.device).cuda_stream),
+                  "gmt_xcd_of_workgroups")
+    return out.cpu().tolist()
+
+
 def diff_norm(a: torch.Tensor, b: torch.Tensor) -> float:
     return float(diff_sq(a, b).sqrt())
 

@@ -36,6 +36,7 @@ class DistEnv:
     n_devices: int = 0
     ranks_per_device: int = 1
     backend: str = "none"  # "nccl" (= RCCL on ROCm), "gloo" or "none" (single process)
+    pinned_cpu: int = -1   # the core this rank pinned itself to (pin_rank), -1 = not pinned
     initialized_here: bool = False
     host_group: object = None  # a gloo group for host-side control / host-staged data
 
@@ -82,6 +83,27 @@ def select_device(local_rank: int, local_world_size: int, n_devices: int) -> tup
     return local_rank, 1
 
 
+def pin_rank(local_rank: int, local_world_size: int, ranks_per_device: int) -> int:
+    """Pin this process to one physical core near its GPU, a distinct core
+    per local rank (native gmt_rt_pin_rank, gmt/numa_bind.hpp pin_rank_core:
+    the same rule as the C++ apps' set_rank_device).  Unpinned ranks showed
+    a bimodal slow mode in the host-staged exchange that ``mpirun -bind-to
+    core`` removed (profiles/r05_xport/README.md); the reference's Summit
+    launch binds resource sets (summit/run.sh:30).  A launcher's binding is
+    only narrowed.  GMT_PIN=0 turns it off.  Returns the core's first CPU or
+    -1 (nothing changed)."""
+    import ctypes
+
+    from .. import _native
+
+    L = _native.lib()
+    L.gmt_rt_pin_rank.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    L.gmt_rt_pin_rank.restype = ctypes.c_int
+    cpu = ctypes.c_int(-1)
+    L.gmt_rt_pin_rank(int(local_rank), int(local_world_size), int(ranks_per_device), ctypes.byref(cpu))
+    return cpu.value
+
+
 def init(backend: str | None = None, device: str | None = None, timeout_s: float = 600.0) -> DistEnv:
     """Initialise (once) the process group from torchrun-style env vars.
 
@@ -105,6 +127,8 @@ def init(backend: str | None = None, device: str | None = None, timeout_s: float
         torch.cuda.set_device(idx)
         env.device = torch.device("cuda", idx)
         env.ranks_per_device = per
+        if world > 1:
+            env.pinned_cpu = pin_rank(local_rank, local_world, per)
     else:
         env.device = torch.device("cpu")
 

@@ -17,16 +17,20 @@ tag=${um}_${prof}_${nodes}_${ppn}
 here=$(cd "$(dirname "$0")/.." && pwd)
 bin=${GMT_BIN:-$here/build/bin}
 mpirun=${MPIRUN:-/opt/conda/bin/mpirun}
+# one core per rank, like the reference's jsrun resource sets (summit/run.sh:30);
+# the ranks also pin themselves near their GPU when a launcher does not
+# (gmt_rt_pin_rank, GMT_PIN=0 to disable); MPIRUN_BIND="" leaves it to them
+bind=${MPIRUN_BIND--bind-to core}
 app=$bin/mpi_daxpy_nvtx_unmanaged
 [ "$um" == "um" ] && app=$bin/mpi_daxpy_nvtx_managed
 np=$((nodes * ppn))
 if [ "$prof" == "rocprof" ]; then
   mkdir -p profile/$tag
   export TMPDIR=${TMPDIR:-/tmp}
-  $mpirun -np $np rocprofv3 --marker-trace --kernel-trace --memory-copy-trace \
+  $mpirun $bind -np $np rocprofv3 --marker-trace --kernel-trace --memory-copy-trace \
     --selected-regions --output-format csv -d profile/$tag/%rank% -o $tag \
     -- $app > out-${tag}.txt 2>&1
 else
-  $mpirun -np $np $app > out-${tag}.txt 2>&1
+  $mpirun $bind -np $np $app > out-${tag}.txt 2>&1
 fi
 echo "wrote out-${tag}.txt"

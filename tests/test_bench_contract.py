@@ -334,3 +334,29 @@ def test_probe_order_and_margin():
     assert pick({"ipc": 1.00, "push": 0.98}) == "ipc"                   # ranks sharing a GPU: no rccl
     assert pick({"ipc": 1.00, "push": 0.96}) == "push"
     assert pick({"push": 1.0}) == "push" and pick({}) == "auto"
+
+
+def test_bench_push_stalled_neighbour_stops_the_passes_cpu():
+    """an inline-halo hand-over that times out stops
+    every later pass at once (gmt_push_sync sets the stop word the passes
+    check at entry; later hand-overs neither signal nor wait) and the job
+    aborts at the next synchronisation.  Rank 1 stalls at its 11th exchange (a hand-over)
+    (GMT_INJECT_HANG); rank 0's wait gives up after 2 s.  Without the stop
+    every one of the ~40 passes left would wait its own 2 s."""
+    import time
+    port = str(free_port())
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
+               GMT_INJECT_HANG="1:10", GMT_WAIT_TIMEOUT_MS="2000")
+    t0 = time.time()
+    p = subprocess.run(["timeout", "-k", "5", "200", sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port", port, "bench.py",
+                        "--gpus", "2", "--device", "cpu", "--size", "600", "--steps", "800", "--warmup", "1",
+                        "--skip-extras", "--skip-check", "--no-calibrate", "--transport", "push"],
+                       capture_output=True, text=True, timeout=230, cwd=ROOT, env=env)
+    dt = time.time() - t0
+    out = p.stdout + p.stderr
+    assert p.returncode != 0, out[-3000:]
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")], p.stdout
+    assert "GMT FAULT INJECTION: rank 1" in p.stderr, out[-3000:]
+    assert "inline-halo hand-over timed out" in out, out[-3000:]
+    assert dt < 60, dt  # one expired wait, not one per remaining pass

@@ -247,3 +247,38 @@ def test_native_engine_push_multirank(np_, ny, nx, steps, periodic, tblock, dims
     assert r["push"], r
     assert r["diff"] == 0.0, r
     assert r["resid_same"]
+
+
+def _plan(k, ks, cost, measured):
+    import ctypes
+    from gpu_mpi_tests_amd.engine import load
+    lib = load("cpu")
+    lib.gmt_engine_plan_from_costs.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                               ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    lib.gmt_engine_plan_from_costs.restype = ctypes.c_int
+    c = (ctypes.c_double * (ks + 1))(*cost)
+    out = (ctypes.c_int * max(1, k))()
+    n = lib.gmt_engine_plan_from_costs(k, ks, c, int(measured), out, max(1, k))
+    return list(out[:n])
+
+
+def test_pass_plan_tie_break():
+    """The pass planner's 2% handicap on measured passes shorter than the
+    full K: calibration noise of ~1% must not displace full
+    passes, a real 3% gain must."""
+    ks = 20
+    cost = [0.0] + [0.05 + 0.0150 * K for K in range(1, ks + 1)]  # ms: launch + sweeps
+    # 18-sweep passes 1% cheaper per sweep than their share of a 20-sweep pass
+    c18 = list(cost)
+    c18[18] = cost[20] * 18 / 20 * 0.99
+    assert _plan(1000, ks, c18, measured=True) == [20] * 50
+    # ... and 4% cheaper: they win even with the handicap (where they fit)
+    c18[18] = cost[20] * 18 / 20 * 0.96
+    plan = _plan(360, ks, c18, measured=True)
+    assert sum(plan) == 360 and plan.count(18) == 20
+    # table costs (not measured) get no handicap: 1% is enough
+    c18[18] = cost[20] * 18 / 20 * 0.99
+    plan = _plan(360, ks, c18, measured=False)
+    assert sum(plan) == 360 and plan.count(18) == 20
+    # full passes first, the remainder largest first
+    assert _plan(45, ks, cost, measured=True)[:2] == [20, 20]

@@ -384,3 +384,23 @@ def test_stencil2d_gt_halo_check_catches_a_corrupt_cell():
 def test_stencil2d_sycl_halo_check():
     out = run_app("mpi_stencil2d_sycl", "64", "1", "40", "--check", np=2).stdout
     assert re.search(r"# halo check dim:0 buf:1 \(mpi-host\): 0 bad ghost cells, 45 exchanges", out), out
+
+
+def test_mpi_stencil2d_gt_debug_lines():
+    """--debug: the reference DEBUG build's per-rank lines (missing
+    #2): "%d/%d exchange time %0.8f ms" and "%d/%d [%d:0x%08x] err_norm = %.8f"
+    after every test_deriv, "%d/%d allreduce time %0.8f ms" after every
+    test_sum (mpi_stencil2d_gt.cc:536-539,557-560,635-638)."""
+    import re
+    out = run_app("mpi_stencil2d_gt", "32", "3", "--n-other=128", "--no-managed", "--debug", np=2).stdout
+    exch = re.findall(r"^(\d+)/2 exchange time (\d+\.\d{8}) ms$", out, re.M)
+    errs = re.findall(r"^(\d+)/2 \[(\d+):0x([0-9a-f]{8})\] err_norm = (\d+\.\d{8})$", out, re.M)
+    alls = re.findall(r"^(\d+)/2 allreduce time (\d+\.\d{8}) ms$", out, re.M)
+    # 4 test_deriv (2 dims x buf 1/0) and 2 test_sum, each line once per rank
+    assert sorted(r for r, _ in exch) == ["0"] * 4 + ["1"] * 4, out
+    assert sorted(e[0] for e in errs) == ["0"] * 4 + ["1"] * 4 and all(float(e[3]) < 1e-5 for e in errs)
+    assert sorted(r for r, _ in alls) == ["0"] * 2 + ["1"] * 2
+    assert len(_TEST_RE.findall(out)) == 4 and len(_SUM_RE.findall(out)) == 2
+    # without --debug: no per-rank lines
+    plain = run_app("mpi_stencil2d_gt", "32", "3", "--n-other=128", "--no-managed", np=2).stdout
+    assert "exchange time" not in plain and "err_norm" not in plain
