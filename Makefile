@@ -67,7 +67,7 @@ $(OBJ)/kernels/%.o: csrc/kernels/%.hip $(KERNEL_HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJ)/runtime/%.o: csrc/runtime/%.cpp csrc/include/gmt/rt.h csrc/include/gmt/ccl.h
+$(OBJ)/runtime/%.o: csrc/runtime/%.cpp csrc/include/gmt/rt.h csrc/include/gmt/ccl.h csrc/include/gmt/numa_bind.hpp
 	@mkdir -p $(dir $@)
 	$(CXX) $(ROCM_HOST) -c $< -o $@
 
@@ -80,7 +80,7 @@ $(LIB_CCL): $(CCL_OBJ) $(LIB)
 	$(CXX) -shared -fPIC -o $@ $(CCL_OBJ) -Wl,-soname,libgmt_ccl.so \
 	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lrccl -lamdhip64
 
-$(OBJ)/host/%.o: csrc/host/%.cpp csrc/include/gmt/rt.h csrc/include/gmt/kernels.h csrc/include/gmt/ccl.h csrc/include/gmt/tb_geom.h
+$(OBJ)/host/%.o: csrc/host/%.cpp csrc/include/gmt/rt.h csrc/include/gmt/kernels.h csrc/include/gmt/ccl.h csrc/include/gmt/tb_geom.h csrc/include/gmt/numa_bind.hpp
 	@mkdir -p $(dir $@)
 	$(CXX) $(HOSTFLAGS) -c $< -o $@
 

@@ -45,7 +45,7 @@ int main(int argc, char** argv) {
   double start_time = 0, end_time = 0, k_start = 0, k_end = 0, g_start = 0, g_end = 0,
          b_start = 0, b_end = 0;
 
-  GMT_MPI_CHECK(MPI_Init(&argc, &argv));
+  mpi_init_pinned(&argc, &argv);  // pinned near the GPU first (gmt/device.hpp)
   int world_size = 1, world_rank = 0;
   MPI_Comm_size(MPI_COMM_WORLD, &world_size);
   MPI_Comm_rank(MPI_COMM_WORLD, &world_rank);

@@ -33,7 +33,7 @@ int main(int argc, char** argv) {
   const size_t lo = cli.positional(0) ? std::atoll(cli.positional(0)) : 16;
   const size_t hi = cli.positional(1) ? std::atoll(cli.positional(1)) : 64ull << 20;
   const int iters = cli.positional(2) ? std::atoi(cli.positional(2)) : 50;
-  GMT_MPI_CHECK(MPI_Init(&argc, &argv));
+  mpi_init_pinned(&argc, &argv);  // pinned near the GPU first (gmt/device.hpp)
   int world = 1, rank = 0;
   MPI_Comm_size(MPI_COMM_WORLD, &world);
   MPI_Comm_rank(MPI_COMM_WORLD, &rank);
@@ -42,6 +42,17 @@ int main(int argc, char** argv) {
   if (kind == comm::Kind::Auto && world == 1) kind = comm::Kind::Local;
   auto tr = comm::make_transport(comm::resolve(kind, b), MPI_COMM_WORLD, b);
   const int left = (rank + world - 1) % world, right = (rank + 1) % world;
+  {  // where every rank runs (gmt_rt_pin_rank; -1: not pinned): one header line
+    int cpu = b.pinned_cpu, node = b.numa_node;
+    std::vector<int> all(2 * static_cast<size_t>(world));
+    int mine[2] = {cpu, node};
+    MPI_Gather(mine, 2, MPI_INT, all.data(), 2, MPI_INT, 0, MPI_COMM_WORLD);
+    if (rank == 0) {
+      std::printf("# pinned cpu per rank:");
+      for (int r = 0; r < world; ++r) std::printf(" %d", all[2 * r]);
+      std::printf("\n");
+    }
+  }
   if (rank == 0)
     std::printf("# halo exchange sweep: %d ranks, transport=%s, backend=%s, ring neighbours, %d iters\n"
                 "# bytes_per_msg  msgs  us_median  us_min  GB/s_per_rank(sent+recv)  us_stream\n",

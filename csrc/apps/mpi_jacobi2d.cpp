@@ -79,7 +79,7 @@ int main(int argc, char** argv) {
   int64_t n = cli.positional(0) ? std::atoll(cli.positional(0)) : 8192;
   const int n_iter = cli.positional(1) ? std::atoi(cli.positional(1)) : 100;
   const int n_warmup = static_cast<int>(cli.geti("warmup", 10));
-  GMT_MPI_CHECK(MPI_Init(&argc, &argv));
+  mpi_init_pinned(&argc, &argv);  // pinned near the GPU first (gmt/device.hpp)
   int world = 1, rank = 0;
   MPI_Comm_size(MPI_COMM_WORLD, &world);
   MPI_Comm_rank(MPI_COMM_WORLD, &rank);

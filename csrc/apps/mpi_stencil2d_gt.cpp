@@ -62,7 +62,7 @@ int main(int argc, char** argv) {
   const std::string json = cli.get("json", "");
   const bool debug = cli.flag("debug");
 
-  GMT_MPI_CHECK(MPI_Init(&argc, &argv));
+  mpi_init_pinned(&argc, &argv);  // pinned near the GPU first (gmt/device.hpp)
   int world_size = 1, world_rank = 0;
   GMT_MPI_CHECK(MPI_Comm_size(MPI_COMM_WORLD, &world_size));
   GMT_MPI_CHECK(MPI_Comm_rank(MPI_COMM_WORLD, &world_rank));

@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
     n_iter = 1;
     n_warmup = 0;
   }
-  GMT_MPI_CHECK(MPI_Init(&argc, &argv));
+  mpi_init_pinned(&argc, &argv);  // pinned near the GPU first (gmt/device.hpp)
   int world_size = 1, world_rank = 0;
   MPI_Comm_size(MPI_COMM_WORLD, &world_size);
   MPI_Comm_rank(MPI_COMM_WORLD, &world_rank);

@@ -17,6 +17,7 @@
 #include <cstdlib>
 
 #include "gmt/mpi.hpp"
+#include "gmt/numa_bind.hpp"
 #include "gmt/watchdog.hpp"
 
 namespace gmt {
@@ -50,6 +51,28 @@ inline int get_node_count(MPI_Comm comm) {
   MPI_Allreduce(&leader, &nodes, 1, MPI_INT, MPI_SUM, comm);
   (void)lsize;
   return nodes > 0 ? nodes : 1;
+}
+
+// The core this process pinned itself to before MPI_Init (-1: not pinned
+// then).
+inline int& early_pinned_cpu() {
+  static int cpu = -1;
+  return cpu;
+}
+
+// MPI_Init with the rank pinned first (gmt_rt_pin_rank from the launcher's
+// local rank variables): MPI's shared-memory segments, touched during
+// MPI_Init, then land next to the core the rank runs on.  Pinning after
+// MPI_Init reliably gave the host-staged exchange's slow mode (7.3-7.6 GB/s
+// per rank against 15.1-15.3 unpinned, profiles/r06_pin/).  Without the
+// variables the rank is pinned by set_rank_device, after MPI_Init.
+inline void mpi_init_pinned(int* argc, char*** argv) {
+  int lr = 0, ls = 0, ndev = 0;
+  if (launcher_local_rank(&lr, &ls) && gmt_rt_device_count(&ndev) == 0 && ndev > 0) {
+    const int per = ls > ndev && ls % ndev == 0 ? ls / ndev : 1;
+    (void)gmt_rt_pin_rank(lr, ls, per, &early_pinned_cpu());
+  }
+  GMT_MPI_CHECK(MPI_Init(argc, argv));
 }
 
 // Select and set this rank's device.  print: emit the reference's
@@ -86,7 +109,10 @@ inline RankBinding set_rank_device(MPI_Comm comm, bool print) {
   // the GPU's socket: before any transport allocates its staging buffers
   GMT_CHECK("numa bind", gmt_rt_bind_numa(b.device, &b.numa_node));
   // one core near the GPU per rank, distinct per local rank (GMT_PIN=0: off)
-  GMT_CHECK("pin rank", gmt_rt_pin_rank(b.local_rank, b.local_size, b.ranks_per_device, &b.pinned_cpu));
+  if (early_pinned_cpu() >= 0)
+    b.pinned_cpu = early_pinned_cpu();
+  else
+    GMT_CHECK("pin rank", gmt_rt_pin_rank(b.local_rank, b.local_size, b.ranks_per_device, &b.pinned_cpu));
   watchdog_start(b.rank, b.device);
   watchdog_kick("device bound");
   return b;

@@ -146,7 +146,13 @@ inline int set_all_threads_affinity(const cpu_set_t& want) {
 inline int pin_rank_core(int local_rank, int local_size, const int* node_of_rank) {
   cpu_set_t allowed;
   if (local_rank < 0 || local_rank >= local_size || sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return -1;
-  const int node = node_of_rank[local_rank];
+  // GMT_PIN_NEAR=0 (A/B): consecutive cores from the start of the allowed
+  // set, whatever the GPU's node (what `mpirun -bind-to core` does)
+  static const bool near_only = [] {
+    const char* e = std::getenv("GMT_PIN_NEAR");
+    return !(e && e[0] == '0');
+  }();
+  const int node = near_only ? node_of_rank[local_rank] : -1;
   cpu_set_t cand = allowed;
   if (node >= 0) {
     cpu_set_t near, both;
@@ -155,7 +161,17 @@ inline int pin_rank_core(int local_rank, int local_size, const int* node_of_rank
       if (CPU_COUNT(&both) > 0) cand = both;
     }
   }
-  // physical cores of the candidates: the first allowed CPU of each sibling set
+  // physical cores of the candidates: the first allowed CPU of each SMT
+  // sibling set.  A sibling list wider than 4 is not an SMT group (a
+  // virtualised topology reported 32: pinning two ranks to "cores" 0 and 32
+  // put them 32 CPUs apart and halved the host-staged exchange,
+  // profiles/r06_pin/): each CPU is then a core of its own.
+  auto siblings = [](int c, cpu_set_t* sib) {
+    if (!cpu_siblings(c, sib) || CPU_COUNT(sib) > 4 || !CPU_ISSET(c, sib)) {
+      CPU_ZERO(sib);
+      CPU_SET(c, sib);
+    }
+  };
   int cores[CPU_SETSIZE];
   int nc = 0;
   cpu_set_t seen;
@@ -163,10 +179,7 @@ inline int pin_rank_core(int local_rank, int local_size, const int* node_of_rank
   for (int c = 0; c < CPU_SETSIZE; ++c) {
     if (!CPU_ISSET(c, &cand) || CPU_ISSET(c, &seen)) continue;
     cpu_set_t sib;
-    if (!cpu_siblings(c, &sib)) {
-      CPU_ZERO(&sib);
-      CPU_SET(c, &sib);
-    }
+    siblings(c, &sib);
     for (int s = 0; s < CPU_SETSIZE; ++s)
       if (CPU_ISSET(s, &sib)) CPU_SET(s, &seen);
     cores[nc++] = c;
@@ -174,16 +187,33 @@ inline int pin_rank_core(int local_rank, int local_size, const int* node_of_rank
   if (nc == 0) return -1;
   // this rank's index among the local ranks whose GPUs share its node
   int idx = 0;
-  for (int r = 0; r < local_rank; ++r) idx += node_of_rank[r] == node ? 1 : 0;
+  for (int r = 0; r < local_rank; ++r) idx += !near_only || node_of_rank[r] == node ? 1 : 0;
   const int core = cores[idx % nc];
   cpu_set_t want, sib;
-  if (!cpu_siblings(core, &sib)) {
-    CPU_ZERO(&sib);
-    CPU_SET(core, &sib);
-  }
+  siblings(core, &sib);
   CPU_AND(&want, &sib, &allowed);
   if (CPU_COUNT(&want) == 0 || CPU_EQUAL(&want, &allowed)) return -1;
   return set_all_threads_affinity(want) > 0 ? core : -1;
+}
+
+// This process's node-local rank and rank count as the launcher exported
+// them (hydra, Open MPI, torchrun, Slurm), for pinning BEFORE MPI_Init:
+// false when none is set.
+inline bool launcher_local_rank(int* rank, int* size) {
+  static const char* const kVars[][2] = {{"MPI_LOCALRANKID", "MPI_LOCALNRANKS"},
+                                         {"OMPI_COMM_WORLD_LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_SIZE"},
+                                         {"LOCAL_RANK", "LOCAL_WORLD_SIZE"},
+                                         {"SLURM_LOCALID", "SLURM_NTASKS_PER_NODE"}};
+  for (const auto& v : kVars) {
+    const char* r = std::getenv(v[0]);
+    const char* n = std::getenv(v[1]);
+    if (r && n && *r && *n) {
+      *rank = std::atoi(r);
+      *size = std::atoi(n);
+      return *size > 0 && *rank >= 0 && *rank < *size;
+    }
+  }
+  return false;
 }
 
 // GMT_PIN: "0" off, "1" on; unset: on for the GPU backend (default_on)
