@@ -10,7 +10,7 @@ import time
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from gpu_mpi_tests_amd.engine import NativeJacobi  # noqa: E402
 from gpu_mpi_tests_amd.parallel import dist as gd  # noqa: E402
 

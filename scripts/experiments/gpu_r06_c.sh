@@ -11,7 +11,7 @@ OUT=$R/gpurun_out/r06_c
 mkdir -p $OUT
 B=$R/build/bin/gmt_kernel_bench
 : > $OUT/rates.log
-for rep in 1 2; do
+for rep in $([ "${SWEEP:-1}" = 1 ] && echo 1 2); do
   for shp in "--jacobi-n=8192 --iters=200" "--jacobi-ny=8192 --jacobi-nx=16384 --iters=60" "--jacobi-ny=16384 --jacobi-nx=8192 --iters=60" "--jacobi-n=32768 --iters=20"; do
     for c in 1.8 2.1 2.4 2.8 3.3; do
       echo "== c$c $shp" >> $OUT/rates.log
@@ -19,7 +19,7 @@ for rep in 1 2; do
     done
   done
 done
-grep -E "^==|MLUPS" $OUT/rates.log | paste - - | awk '{print $2, $3, $4, $(NF-13), $(NF-5), $(NF-4), $(NF-3), $(NF-2)}'
+[ "${SWEEP:-1}" = 1 ] && grep -E "^==|MLUPS" $OUT/rates.log | paste - - | awk '{print $2, $3, $4, $(NF-13), $(NF-5), $(NF-4), $(NF-3), $(NF-2)}'
 cd $OUT
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace8192 -o t -- python3 $R/scripts/experiments/clock_ab.py 8192 1000 2 > $OUT/trace8192.log 2>&1 || { tail -20 $OUT/trace8192.log; exit 1; }
 grep "^n " $OUT/trace8192.log
