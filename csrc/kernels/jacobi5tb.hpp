@@ -273,6 +273,10 @@ __device__ __forceinline__ void keep_cells(dv<NC>& v, const dv<NC>& c, const uin
 #undef GMT_KEEP_ASM
 }
 
+#ifndef GMT_TB_SKIP_DEAD
+#define GMT_TB_SKIP_DEAD 1
+#endif
+
 // One wave = stage J of one strip: levels PB..PE of the K-level pipeline
 // (PB = J NL + 1, PE = (J + 1) NL).  Stage 0 takes level 0 from the DMA
 // ring; stage J > 0 from hand-off ring J - 1 (rows written by stage J - 1;
@@ -562,7 +566,27 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   };
 
   constexpr int kU = C::U;
-  for (int s0 = 0; s0 < nsteps; s0 += kU) {
+  // The first unrolled block of a later stage (J > 0) computes nothing of
+  // use: level p of step s holds walk row s - D - p, which the output cone
+  // needs only from row p on (rows [p, L + 2K - p) of level p), so every
+  // level PB..PE of this stage is dead for s < D + 2 PB — past the whole
+  // block at K >= 12 (19 <= 2 + 2 * 11 at K = 20).  That block only keeps
+  // the step barriers and, at its last step, reads the rows of step kU;
+  // the loop then starts at kU with the registers as at its usual start.
+  // (Its stores fall before the segment's output rows: dropped anyway; this
+  // stage issues no DMA, so no vmcnt accounting changes.  Round 6: the
+  // partly dead blocks compiled with their dead levels left out spilled the
+  // K = 20 kernels, 20-590 VGPRs.)  GMT_TB_SKIP_DEAD 0 (A/B builds): off.
+  constexpr bool kSkip0 = GMT_TB_SKIP_DEAD && !kIn && SYNC && kU <= D + 2 * PB;
+  int s_first = 0;
+  if constexpr (kSkip0) {
+    for (int s = 0; s < kU - 1; ++s) step_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    load_rows(kU);
+    asm volatile("s_barrier" ::: "memory");
+    s_first = kU;
+  }
+  for (int s0 = s_first; s0 < nsteps; s0 += kU) {
     static_for<0, kU>([&](auto Jc) { step(Jc, s0 + decltype(Jc)::value); });
     // A row band's output wave: once the unrolled block holding step
     // sig_step is done, the band's rows are written — visible device-wide,
