@@ -219,6 +219,13 @@ typedef struct gmt_tb_opts {
      clock[2] (device memory, zeroed by the caller): the clock the pass ran
      at is clock[0] / clock[1] x 100 MHz. */
   uint64_t* clock;
+  /* Shared hand-off groups (csrc/kernels/jacobi5tb.hpp Sh<K>): K = 12, 16,
+     20 passes of one rect at least a group wide (920 columns at K = 20),
+     with no push, signals or wg_waves, run as workgroups of four strips
+     whose stage-1 waves read windows of one shared hand-off row — 6% fewer
+     level updates per output at K = 20.  Bitwise the same field.  1 = on,
+     -1 = off, 0 = default (off unless GMT_TB_SHARED=1). */
+  int shared;
 } gmt_tb_opts;
 enum { GMT_PUSH_S = 0, GMT_PUSH_N = 1, GMT_PUSH_W = 2, GMT_PUSH_E = 3,
        GMT_PUSH_SW = 4, GMT_PUSH_SE = 5, GMT_PUSH_NW = 6, GMT_PUSH_NE = 7 };

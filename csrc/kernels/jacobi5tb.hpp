@@ -70,6 +70,52 @@ __host__ __device__ constexpr int64_t strip_lds() {
   return static_cast<int64_t>(C::RS) * C::ROW + static_cast<int64_t>(C::S - 1) * C::HS * C::ROW;
 }
 
+
+// Shared hand-off groups (SH: gmt_tb_opts.shared; one-rect passes without
+// signals).  A workgroup of NW adjacent two-stage strips writes its stage-0
+// output (level NL = K/2) into ONE hand-off row of the whole group instead
+// of one per strip, so a stage-1 wave can read any 256-column window of the
+// group's valid level-NL columns: each stage loses NL columns per side to
+// its own cone instead of the strip losing K.  Stage-0 windows are S0 =
+// 256 - 2 NL apart (their valid columns [NL, 256 - NL) abut, each column
+// written by exactly one wave: exec-masked hand-off stores), stage-1
+// windows start O (>= NL, a lane boundary) into the group and are S1 apart,
+// the last ending inside the group's valid columns.  K = 20: 4 strips,
+// 920 output columns per 8 waves against 4 x 216 = 864 for four separate
+// strips — 6% fewer level updates per output update.  The row is laid out
+// by 4-column groups g (lane l of a window starting at group g0 holds group
+// g0 + l): pair q of group g at byte q QS + 16 g, conflict-free for every
+// window offset.  NL even: every ownership boundary is a column pair.
+template <int K>
+struct Sh {
+  static constexpr int NW = 4;                             // strips per workgroup
+  static constexpr int NL = K / 2;                         // levels per stage
+  static constexpr bool kOk = tb_stages(K) == 2 && NL % 2 == 0;
+  static constexpr int S0 = 256 - 2 * NL;                  // stage-0 window spacing
+  static constexpr int O = (NL + 3) / 4 * 4;               // first stage-1 window, from the group's
+  static constexpr int S1 = (S0 * (NW - 1) - NL - O) / (NW - 1) / 4 * 4;  // stage-1 spacing
+  static constexpr int GOUT = S1 * (NW - 1) + 256 - 2 * NL;  // output columns of a group
+  static constexpr int ML = O + NL;                        // group window start -> output start
+  // column slot of the W / E ghost column in the first / last strip's
+  // windows of a pass whose rect is the interior (both stages alike: O, S0
+  // and S1 are multiples of 4)
+  static constexpr int kJW = (ML - 1) % 4;
+  static constexpr int kJE = (GOUT + ML) % 4;
+  static constexpr int NG = 256;                           // 4-column groups of a shared row
+  static constexpr uint32_t QS = NG * 16;                  // pair-plane stride (bytes)
+  static constexpr uint32_t ROWG = 2 * QS;                 // one shared row (bytes)
+  static_assert(!kOk || (S0 % 4 == 0 && S1 > 0 && S1 <= S0 && O + S1 * (NW - 1) + 256 <= S0 * (NW - 1) + 256 - NL),
+                "stage-1 windows inside the group's valid level-NL columns");
+  static_assert(!kOk || (S0 * (NW - 1) + 256) / 4 <= NG, "shared row holds the group");
+};
+
+// LDS of an SH workgroup: the shared hand-off ring, then NW DMA rings
+template <int K>
+__host__ __device__ constexpr int64_t sh_lds() {
+  using C = Cfg<K>;
+  return static_cast<int64_t>(C::HS) * Sh<K>::ROWG + static_cast<int64_t>(Sh<K>::NW) * C::RS * C::ROW;
+}
+
 struct Args {
   int64_t r[kMaxRect][4];        // output rects: x0, nx, y0, ny (absolute)
   int64_t nstrip[kMaxRect];      // strips per rect
@@ -110,6 +156,9 @@ struct Args {
   // over the XCDs, after each XCD's contiguous range of the other tiles
   // (tail_swizzle); 0: every tile XCD-contiguous in tile order
   int64_t edges_last;
+  int sh;                        // an SH launch (Sh<K> groups of nw = Sh<K>::NW strips)
+  int shmap;                     // SH: waves stage-major (GMT_TB_SH_MAP, A/B)
+  int col_keep;                  // SH: the one-column Dirichlet keep (GMT_TB_COL_KEEP=0: off, A/B)
   // column bands (gmt_tb_opts.signal_cols): rect cb_rect's first (cb_lo)
   // and last (cb_hi) strip groups — every segment at full length — are
   // dispatched before everything else of the rect, and each of their
@@ -215,6 +264,41 @@ __device__ __forceinline__ void lds_put(char* slot, int lane, const dv<NC>& v) {
   });
 }
 
+// SH rows: a lane's NC columns at p (its group's byte in the row), pair
+// plane q at p + q QS
+template <int NC, uint32_t QS>
+__device__ __forceinline__ dv<NC> lds_row_sh(const char* p) {
+  dv<NC> r;
+  static_for<0, NC / 2>([&](auto Q) {
+    constexpr int q = decltype(Q)::value;
+    const d2 a = *reinterpret_cast<const d2*>(p + q * QS);
+    r.c[2 * q] = a.x;
+    r.c[2 * q + 1] = a.y;
+  });
+  return r;
+}
+
+// SH stage-0 hand-off store: pair plane 0 under EXEC = m0, plane 1 under m1
+// (the lanes whose column pair this strip owns in the shared row; EXEC back
+// to all lanes after, and the s_nop for the SALU-writes-EXEC -> DPP hazard
+// of the next step's lane shifts, as keep_cells)
+template <int NC, uint32_t QS>
+__device__ __forceinline__ void lds_put_sh(char* p, const dv<NC>& v, uint64_t m0, uint64_t m1) {
+  static_assert(NC == 4, "four columns per lane");
+  const d2 lo = d2{v.c[0], v.c[1]}, hi = d2{v.c[2], v.c[3]};
+  typedef __attribute__((address_space(3))) char lds_char;
+  const uint32_t ad = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_char*)p));  // the LDS offset
+  asm volatile(
+      "s_mov_b64 exec, %[m0]\n\t"
+      "ds_write_b128 %[ad], %[lo]\n\t"
+      "s_mov_b64 exec, %[m1]\n\t"
+      "ds_write_b128 %[ad], %[hi] offset:%[qs]\n\t"
+      "s_mov_b64 exec, -1\n\t"
+      "s_nop 4" ::[ad] "v"(ad),
+      [lo] "v"(lo), [hi] "v"(hi), [m0] "s"(m0), [m1] "s"(m1), [qs] "i"(QS)
+      : "memory");
+}
+
 template <int NC>
 __device__ __forceinline__ dv<NC> dv_zero() {
   dv<NC> r;
@@ -273,6 +357,33 @@ __device__ __forceinline__ void keep_cells(dv<NC>& v, const dv<NC>& c, const uin
 #undef GMT_KEEP_ASM
 }
 
+// The Dirichlet keep of one ghost COLUMN (RULE >= 2 waves: a window that
+// holds exactly one fixed ghost column, in column slot RULE - 2 of the lane
+// in m, and no fixed row): one write under EXEC = that lane.  The columns
+// beyond the ghost one are garbage that nothing reads (the ghost column's
+// value depends on its own cell alone), so they need no keep.  Against
+// keep_cells' four writes and 7 SALU per level: 1 write and 2 SALU.  (All
+// four columns are operands, as in keep_cells: with the one column alone
+// the K = 20 stage-1 body spilled 17 VGPRs.)
+template <bool EXACT, int J, int NC>
+__device__ __forceinline__ void keep_col(dv<NC>& v, double c, uint64_t m) {
+  static_assert(NC == 4, "four columns per lane");
+#define GMT_KC(OP) asm("s_mov_b64 exec, %[m]\n\t" OP "\n\ts_mov_b64 exec, -1\n\ts_nop 4" \
+      : [v0] "+v"(v.c[0]), [v1] "+v"(v.c[1]), [v2] "+v"(v.c[2]), [v3] "+v"(v.c[3]) : [c] "v"(c), [m] "s"(m))
+  if constexpr (EXACT) {
+    if constexpr (J == 0) GMT_KC("v_mov_b64 %[v0], %[c]");
+    else if constexpr (J == 1) GMT_KC("v_mov_b64 %[v1], %[c]");
+    else if constexpr (J == 2) GMT_KC("v_mov_b64 %[v2], %[c]");
+    else GMT_KC("v_mov_b64 %[v3], %[c]");
+  } else {
+    if constexpr (J == 0) GMT_KC("v_mul_f64 %[v0], %[c], 4.0");
+    else if constexpr (J == 1) GMT_KC("v_mul_f64 %[v1], %[c], 4.0");
+    else if constexpr (J == 2) GMT_KC("v_mul_f64 %[v2], %[c], 4.0");
+    else GMT_KC("v_mul_f64 %[v3], %[c], 4.0");
+  }
+#undef GMT_KC
+}
+
 #ifndef GMT_TB_SKIP_DEAD
 #define GMT_TB_SKIP_DEAD 1
 #endif
@@ -291,10 +402,17 @@ __device__ __forceinline__ void keep_cells(dv<NC>& v, const dv<NC>& c, const uin
 // PUSH (inline halo exchange, output stage): bit 0 = this strip holds an x
 // face (W / E columns), bit 1 = this segment holds y-face rows (S / N); both:
 // the corner too.
-template <int K, int J, bool EXACT, bool EDGE, bool RULE, bool UP, int PUSH>
+// SH (shared hand-off group): cf is the wave's own window (stage-dependent),
+// ring + hdelta + 16 lane this lane's group in the shared hand-off ring
+// (stage 0 writes it under the ownership masks hm0 / hm1, stage 1 reads it;
+// a wave-uniform delta from the DMA ring's lane address, so both share one
+// address VGPR); otherwise cf = xs - KL and the hand-off rings are the
+// strip's own.
+template <int K, int J, bool EXACT, bool EDGE, int RULE, bool UP, int PUSH, bool SH>
 __device__ __forceinline__ void run_stage(const Args& a, const double* __restrict__ u, double* __restrict__ un,
                                           char* ring, int lane, int64_t xs, int64_t xe, int64_t ys, int64_t ye,
-                                          int nsteps, int sig_step, int xd) {
+                                          int nsteps, int sig_step, int xd, int64_t cf, int hdelta, uint64_t hm0,
+                                          uint64_t hm1) {
   using C = Cfg<K>;
   constexpr int NC = C::NC;
   constexpr int PB = J * C::NL + 1, PE = (J + 1) * C::NL;
@@ -321,7 +439,9 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   const double quarter = a.quarter;
   const int64_t dx0 = a.dom[0], dx1 = a.dom[0] + a.dom[1];
   const int64_t dy0 = a.dom[2], dy1 = a.dom[2] + a.dom[3];
-  const int64_t cf = xs - C::KL;        // first column of the strip window
+  static_assert(!SH || (Sh<K>::kOk && !EDGE && PUSH == 0 && !UP), "SH: one-rect passes, plain bodies");
+  constexpr uint32_t kQS = Sh<K>::QS, kRowG = Sh<K>::ROWG;
+  char* const hsh = ring + 16 * lane + hdelta;
   const int64_t c0 = cf + NC * lane;    // this lane: columns c0 .. c0+NC-1
   const int64_t yl = ys - K;            // the window's first row
   const int L = static_cast<int>(ye - ys);
@@ -343,14 +463,31 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   // the row's bytes [1024 q + 16 lane, +16)
   const uint32_t loff = static_cast<uint32_t>(cf) * 8u + static_cast<uint32_t>(lane) * (kPieces ? NC * 8u : 16u);
   constexpr uint32_t kPieceStride = kPieces ? 16u : 1024u;
+  // SH: one running row offset (the rows are requested in order, one per
+  // call) advanced by an opaque v_add, with the pieces in the immediate
+  // offset — the compiler otherwise keeps one offset VGPR per unrolled step
+  // (~19), which the SH stage-0 body cannot spare (K = 20: 6 VGPRs spilled)
+  uint32_t dmo = loff + dbase;
   auto dma = [&](int s, int slot) {
     if constexpr (kDma) {
       char* dst = ring + slot * kRow;
-      const uint32_t o = dbase + static_cast<uint32_t>(s) * rstep;
-      static_for<0, C::NDMA>([&](auto Q) {
-        constexpr uint32_t q = decltype(Q)::value;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + q * 1024u, 16, loff + q * kPieceStride + o, 0, 0, 0);
-      });
+      if constexpr (SH) {
+        (void)s;
+        static_for<0, C::NDMA>([&](auto Q) {
+          constexpr uint32_t q = decltype(Q)::value;
+          // (the immediate offset moves the LDS destination too: M0 is
+          // lowered by it)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + q * (1024u - kPieceStride), 16, dmo, 0,
+                                                   q * kPieceStride, 0);
+        });
+        asm volatile("v_add_u32 %0, %1, %0" : "+v"(dmo) : "s"(rstep));
+      } else {
+        const uint32_t o = dbase + static_cast<uint32_t>(s) * rstep;
+        static_for<0, C::NDMA>([&](auto Q) {
+          constexpr uint32_t q = decltype(Q)::value;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, dst + q * 1024u, 16, loff + q * kPieceStride + o, 0, 0, 0);
+        });
+      }
     }
   };
   //  stores: rows [ys, ye) from column xs.  The left output edge is a column
@@ -452,6 +589,11 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   uint64_t kxm[NC];
 #pragma unroll
   for (int j = 0; j < NC; ++j) kxm[j] = __builtin_amdgcn_ballot_w64(kept_col(c0 + j));
+  // RULE >= 2: the one ghost column's lane (tb_block: slot RULE - 2)
+  constexpr int kColSlot = RULE >= 2 ? RULE - 2 : 0;
+  static_assert(RULE < 2 || kColSlot < NC, "column slot");
+  const int64_t gcol = !gw && cf <= dx0 - 1 && dx0 - 1 < cf + C::COLS ? dx0 - 1 : dx1;
+  const uint64_t kcm = RULE >= 2 ? __builtin_amdgcn_ballot_w64(c0 + kColSlot == gcol) : 0;
 
   // fixed ring rows, in walk coordinates t = +-(row - yanchor) (- bottom-up;
   // the walk's rows: t = s - D - p for level p of step s): kept iff t < tlo
@@ -480,7 +622,9 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
       if constexpr (EXACT) v.c[j] = quarter * ((l + r) + (up_.c[j] + dn.c[j]));
       else v.c[j] = (l + r) + (up_.c[j] + dn.c[j]);
     });
-    if constexpr (RULE) {
+    if constexpr (RULE >= 2) {
+      keep_col<EXACT, kColSlot, NC>(v, c.c[kColSlot], kcm);
+    } else if constexpr (RULE == 1) {
       // a kept cell: V_p = V_{p-1} (exact) / 4 V_{p-1} (scaled levels),
       // written under EXEC = the lanes to keep: all lanes on a fixed ring
       // row, the ring-column lanes otherwise (none in most levels of most
@@ -526,9 +670,15 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
       r1 = lds_row<NC>(ring + ((s + kRS - 1) % kRS) * kRow, lane);
       r2 = lds_row<NC>(ring + (s % kRS) * kRow, lane);
     } else {
-      r0 = lds_row<NC>(hand_rd + ((s + kHS - 4) % kHS) * kRow, lane);
-      r1 = lds_row<NC>(hand_rd + ((s + kHS - 3) % kHS) * kRow, lane);
-      r2 = lds_row<NC>(hand_rd + ((s + kHS - 2) % kHS) * kRow, lane);
+      if constexpr (SH) {
+        r0 = lds_row_sh<NC, kQS>(hsh + ((s + kHS - 4) % kHS) * kRowG);
+        r1 = lds_row_sh<NC, kQS>(hsh + ((s + kHS - 3) % kHS) * kRowG);
+        r2 = lds_row_sh<NC, kQS>(hsh + ((s + kHS - 2) % kHS) * kRowG);
+      } else {
+        r0 = lds_row<NC>(hand_rd + ((s + kHS - 4) % kHS) * kRow, lane);
+        r1 = lds_row<NC>(hand_rd + ((s + kHS - 3) % kHS) * kRow, lane);
+        r2 = lds_row<NC>(hand_rd + ((s + kHS - 2) % kHS) * kRow, lane);
+      }
     }
   };
   load_rows(0);
@@ -553,6 +703,8 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
         for (int q = 0; q < NC; ++q) v.c[q] = __builtin_amdgcn_ldexp(v.c[q], -2 * K);  // exact power-of-two unscale
       }
       store_step(s, v);  // issued every step (warm-up rows are out of range)
+    } else if constexpr (SH) {
+      lds_put_sh<NC, kQS>(hsh + (s % kHS) * kRowG, v, hm0, hm1);
     } else {
       lds_put<NC>(hand_wr + (s % kHS) * kRow, lane, v);
     }
@@ -612,7 +764,7 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
 // A workgroup = nw adjacent strips of one segment row, S waves per strip
 // (adjacent strips share their overlap columns in the CU's L1 / the XCD's
 // L2).  S == 1: every wave is independent (no barrier).
-template <int K, bool EXACT, bool EDGE, bool PUSH>
+template <int K, bool EXACT, bool EDGE, bool PUSH, bool SH>
 __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict__ u, double* __restrict__ un,
                                          int64_t t) {
   using C = Cfg<K>;
@@ -620,7 +772,10 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   extern __shared__ d2 lds_dyn[];
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
-  const int sl = wave / G, stage = wave % G;  // strip of the workgroup, stage of the strip
+  // strip of the workgroup, stage of the strip (SH with Args::shmap: stage
+  // major, wave w = strip w % NW's stage w / NW)
+  const bool smaj = SH && a.shmap;
+  const int sl = smaj ? wave % a.nw : wave / G, stage = smaj ? wave / a.nw : wave % G;
   int k = 0;
   while (k + 1 < a.n && t >= a.tstart[k + 1]) ++k;
   const int64_t lt = t - a.tstart[k];
@@ -718,14 +873,65 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   }
   constexpr int64_t wout = C::WOUT;
   const int64_t rx0 = a.r[k][0], rx1 = a.r[k][0] + a.r[k][1];
-  int64_t xs = rx0 + strip * wout;
-  if (xs + wout > rx1) xs = rx1 - wout > rx0 ? rx1 - wout : rx0;  // last strip: shifted left to end at rx1
-  const int64_t xe = xs + wout < rx1 ? xs + wout : rx1;
+  int64_t xs, xe, cf;  // output columns [xs, xe) of this wave's strip, its window's first column
+  char* ring;          // the strip's DMA ring (and, not SH, its hand-off rings)
+  int hdelta = 0;      // SH: the shared hand-off ring's lane address - the DMA ring's
+  uint64_t hm0 = 0, hm1 = 0;
+  if constexpr (SH) {
+    // group gi: output [gx, gx + GOUT), the last one shifted left to end at
+    // rx1 (launch_tb: the rect is at least GOUT wide); stage 0 of strip sl
+    // reads window ga + S0 sl, stage 1 window ga + O + S1 sl and stores its
+    // slice of the group's output
+    using H = Sh<K>;
+    int64_t gx = rx0 + gi * H::GOUT;
+    if (gx + H::GOUT > rx1) gx = rx1 - H::GOUT;
+    const int64_t ga = gx - H::ML;
+    char* const lds = reinterpret_cast<char*>(lds_dyn);
+    ring = lds + C::HS * H::ROWG + sl * (C::RS * C::ROW);
+    int64_t off;
+    if (stage == 0) {
+      off = H::S0 * sl;
+      xs = ga + off;
+      xe = xs;  // stores nothing
+      // the level-NL columns this strip owns in the shared row: [NL, NL + S0)
+      // of its window (from 0 / to 256 for the first / last strip)
+      const int lo = sl == 0 ? 0 : H::NL, hi = sl == H::NW - 1 ? 256 : H::NL + H::S0;
+      const int c = 4 * lane;
+      hm0 = __builtin_amdgcn_ballot_w64(c >= lo && c + 1 < hi);
+      hm1 = __builtin_amdgcn_ballot_w64(c + 2 >= lo && c + 3 < hi);
+    } else {
+      off = H::O + H::S1 * sl;
+      xs = gx + H::S1 * sl;
+      xe = sl < H::NW - 1 ? xs + H::S1 : gx + H::GOUT;
+    }
+    cf = ga + off;
+    // this lane's group in the shared row: off / 4 + lane, 16 B per group and plane
+    hdelta = static_cast<int>(4 * off - (ring - lds));
+  } else {
+    xs = rx0 + strip * wout;
+    if (xs + wout > rx1) xs = rx1 - wout > rx0 ? rx1 - wout : rx0;  // last strip: shifted left to end at rx1
+    xe = xs + wout < rx1 ? xs + wout : rx1;
+    cf = xs - C::KL;
+    ring = reinterpret_cast<char*>(lds_dyn) + sl * strip_lds<K>();
+  }
   // the rule path only where a computed cell can be a fixed ring cell
-  const int64_t cx0 = xs - C::KL, cx1 = cx0 + C::COLS;
+  const int64_t cx0 = cf, cx1 = cx0 + C::COLS;
   const bool rule = (cx0 < a.dom[0] && !(a.mask & 1)) || (cx1 > a.dom[0] + a.dom[1] && !(a.mask & 2)) ||
                     (ys - K < a.dom[2] && !(a.mask & 4)) || (ye + K > a.dom[2] + a.dom[3] && !(a.mask & 8));
-  char* ring = reinterpret_cast<char*>(lds_dyn) + sl * strip_lds<K>();
+  // SH: a rule wave whose window holds one ghost column (a W / E Dirichlet
+  // side) and no fixed row runs the one-column keep (RULE 2 + the ghost's
+  // column slot — compile-time for the usual rect = interior pass, so only
+  // those two bodies are built; other slots take the general rule)
+  int rule_kind = rule ? 1 : 0;
+  if constexpr (SH) {
+    const bool ry = (ys - K < a.dom[2] && !(a.mask & 4)) || (ye + K > a.dom[2] + a.dom[3] && !(a.mask & 8));
+    const int64_t gw0 = a.dom[0] - 1, ge0 = a.dom[0] + a.dom[1];
+    const bool hw = !(a.mask & 1) && cx0 <= gw0 && gw0 < cx1, he = !(a.mask & 2) && cx0 <= ge0 && ge0 < cx1;
+    if (rule && !ry && hw != he && a.col_keep) {
+      const int jslot = static_cast<int>(((hw ? gw0 : ge0) - cx0) & 3);
+      if (jslot == Sh<K>::kJW || jslot == Sh<K>::kJE) rule_kind = 2 + jslot;
+    }
+  }
   // one instantiation per (stage, rule path, direction); the direction is
   // bottom-up only for the N row bands
   // the x face this strip pushes (PUSH): the first strip holds the W one,
@@ -747,8 +953,8 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   auto go = [&](auto jc, auto rule_c, auto up_c, int sstep) {
     constexpr int j = decltype(jc)::value;
     auto run = [&](auto push_c) {
-      run_stage<K, j, EXACT, EDGE, decltype(rule_c)::value, decltype(up_c)::value, decltype(push_c)::value>(
-          a, u, un, ring, lane, xs, xe, ys, ye, nsteps, sstep, xd);
+      run_stage<K, j, EXACT, EDGE, decltype(rule_c)::value, decltype(up_c)::value, decltype(push_c)::value, SH>(
+          a, u, un, ring, lane, xs, xe, ys, ye, nsteps, sstep, xd, cf, hdelta, hm0, hm1);
     };
     using P0 = std::integral_constant<int, 0>;
     if constexpr (PUSH && j == G - 1) {
@@ -762,12 +968,26 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
     }
   };
   auto stage_go = [&](auto jc, int sstep) {
-    if (!PUSH && dir < 0) {  // (no row bands in an inline-halo pass)
-      if (rule) go(jc, T{}, T{}, sstep);
-      else go(jc, F{}, T{}, sstep);
+    if constexpr (!SH) {
+      if (!PUSH && dir < 0) {  // (no row bands in an inline-halo pass)
+        if (rule) go(jc, std::integral_constant<int, 1>{}, T{}, sstep);
+        else go(jc, std::integral_constant<int, 0>{}, T{}, sstep);
+        return;
+      }
+    }
+    // (an SH pass has no row bands: top-down bodies only)
+    using R0 = std::integral_constant<int, 0>;
+    using R1 = std::integral_constant<int, 1>;
+    if constexpr (SH) {
+      using RW = std::integral_constant<int, 2 + Sh<K>::kJW>;
+      using RE = std::integral_constant<int, 2 + Sh<K>::kJE>;
+      if (rule_kind == 0) go(jc, R0{}, F{}, sstep);
+      else if (rule_kind == RW::value) go(jc, RW{}, F{}, sstep);
+      else if (rule_kind == RE::value && RE::value != RW::value) go(jc, RE{}, F{}, sstep);
+      else go(jc, R1{}, F{}, sstep);
     } else {
-      if (rule) go(jc, T{}, F{}, sstep);
-      else go(jc, F{}, F{}, sstep);
+      if (rule) go(jc, R1{}, F{}, sstep);
+      else go(jc, R0{}, F{}, sstep);
     }
   };
   if constexpr (G == 1) {
@@ -816,7 +1036,7 @@ inline bool tail_swizzle_ok(int64_t nb, int64_t ne) {
   return true;
 }
 
-template <int K, bool EXACT, bool EDGE, bool PUSH>
+template <int K, bool EXACT, bool EDGE, bool PUSH, bool SH>
 __global__ __launch_bounds__(kMaxThreads) __attribute__((amdgpu_waves_per_eu(2)))
 void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__ un, int64_t nblocks) {
   if constexpr (PUSH) {
@@ -832,7 +1052,8 @@ void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__
   // atomics here cost a one-round 8192^2 pass 1.6%, profiles/r06_clock/),
   // the deltas go out by vector atomics once the workgroup's work is done
   extern __shared__ d2 lds_dyn[];
-  uint64_t* stamp = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(lds_dyn) + a.nw * strip_lds<K>());
+  uint64_t* stamp = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(lds_dyn) +
+                                                (SH ? sh_lds<K>() : a.nw * strip_lds<K>()));
   const bool clk = a.clk && (b & 255) == 128 && threadIdx.x == 0;
   if (clk) {
     stamp[0] = __builtin_amdgcn_s_memtime();
@@ -845,7 +1066,7 @@ void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__
 #if GMT_TB_WG_TRACE
   const uint64_t wg_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  tb_block<K, EXACT, EDGE, PUSH>(a, u, un, t);
+  tb_block<K, EXACT, EDGE, PUSH, SH>(a, u, un, t);
   if (clk) {
     const uint64_t m1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     __hip_atomic_fetch_add(a.clk, m1 - stamp[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -926,6 +1147,18 @@ inline double tb_rule_cost() {
   return c;
 }
 
+// The step cost of a wave running the one-column Dirichlet keep (SH x-side
+// rule waves: one write and 2 SALU per level, ~1.06x the VALU of a plain
+// wave) relative to a plain one.  GMT_TB_RULE_COL_COST=c overrides it.
+inline double tb_rule_col_cost() {
+  static const double c = [] {
+    const char* e = std::getenv("GMT_TB_RULE_COL_COST");
+    const double v = e ? std::atof(e) : 0.0;
+    return v >= 1.0 && v <= 4.0 ? v : 1.15;
+  }();
+  return c;
+}
+
 // The step cost of a wave running the inline-halo body (three face store
 // groups per step, the ones out of range dropped) relative to a plain one:
 // a one-round pass whose push waves had plain-length segments ran
@@ -973,9 +1206,12 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
   // push body (pushed face), out[0..3] = W, E, S, N
   auto side_cost = [&](int k, double* out) {
     const int64_t ry0 = a.r[k][2], ry1 = ry0 + a.r[k][3], rx0 = a.r[k][0], rx1 = rx0 + a.r[k][1];
-    const bool rule[4] = {rx0 - Cfg<K>::KL < a.dom[0] && !(a.mask & 1), rx1 + Cfg<K>::KL > a.dom[0] + a.dom[1] && !(a.mask & 2),
+    const int64_t kl = a.sh ? Sh<K>::ML : Cfg<K>::KL;  // window columns left of the first output column
+    const bool rule[4] = {rx0 - kl < a.dom[0] && !(a.mask & 1), rx1 + kl > a.dom[0] + a.dom[1] && !(a.mask & 2),
                           ry0 - K < a.dom[2] && !(a.mask & 4), ry1 + K > a.dom[2] + a.dom[3] && !(a.mask & 8)};
-    for (int d = 0; d < 4; ++d) out[d] = (rule[d] ? fr : 1.0) * ((push_sides >> d) & 1 ? fp : 1.0);
+    // (SH: the x sides' interior segments run the one-column keep)
+    const double frx = a.sh && a.col_keep ? tb_rule_col_cost() : fr;
+    for (int d = 0; d < 4; ++d) out[d] = (rule[d] ? (d < 2 ? frx : fr) : 1.0) * ((push_sides >> d) & 1 ? fp : 1.0);
   };
   bool long_edges = false;
   auto fill = [&](int64_t L0, int64_t* wgs) {
@@ -1191,7 +1427,7 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
 // Fills the kernel arguments and the launch shape; info (optional) gets
 // {workgroups, resident workgroups, threads per workgroup, rows per interior
 // segment and interior segments of the first rect, VGPRs per lane}.
-template <int K, bool EXACT, bool EDGE, bool PUSH>
+template <int K, bool EXACT, bool EDGE, bool PUSH, bool SH>
 int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int64_t* dom, int mask, const double* u,
               double* un, int64_t ld, int64_t nrows, hipStream_t s, int64_t* info = nullptr) {
   using C = Cfg<K>;
@@ -1199,6 +1435,21 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   constexpr int kMaxStrips = tb_max_strips(K);
   Args a{};
   a.nw = std::min(o.wg_waves > 0 ? o.wg_waves : tb_default_strips(K), kMaxStrips);  // multi-stage: one strip (profiles/r02_tb4/launch_shapes.txt)
+  if constexpr (SH) {
+    static_assert(Sh<K>::kOk && !EDGE && !PUSH, "SH launches: plain two-stage bodies");
+    a.nw = Sh<K>::NW;
+    a.sh = 1;
+    static const int shmap = [] {
+      const char* e = std::getenv("GMT_TB_SH_MAP");
+      return e ? std::atoi(e) : 0;
+    }();
+    static const int col_keep = [] {
+      const char* e = std::getenv("GMT_TB_COL_KEEP");
+      return e ? std::atoi(e) : 1;
+    }();
+    a.shmap = shmap != 0;
+    a.col_keep = col_keep != 0;
+  }
   a.ld = ld;
   a.last_row = nrows - 1;
   a.mask = mask;
@@ -1224,13 +1475,14 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
         (dom[1] + C::WOUT - 1) / C::WOUT < 2)
       return static_cast<int>(hipErrorInvalidValue);
   }
-  constexpr int64_t wout = C::WOUT;
+  constexpr int64_t wout = SH ? Sh<K>::GOUT : C::WOUT;  // SH: a group's columns
   int64_t maxh = 0;
   for (int k = 0; k < n_rect; ++k) {
     const int64_t* r = rects + 4 * k;
     if (r[1] <= 0 || r[3] <= 0) continue;
+    if (SH && r[1] < wout) return static_cast<int>(hipErrorInvalidValue);  // (dispatch_k checks it)
     for (int j = 0; j < 4; ++j) a.r[a.n][j] = r[j];
-    a.nstrip[a.n] = (r[1] + wout - 1) / wout;
+    a.nstrip[a.n] = SH ? Sh<K>::NW * ((r[1] + wout - 1) / wout) : (r[1] + wout - 1) / wout;
     maxh = std::max(maxh, r[3]);
     ++a.n;
   }
@@ -1245,9 +1497,9 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   if (lmax < 1) return static_cast<int>(hipErrorInvalidValue);
   (void)maxh;
   // + 16 B: the clock record's start stamps (jacobi5tb_kernel)
-  const size_t smem = static_cast<size_t>(a.nw * strip_lds<K>()) + 16;
+  const size_t smem = static_cast<size_t>(SH ? sh_lds<K>() : a.nw * strip_lds<K>()) + 16;
   if (smem > 65536) {  // above the default dynamic-LDS limit (gfx950 has 160 KB per CU)
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE, PUSH>),
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE, PUSH, SH>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem));
     if (e != hipSuccess) return static_cast<int>(e);
   }
@@ -1255,14 +1507,14 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   // queried once per device, kernel and strips-per-workgroup (an idempotent
   // cache: a process driving several devices keeps one entry per device)
   constexpr int kMaxDev = 64;
-  static std::atomic<int> resident[kMaxDev][kMaxThreads / kWave + 1] = {};
+  static std::atomic<int> resident[kMaxDev][2][kMaxThreads / kWave + 1] = {};
   int dev = 0;
   (void)hipGetDevice(&dev);
-  std::atomic<int>* slot = dev >= 0 && dev < kMaxDev ? &resident[dev][a.nw] : nullptr;
+  std::atomic<int>* slot = dev >= 0 && dev < kMaxDev ? &resident[dev][SH ? 1 : 0][a.nw] : nullptr;
   int per_cu = slot ? slot->load(std::memory_order_relaxed) : 0;
   if (per_cu <= 0) {
     int occ = 0, cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE, PUSH>),
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE, PUSH, SH>),
                                                      a.nw * G * kWave, smem) != hipSuccess || occ < 1)
       occ = 1;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1289,7 +1541,7 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   // search costs milliseconds; the engine launches the same passes over and over)
   SegPlan sp;
   {
-    std::vector<int64_t> key = {a.n, a.nw, a.mask, o.seg_rows, lmax, per_cu, sig_rects, rbk, rbs + rbn, rb_min, push_sides};
+    std::vector<int64_t> key = {a.n, a.nw, a.mask, o.seg_rows, lmax, per_cu, sig_rects, rbk, rbs + rbn, rb_min, push_sides, SH};
     for (int k = 0; k < a.n; ++k) key.insert(key.end(), a.r[k], a.r[k] + 4);
     key.insert(key.end(), a.dom, a.dom + 4);
     static std::mutex mu;
@@ -1381,7 +1633,7 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   a.clk = o.clock;
   if (info) {
     hipFuncAttributes fa{};
-    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE, PUSH>));
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE, PUSH, SH>));
     const int64_t v[6] = {nb, per_cu, a.nw * G * kWave, a.lmid[0], a.nmid[0], fa.numRegs};
     for (int j = 0; j < 6; ++j) info[j] = v[j];
     return 0;
@@ -1403,7 +1655,7 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     a.wg_trace = trace_buf;
   }
 #endif
-  jacobi5tb_kernel<K, EXACT, EDGE, PUSH><<<grid_1d(nb), a.nw * G * kWave, smem, s>>>(a, u, un, nb);
+  jacobi5tb_kernel<K, EXACT, EDGE, PUSH, SH><<<grid_1d(nb), a.nw * G * kWave, smem, s>>>(a, u, un, nb);
 #if GMT_TB_WG_TRACE
   if (tracing) {
     std::vector<uint64_t> h(static_cast<size_t>(nb) * 4);
@@ -1435,9 +1687,40 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
 namespace gmt {
 namespace tb {
 
+// An SH launch (Sh<K>: stage-1 windows over a shared hand-off row) for a
+// pass of one rect at least a group wide, with no inline halo, completion
+// signals or explicit workgroup shape.  gmt_tb_opts.shared: 1 on, -1 off,
+// 0 the default — off unless GMT_TB_SHARED=1 (A/B).
+template <int K>
+bool sh_launch(const gmt_tb_opts& o, int n_rect, const int64_t* rects) {
+  if constexpr (!Sh<K>::kOk) {
+    return false;
+  } else {
+    static const bool env_on = [] {
+      const char* e = std::getenv("GMT_TB_SHARED");
+      return e && std::atoi(e) != 0;
+    }();
+    if (!(o.shared > 0 || (o.shared == 0 && env_on))) return false;
+    if (o.push_w > 0 || o.wg_waves > 0 || o.signal_rects > 0 || o.signal_rows > 0 || (o.signal_cols & 3)) return false;
+    int n = 0;
+    for (int k = 0; k < n_rect; ++k) {
+      const int64_t* r = rects + 4 * k;
+      if (r[1] <= 0 || r[3] <= 0) continue;
+      if (r[1] < Sh<K>::GOUT) return false;
+      ++n;
+    }
+    return n == 1;
+  }
+}
+
 template <int K>
 int dispatch_k(const gmt_tb_opts& o, bool exact, int n_rect, const int64_t* rects, const int64_t* dom, int mask,
                const double* u, double* un, int64_t ld, int64_t nrows, hipStream_t s, int64_t* info) {
+  if constexpr (Sh<K>::kOk) {
+    if (sh_launch<K>(o, n_rect, rects))
+      return exact ? launch_tb<K, true, false, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
+                   : launch_tb<K, false, false, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
+  }
   // a rect narrower than a strip whose width is odd ends inside a lane pair:
   // that lane stores column 0 or 2 alone (wider rects end on a lane
   // boundary: their last strip is shifted to end at the rect's edge)
@@ -1448,17 +1731,17 @@ int dispatch_k(const gmt_tb_opts& o, bool exact, int n_rect, const int64_t* rect
   if (o.push_w > 0) {  // inline halo exchange: no odd-edge stores (checked in launch_tb)
     if constexpr (tb_push_built(K)) {
       if (edge) return static_cast<int>(hipErrorInvalidValue);
-      return exact ? launch_tb<K, true, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
-                   : launch_tb<K, false, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
+      return exact ? launch_tb<K, true, false, true, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
+                   : launch_tb<K, false, false, true, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
     } else {
       return static_cast<int>(hipErrorInvalidValue);
     }
   }
   if (edge)
-    return exact ? launch_tb<K, true, true, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
-                 : launch_tb<K, false, true, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
-  return exact ? launch_tb<K, true, false, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
-               : launch_tb<K, false, false, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
+    return exact ? launch_tb<K, true, true, false, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
+                 : launch_tb<K, false, true, false, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
+  return exact ? launch_tb<K, true, false, false, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
+               : launch_tb<K, false, false, false, false>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
 }
 
 }  // namespace tb

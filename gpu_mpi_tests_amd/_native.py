@@ -73,6 +73,7 @@ class TbOpts(ctypes.Structure):
         ("push_w", c_int),
         ("stop", c_vp),
         ("clock", c_vp),
+        ("shared", c_int),
     ]
 
 _SIGS = {

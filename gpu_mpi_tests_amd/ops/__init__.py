@@ -19,6 +19,7 @@ from .kernels import (  # noqa: F401
     jacobi5_rects,
     jacobi5xk,
     jacobi5tb,
+    jacobi5tb_plan,
     tb_supported,
     stencil5_1d,
     stencil5_2d,

@@ -349,7 +349,7 @@ def _check_xk_bounds(k: int, u: torch.Tensor, un: torch.Tensor, rects) -> None:
 
 def jacobi5tb(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, int, int, int]],
               dom: tuple[int, int, int, int], halo_mask: int = 0, *, wg_waves: int = 0, seg_rows: int = 0,
-              exact: bool = False, push: "dict | None" = None, push_w: int = 0) -> None:
+              exact: bool = False, push: "dict | None" = None, push_w: int = 0, shared: int = 0) -> None:
     """``k`` fused Laplace sweeps per memory pass with the temporal-blocking kernel
     (csrc/kernels/jacobi5tb.hip): ``un = J^k(u)`` on up to 8 output rects (absolute
     coordinates, each with its k-wide ring inside the array); the rest of ``un``
@@ -361,7 +361,8 @@ def jacobi5tb(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[i
     levels.  ``push`` ({direction: tensor}, directions "S" "N" "W" "E" "SW" "SE"
     "NW" "NE") with ``push_w``: the inline halo exchange (gmt_tb_opts.push) —
     the output's face cells are also stored into each tensor at the same
-    coordinates (a tensor with ``un``'s row pitch)."""
+    coordinates (a tensor with ``un``'s row pitch).  ``shared``: the shared hand-off
+    group launch (gmt_tb_opts.shared: 1 on, -1 off, 0 default = on where it applies)."""
     rects = [tuple(int(v) for v in r) for r in rects if r[1] > 0 and r[3] > 0]
     if not tb_supported(k):
         raise ValueError(f"jacobi5tb: {k} sweeps per pass is not built (1..10 or even 12..{TB_MAX_SWEEPS})")
@@ -379,6 +380,7 @@ def jacobi5tb(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[i
     arr = (ctypes.c_int64 * (4 * len(rects)))(*[v for r in rects for v in r])
     d = (ctypes.c_int64 * 4)(*[int(v) for v in dom])
     o = _native.TbOpts(int(k), int(wg_waves), int(seg_rows), int(bool(exact)))
+    o.shared = int(shared)
     if push:
         order = ("S", "N", "W", "E", "SW", "SE", "NW", "NE")
         for dirn, t in push.items():
@@ -390,6 +392,26 @@ def jacobi5tb(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[i
                                   ctypes.cast(d, ctypes.c_void_p), int(halo_mask), u.data_ptr(),
                                   un.data_ptr(), u.stride(0), u.shape[0], _stream(u)),
                   "gmt_jacobi5tb")
+
+
+def jacobi5tb_plan(k: int, rects: Sequence[tuple[int, int, int, int]], dom: tuple[int, int, int, int],
+                   halo_mask: int, ld: int, nrows: int, *, wg_waves: int = 0, seg_rows: int = 0,
+                   shared: int = 0) -> dict:
+    """The launch :func:`jacobi5tb` would make (gmt_jacobi5tb_plan), without
+    launching: workgroups, resident workgroups, threads per workgroup (512 for
+    a shared hand-off group launch), interior segment rows and count, VGPRs."""
+    L = _native.lib()
+    rects = [tuple(int(v) for v in r) for r in rects]
+    arr = (ctypes.c_int64 * (4 * len(rects)))(*[v for r in rects for v in r])
+    d = (ctypes.c_int64 * 4)(*[int(v) for v in dom])
+    o = _native.TbOpts(int(k), int(wg_waves), int(seg_rows), 0)
+    o.shared = int(shared)
+    info = (ctypes.c_int64 * 6)()
+    _native.check(L.gmt_jacobi5tb_plan(ctypes.byref(o), len(rects), ctypes.cast(arr, ctypes.c_void_p),
+                                       ctypes.cast(d, ctypes.c_void_p), int(halo_mask), int(ld), int(nrows),
+                                       ctypes.cast(info, ctypes.c_void_p)), "gmt_jacobi5tb_plan")
+    keys = ("workgroups", "resident", "threads", "seg_rows", "segments", "vgprs")
+    return dict(zip(keys, (int(v) for v in info)))
 
 
 def jacobi5xk(k: int, u: torch.Tensor, un: torch.Tensor, rects: Sequence[tuple[int, int, int, int]],
