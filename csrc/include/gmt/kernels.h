@@ -224,7 +224,8 @@ typedef struct gmt_tb_opts {
      with no push, signals or wg_waves, run as workgroups of four strips
      whose stage-1 waves read windows of one shared hand-off row — 6% fewer
      level updates per output at K = 20.  Bitwise the same field.  1 = on,
-     -1 = off, 0 = default (off unless GMT_TB_SHARED=1). */
+     -1 = off, 0 = default: rects whose x sides both exchange halos, or
+     larger than 2^28 points (GMT_TB_SHARED=1 / 0 forces it on / off). */
   int shared;
 } gmt_tb_opts;
 enum { GMT_PUSH_S = 0, GMT_PUSH_N = 1, GMT_PUSH_W = 2, GMT_PUSH_E = 3,

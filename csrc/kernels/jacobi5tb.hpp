@@ -1439,9 +1439,14 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     static_assert(Sh<K>::kOk && !EDGE && !PUSH, "SH launches: plain two-stage bodies");
     a.nw = Sh<K>::NW;
     a.sh = 1;
+    // stage-major waves: each SIMD then holds one stage-0 and one stage-1
+    // wave (the dispatcher deals a workgroup's waves to the SIMDs in turn);
+    // strip-major put both stage-1 waves — stores and unscale on top of the
+    // levels — on the same SIMDs: 32768^2 5.0M against 4.8M MLUPS
+    // (profiles/r06_shared/)
     static const int shmap = [] {
       const char* e = std::getenv("GMT_TB_SH_MAP");
-      return e ? std::atoi(e) : 0;
+      return e ? std::atoi(e) : 1;
     }();
     static const int col_keep = [] {
       const char* e = std::getenv("GMT_TB_COL_KEEP");
@@ -1690,23 +1695,29 @@ namespace tb {
 // An SH launch (Sh<K>: stage-1 windows over a shared hand-off row) for a
 // pass of one rect at least a group wide, with no inline halo, completion
 // signals or explicit workgroup shape.  gmt_tb_opts.shared: 1 on, -1 off,
-// 0 the default — off unless GMT_TB_SHARED=1 (A/B).
+// 0 the default (GMT_TB_SHARED=1 / 0 forces it on / off).
 template <int K>
-bool sh_launch(const gmt_tb_opts& o, int n_rect, const int64_t* rects) {
+bool sh_launch(const gmt_tb_opts& o, int n_rect, const int64_t* rects, int mask) {
   if constexpr (!Sh<K>::kOk) {
     return false;
   } else {
-    static const bool env_on = [] {
+    // GMT_TB_SHARED: 1 on wherever it applies, 0 off, unset: the default
+    static const int env = [] {
       const char* e = std::getenv("GMT_TB_SHARED");
-      return e && std::atoi(e) != 0;
+      return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
     }();
-    if (!(o.shared > 0 || (o.shared == 0 && env_on))) return false;
+    if (o.shared < 0 || (o.shared == 0 && env == 0)) return false;
     if (o.push_w > 0 || o.wg_waves > 0 || o.signal_rects > 0 || o.signal_rows > 0 || (o.signal_cols & 3)) return false;
     int n = 0;
     for (int k = 0; k < n_rect; ++k) {
       const int64_t* r = rects + 4 * k;
       if (r[1] <= 0 || r[3] <= 0) continue;
       if (r[1] < Sh<K>::GOUT) return false;
+      // the default: a rect whose x sides both exchange halos, or a large
+      // one (32768^2 Dirichlet: +5%).  Smaller Dirichlet rects lose 1-2% to
+      // their boundary groups in one-round launches (8192^2, the N = 8
+      // shares; profiles/r06_shared/)
+      if (o.shared == 0 && env < 0 && !((mask & 3) == 3 || r[1] * r[3] > (int64_t(1) << 28))) return false;
       ++n;
     }
     return n == 1;
@@ -1717,7 +1728,7 @@ template <int K>
 int dispatch_k(const gmt_tb_opts& o, bool exact, int n_rect, const int64_t* rects, const int64_t* dom, int mask,
                const double* u, double* un, int64_t ld, int64_t nrows, hipStream_t s, int64_t* info) {
   if constexpr (Sh<K>::kOk) {
-    if (sh_launch<K>(o, n_rect, rects))
+    if (sh_launch<K>(o, n_rect, rects, mask))
       return exact ? launch_tb<K, true, false, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
                    : launch_tb<K, false, false, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
   }
