@@ -124,16 +124,22 @@ int main(int argc, char** argv) {
              {8192, 16384, 0, 1024},  {16384, 8192, 0, 1024},   {8192, 16384, 5, 1024}, {16384, 8192, 6, 1024}};
   constexpr int K = 20;
   using C = Cfg<K>;
-  for (const Case& c : cases) {
+  // GMT_PLAN_SH=1: the shared hand-off group launch (Sh<K>, one 8-wave
+  // workgroup per CU: 256 slots unless given)
+  const bool sh = std::getenv("GMT_PLAN_SH") && std::atoi(std::getenv("GMT_PLAN_SH")) != 0;
+  for (Case c : cases) {
+    if (sh && c.resident == 1024) c.resident = 256;
     Args a{};
-    a.nw = 1;
+    a.nw = sh ? Sh<K>::NW : 1;
+    a.sh = sh ? 1 : 0;
+    a.col_keep = 1;
     a.n = 1;
     const int64_t x0 = 24, y0 = K;
     a.r[0][0] = x0;
     a.r[0][1] = c.nx;
     a.r[0][2] = y0;
     a.r[0][3] = c.ny;
-    a.nstrip[0] = (c.nx + C::WOUT - 1) / C::WOUT;
+    a.nstrip[0] = sh ? Sh<K>::NW * ((c.nx + Sh<K>::GOUT - 1) / Sh<K>::GOUT) : (c.nx + C::WOUT - 1) / C::WOUT;
     a.dom[0] = x0;
     a.dom[1] = c.nx;
     a.dom[2] = y0;
@@ -143,7 +149,7 @@ int main(int argc, char** argv) {
     const int64_t lmax = std::min<int64_t>(1 << 20, (int64_t(1) << 31) / (ld * 8) - 3 * K - C::LAG - 2 * C::U - C::P);
     const char* ps = std::getenv("GMT_PLAN_PUSH");
     const SegPlan p = plan_segments<K>(a, 0, lmax, c.resident, 0, -1, 0, 0, ps ? std::atoi(ps) : 0);
-    const int64_t g = a.nstrip[0], nb = g < 2 ? g : 2;
+    const int64_t g = (a.nstrip[0] + a.nw - 1) / a.nw, nb = g < 2 ? g : 2;
     const int64_t wgs = g * ((p.e0[0] > 0) + (p.e1[0] > 0)) + nb * p.nmid_b[0] + (g - nb) * p.nmid[0];
     std::printf("%6lld x %6lld mask %2d: edges %lld / %lld rows, interior %lld x %lld rows, rule groups %lld x %lld rows, "
                 "%lld workgroups on %lld slots%s\n",

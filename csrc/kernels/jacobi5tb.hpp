@@ -157,7 +157,8 @@ struct Args {
   // (tail_swizzle); 0: every tile XCD-contiguous in tile order
   int64_t edges_last;
   int sh;                        // an SH launch (Sh<K> groups of nw = Sh<K>::NW strips)
-  int shmap;                     // SH: waves stage-major (GMT_TB_SH_MAP, A/B)
+  int shmap;                     // waves stage-major (SH: GMT_TB_SH_MAP, default on; several
+                                 // two-stage strips per workgroup: GMT_TB_STRIP_MAP, A/B)
   int col_keep;                  // SH: the one-column Dirichlet keep (GMT_TB_COL_KEEP=0: off, A/B)
   // column bands (gmt_tb_opts.signal_cols): rect cb_rect's first (cb_lo)
   // and last (cb_hi) strip groups — every segment at full length — are
@@ -772,9 +773,9 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   extern __shared__ d2 lds_dyn[];
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
-  // strip of the workgroup, stage of the strip (SH with Args::shmap: stage
-  // major, wave w = strip w % NW's stage w / NW)
-  const bool smaj = SH && a.shmap;
+  // strip of the workgroup, stage of the strip (Args::shmap: stage major,
+  // wave w = strip w % nw's stage w / nw)
+  const bool smaj = G > 1 && a.shmap;
   const int sl = smaj ? wave % a.nw : wave / G, stage = smaj ? wave / a.nw : wave % G;
   int k = 0;
   while (k + 1 < a.n && t >= a.tstart[k + 1]) ++k;
@@ -1435,6 +1436,13 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   constexpr int kMaxStrips = tb_max_strips(K);
   Args a{};
   a.nw = std::min(o.wg_waves > 0 ? o.wg_waves : tb_default_strips(K), kMaxStrips);  // multi-stage: one strip (profiles/r02_tb4/launch_shapes.txt)
+  if constexpr (!SH && G > 1) {
+    static const int strip_map = [] {
+      const char* e = std::getenv("GMT_TB_STRIP_MAP");
+      return e ? std::atoi(e) : 0;
+    }();
+    a.shmap = strip_map != 0;
+  }
   if constexpr (SH) {
     static_assert(Sh<K>::kOk && !EDGE && !PUSH, "SH launches: plain two-stage bodies");
     a.nw = Sh<K>::NW;
