@@ -154,8 +154,10 @@ int gmt_jacobi5_rects(int n_rect, const int64_t* rects, const double* u, double*
 #define GMT_TB_MAX_SWEEPS 20
 typedef struct gmt_tb_opts {
   int sweeps;   /* K, see gmt_jacobi5tb_supported */
-  int wg_waves; /* 256-column strips per workgroup, 1..8 (0 = default; at
-                   most 4 when K > 10) */
+  int wg_waves; /* 256-column strips per workgroup, 1..8 (0 = default: four
+                   one-stage strips for K <= 10; for K > 10 one two-stage
+                   strip, two (stage-major waves) for a one-rect pass
+                   larger than 2^28 points; at most 4 when K > 10) */
   int seg_rows; /* output rows per strip segment (0 = default: short edge
                    segments where a rect touches a Dirichlet row, interior
                    segments sized to fill the device's resident workgroups) */

@@ -1437,11 +1437,28 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   Args a{};
   a.nw = std::min(o.wg_waves > 0 ? o.wg_waves : tb_default_strips(K), kMaxStrips);  // multi-stage: one strip (profiles/r02_tb4/launch_shapes.txt)
   if constexpr (!SH && G > 1) {
+    // several two-stage strips per workgroup: stage-major waves (all the
+    // stage-0 waves first) — 32768^2 with two strips 5.24-5.25M MLUPS
+    // against 4.91-4.93M for one strip per workgroup, same box
+    // (profiles/r06_shared/ab_p.txt).  A large one-rect pass (more than
+    // 2^28 points: several rounds) defaults to two strips; one-round passes
+    // keep one (the N = 8 shares lost up to 9% with two).  GMT_TB_STRIP_MAP=0
+    // keeps strip-major waves and one strip (A/B).
     static const int strip_map = [] {
       const char* e = std::getenv("GMT_TB_STRIP_MAP");
-      return e ? std::atoi(e) : 0;
+      return e ? std::atoi(e) : 1;
     }();
-    a.shmap = strip_map != 0;
+    if (strip_map != 0 && !PUSH && o.wg_waves == 0 && o.seg_rows == 0 && o.signal_rects == 0 &&
+        o.signal_rows == 0 && (o.signal_cols & 3) == 0) {
+      int64_t nonempty = 0, area = 0;
+      for (int k = 0; k < n_rect; ++k)
+        if (rects[4 * k + 1] > 0 && rects[4 * k + 3] > 0) {
+          ++nonempty;
+          area = rects[4 * k + 1] * rects[4 * k + 3];
+        }
+      if (nonempty == 1 && area > (int64_t(1) << 28)) a.nw = 2;
+    }
+    a.shmap = strip_map != 0 && a.nw > 1;
   }
   if constexpr (SH) {
     static_assert(Sh<K>::kOk && !EDGE && !PUSH, "SH launches: plain two-stage bodies");
@@ -1721,11 +1738,12 @@ bool sh_launch(const gmt_tb_opts& o, int n_rect, const int64_t* rects, int mask)
       const int64_t* r = rects + 4 * k;
       if (r[1] <= 0 || r[3] <= 0) continue;
       if (r[1] < Sh<K>::GOUT) return false;
-      // the default: a rect whose x sides both exchange halos, or a large
-      // one (32768^2 Dirichlet: +5%).  Smaller Dirichlet rects lose 1-2% to
-      // their boundary groups in one-round launches (8192^2, the N = 8
-      // shares; profiles/r06_shared/)
-      if (o.shared == 0 && env < 0 && !((mask & 3) == 3 || r[1] * r[3] > (int64_t(1) << 28))) return false;
+      // the default: a rect whose x sides both exchange halos (+2-3% on
+      // the one-round N = 8 shares, +7% at 32768^2).  With a Dirichlet x
+      // side the boundary groups (every strip waits for the rule strip at
+      // each step) cost it the gain: two-strip workgroups win at 32768^2
+      // and one-strip ones elsewhere (launch_tb; profiles/r06_shared/)
+      if (o.shared == 0 && env < 0 && (mask & 3) != 3) return false;
       ++n;
     }
     return n == 1;
