@@ -159,7 +159,7 @@ struct Args {
   int sh;                        // an SH launch (Sh<K> groups of nw = Sh<K>::NW strips)
   int shmap;                     // waves stage-major (SH: GMT_TB_SH_MAP, default on; several
                                  // two-stage strips per workgroup: GMT_TB_STRIP_MAP, A/B)
-  int col_keep;                  // SH: the one-column Dirichlet keep (GMT_TB_COL_KEEP=0: off, A/B)
+  int col_keep;                  // the one-column Dirichlet keep (GMT_TB_COL_KEEP=0: off, A/B)
   // column bands (gmt_tb_opts.signal_cols): rect cb_rect's first (cb_lo)
   // and last (cb_hi) strip groups — every segment at full length — are
   // dispatched before everything else of the rect, and each of their
@@ -919,18 +919,25 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   const int64_t cx0 = cf, cx1 = cx0 + C::COLS;
   const bool rule = (cx0 < a.dom[0] && !(a.mask & 1)) || (cx1 > a.dom[0] + a.dom[1] && !(a.mask & 2)) ||
                     (ys - K < a.dom[2] && !(a.mask & 4)) || (ye + K > a.dom[2] + a.dom[3] && !(a.mask & 8));
-  // SH: a rule wave whose window holds one ghost column (a W / E Dirichlet
+  // A rule wave whose window holds one ghost column (a W / E Dirichlet
   // side) and no fixed row runs the one-column keep (RULE 2 + the ghost's
   // column slot — compile-time for the usual rect = interior pass, so only
   // those two bodies are built; other slots take the general rule)
   int rule_kind = rule ? 1 : 0;
-  if constexpr (SH) {
+  // the ghost columns' slots (SH: Sh<K>; a per-strip window starts KL, a
+  // multiple of 4, left of its first output column: W ghost in slot 3, E
+  // ghost 256 - KL right of the last strip's window start, slot 0)
+  // (SH only: in the per-strip K = 20 kernel the two extra bodies spilled
+  // 12-14 VGPRs)
+  constexpr bool kColBodies = SH;
+  constexpr int kJW = SH ? Sh<K>::kJW : 3, kJE = SH ? Sh<K>::kJE : 0;
+  if constexpr (kColBodies) {
     const bool ry = (ys - K < a.dom[2] && !(a.mask & 4)) || (ye + K > a.dom[2] + a.dom[3] && !(a.mask & 8));
     const int64_t gw0 = a.dom[0] - 1, ge0 = a.dom[0] + a.dom[1];
     const bool hw = !(a.mask & 1) && cx0 <= gw0 && gw0 < cx1, he = !(a.mask & 2) && cx0 <= ge0 && ge0 < cx1;
     if (rule && !ry && hw != he && a.col_keep) {
       const int jslot = static_cast<int>(((hw ? gw0 : ge0) - cx0) & 3);
-      if (jslot == Sh<K>::kJW || jslot == Sh<K>::kJE) rule_kind = 2 + jslot;
+      if (jslot == kJW || jslot == kJE) rule_kind = 2 + jslot;
     }
   }
   // one instantiation per (stage, rule path, direction); the direction is
@@ -979,9 +986,9 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
     // (an SH pass has no row bands: top-down bodies only)
     using R0 = std::integral_constant<int, 0>;
     using R1 = std::integral_constant<int, 1>;
-    if constexpr (SH) {
-      using RW = std::integral_constant<int, 2 + Sh<K>::kJW>;
-      using RE = std::integral_constant<int, 2 + Sh<K>::kJE>;
+    if constexpr (kColBodies) {
+      using RW = std::integral_constant<int, 2 + kJW>;
+      using RE = std::integral_constant<int, 2 + kJE>;
       if (rule_kind == 0) go(jc, R0{}, F{}, sstep);
       else if (rule_kind == RW::value) go(jc, RW{}, F{}, sstep);
       else if (rule_kind == RE::value && RE::value != RW::value) go(jc, RE{}, F{}, sstep);
@@ -1210,8 +1217,8 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
     const int64_t kl = a.sh ? Sh<K>::ML : Cfg<K>::KL;  // window columns left of the first output column
     const bool rule[4] = {rx0 - kl < a.dom[0] && !(a.mask & 1), rx1 + kl > a.dom[0] + a.dom[1] && !(a.mask & 2),
                           ry0 - K < a.dom[2] && !(a.mask & 4), ry1 + K > a.dom[2] + a.dom[3] && !(a.mask & 8)};
-    // (SH: the x sides' interior segments run the one-column keep)
-    const double frx = a.sh && a.col_keep ? tb_rule_col_cost() : fr;
+    // (the x sides' interior segments run the one-column keep)
+    const double frx = a.col_keep ? tb_rule_col_cost() : fr;
     for (int d = 0; d < 4; ++d) out[d] = (rule[d] ? (d < 2 ? frx : fr) : 1.0) * ((push_sides >> d) & 1 ? fp : 1.0);
   };
   bool long_edges = false;
@@ -1436,6 +1443,11 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   constexpr int kMaxStrips = tb_max_strips(K);
   Args a{};
   a.nw = std::min(o.wg_waves > 0 ? o.wg_waves : tb_default_strips(K), kMaxStrips);  // multi-stage: one strip (profiles/r02_tb4/launch_shapes.txt)
+  static const int col_keep = [] {
+    const char* e = std::getenv("GMT_TB_COL_KEEP");
+    return e ? std::atoi(e) : 1;
+  }();
+  a.col_keep = col_keep != 0 && SH;
   if constexpr (!SH && G > 1) {
     // several two-stage strips per workgroup: stage-major waves (all the
     // stage-0 waves first) — 32768^2 with two strips 5.24-5.25M MLUPS
@@ -1473,12 +1485,7 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
       const char* e = std::getenv("GMT_TB_SH_MAP");
       return e ? std::atoi(e) : 1;
     }();
-    static const int col_keep = [] {
-      const char* e = std::getenv("GMT_TB_COL_KEEP");
-      return e ? std::atoi(e) : 1;
-    }();
     a.shmap = shmap != 0;
-    a.col_keep = col_keep != 0;
   }
   a.ld = ld;
   a.last_row = nrows - 1;

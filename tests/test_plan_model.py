@@ -41,3 +41,21 @@ def test_tail_swizzle_is_a_permutation():
     p = subprocess.run([_tool(), "--check-swizzle"], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-3000:]
     assert " 0 of " in p.stdout
+
+
+def test_shared_group_plans():
+    """Shared hand-off group launches (GMT_PLAN_SH=1: four strips per
+    8-wave workgroup, 920 output columns per group at K = 20, one workgroup
+    per CU): the x-halo shapes the launcher gives them fit their 256 slots
+    in one round where the per-strip plan does, and the 32768^2 plan runs
+    several rounds with its edge segments last."""
+    env = dict(os.environ, GMT_PLAN_SH="1")
+    p = subprocess.run([_tool(), "8192", "8192", "15", "1024", "8192", "16384", "15", "1024",
+                        "32768", "32768", "0", "1024"], capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 0, p.stdout + p.stderr
+    lines = p.stdout.strip().splitlines()
+    assert len(lines) == 3, p.stdout
+    for ln in lines[:2]:
+        wgs = int(ln.split(" workgroups on ")[0].rsplit(" ", 1)[1])
+        assert "on 256 slots" in ln and 200 <= wgs <= 256, ln
+    assert "edges last" in lines[2] and "on 256 slots" in lines[2], lines[2]
