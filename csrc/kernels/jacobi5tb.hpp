@@ -1460,7 +1460,7 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
       const char* e = std::getenv("GMT_TB_STRIP_MAP");
       return e ? std::atoi(e) : 1;
     }();
-    if (strip_map != 0 && !PUSH && o.wg_waves == 0 && o.seg_rows == 0 && o.signal_rects == 0 &&
+    if (strip_map != 0 && o.wg_waves == 0 && o.seg_rows == 0 && o.signal_rects == 0 &&
         o.signal_rows == 0 && (o.signal_cols & 3) == 0) {
       int64_t nonempty = 0, area = 0;
       for (int k = 0; k < n_rect; ++k)

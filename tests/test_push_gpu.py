@@ -71,6 +71,31 @@ def test_push_faces_kernel(k, ny, nx, dirs, w):
         assert torch.equal(got, want), (d, int((got != want).sum()))
 
 
+@pytest.mark.parametrize("k", [12, 16, 20])
+@pytest.mark.parametrize("wg", [2, 3])
+@pytest.mark.parametrize("dirs", [DIRS, ("W", "E"), ("N", "E", "NE", "SE")])
+def test_push_faces_kernel_multi_strip(k, wg, dirs):
+    """Several two-stage strips per workgroup with stage-major waves (the
+    default shape of push passes over 2^28 points, the N = 2 shares): face
+    strips share their workgroup's step barriers with plain ones."""
+    ny, nx, w, g, xo = 333, 1100, 20, k, 24
+    gen = torch.Generator(device="cpu").manual_seed(ny + nx + k + wg)
+    u = torch.rand(ny + 2 * g, xo + nx + g + 5, generator=gen, dtype=torch.float64).to(DEV)
+    dom = (xo, nx, g, ny)
+    un = torch.full_like(u, 7.0)
+    tg = {d: torch.full_like(u, 3.0) for d in dirs}
+    ops.jacobi5tb(k, u, un, [dom], dom, 15, push=tg, push_w=w, wg_waves=wg)
+    exp = torch.full(u.shape, 7.0, dtype=torch.float64)
+    ref.jacobi5xk(k, u.cpu(), exp, [dom], dom, 15)
+    torch.cuda.synchronize()
+    assert torch.equal(un.cpu(), exp), (un.cpu() - exp).abs().max()
+    for d, t in tg.items():
+        want = torch.full(u.shape, 3.0, dtype=torch.float64)
+        ys, xs = _face(d, dom, w)
+        want[ys, xs] = exp[ys, xs]
+        assert torch.equal(t.cpu(), want), d
+
+
 def test_push_refuses_what_it_cannot_do():
     """Odd face width, several rects, a rect other than the interior, a
     domain too short for two segments, both x faces on one strip."""
