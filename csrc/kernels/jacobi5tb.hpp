@@ -1663,7 +1663,12 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     const int64_t groups = (a.nstrip[0] + a.nw - 1) / a.nw, nbnd = groups < 2 ? groups : 2;
     a.sig_dispatch = groups * ((sp.e0[0] > 0) + (sp.e1[0] > 0)) + nbnd * sp.nmid_b[0];
   }
-  a.prio = nb <= per_cu ? 1 : 0;
+  // GMT_TB_PRIO=0 / 1: never / always (A/B); default: one-round launches
+  static const int prio_mode = [] {
+    const char* e = std::getenv("GMT_TB_PRIO");
+    return e ? std::atoi(e) : -1;
+  }();
+  a.prio = prio_mode >= 0 ? (prio_mode > 0 ? 1 : 0) : (nb <= per_cu ? 1 : 0);
   a.sig_count = o.signal_count;
   a.signal = o.signal;
   a.stop = PUSH ? o.stop : nullptr;
