@@ -149,12 +149,16 @@ asan-host:
 # tuning harnesses (standalone, not part of the libraries): stream_sweep, and
 # variant_bench — the A/B kernel variants checked and timed against libgmt
 sweep: $(BUILD)/bench/stream_sweep $(BUILD)/bench/variant_bench $(BUILD)/bench/d1_walk $(BUILD)/bench/sdma_probe \
-       $(BUILD)/bench/plan_model
+       $(BUILD)/bench/plan_model $(BUILD)/bench/wave_place
 # the segment planner on the host (no GPU): plan_model [ny nx mask [resident]] ...
 $(BUILD)/bench/plan_model: csrc/bench/plan_model.hip $(KERNEL_HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -Icsrc/include -Icsrc/kernels --cuda-host-only -o $@ $<
 $(BUILD)/bench/sdma_probe: csrc/bench/sdma_probe.hip
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+# where the dispatcher puts a workgroup's waves: wave_place [strips_per_wg] [lds_kb_per_strip]
+$(BUILD)/bench/wave_place: csrc/bench/wave_place.hip
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 $(BUILD)/bench/stream_sweep: csrc/bench/stream_sweep.hip
