@@ -1477,10 +1477,9 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     a.nw = Sh<K>::NW;
     a.sh = 1;
     // stage-major waves: each SIMD then holds one stage-0 and one stage-1
-    // wave (the dispatcher deals a workgroup's waves to the SIMDs in turn);
-    // strip-major put both stage-1 waves — stores and unscale on top of the
-    // levels — on the same SIMDs: 32768^2 5.0M against 4.8M MLUPS
-    // (profiles/r06_shared/)
+    // wave (the dispatcher deals a workgroup's waves to consecutive SIMDs,
+    // build/bench/wave_place); strip-major put two stage-0 or two stage-1
+    // waves on every SIMD: 32768^2 5.0M against 4.8M MLUPS (profiles/r06_shared/)
     static const int shmap = [] {
       const char* e = std::getenv("GMT_TB_SH_MAP");
       return e ? std::atoi(e) : 1;
