@@ -135,7 +135,8 @@ def bench_native(env, shape, steps, warmup, overlap, dims, graph, tblock, wg_wav
             "exact": eng.exact, "max_abs_u0": eng.max_abs_u0, "pass_cost_ms": eng.pass_cost_ms(),
             "transport": (eng.transport + (" inline halo" if eng.push_active else "")
                           if env.world_size > 1 else "none"),
-            "halo_bytes_per_rank": eng.halo_bytes, "dims": (eng.py, eng.px)}
+            "halo_bytes_per_rank": eng.halo_bytes, "dims": (eng.py, eng.px),
+            "tb_launch": eng.tb_launch(eng.tsteps) if eng.tblock and eng.tsteps > 1 else None}
     return eng, dt, info
 
 
@@ -616,6 +617,7 @@ def result_record(args, env, shape, mlups, ms_per_step, info, dims):
             "init": args.init,
             "max_abs_u0": info.get("max_abs_u0"),
             "pass_cost_ms": info.get("pass_cost_ms"),
+            "tb_launch": info.get("tb_launch"),
             "transport": info["transport"],
             "halo_bytes_per_rank": info["halo_bytes_per_rank"],
             "device": str(env.device),

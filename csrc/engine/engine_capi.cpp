@@ -213,6 +213,9 @@ int gmt_engine_jacobi_info(void* p, int64_t* out) {
   out[15] = s.push_active();
   return 0;
 }
+int gmt_engine_jacobi_tb_info(void* p, int K, int64_t* out) {
+  return static_cast<Handle*>(p)->s->tb_launch_info(K, out);
+}
 int gmt_engine_jacobi_plan(void* p, int steps, int* out, int max) {
   const std::vector<int> plan = static_cast<Handle*>(p)->s->plan_passes(steps);
   for (int i = 0; i < static_cast<int>(plan.size()) && i < max; ++i) out[i] = plan[i];

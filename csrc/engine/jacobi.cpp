@@ -612,6 +612,20 @@ void JacobiSolver::push_block(int parity, int K) {
   fresh_[parity ^ 1] = true;
 }
 
+int JacobiSolver::tb_launch_info(int K, int64_t out[6]) const {
+  const int64_t dom[4] = {xo_, nx_, yo_, ny_};
+  gmt_tb_opts o{};
+  o.sweeps = K;
+  o.wg_waves = cfg_.wg_waves;
+  o.seg_rows = cfg_.seg_rows;
+  o.exact = exact_ ? 1 : 0;
+  if (push_on_) {
+    for (int d = 0; d < 8; ++d) o.push[d] = push_base_[parity_][d];
+    o.push_w = g_;
+  }
+  return gmt_jacobi5tb_plan(&o, 1, dom, dom, halo_mask(), ld_, ny_ + 2 * g_, out);
+}
+
 bool JacobiSolver::band_mode(int K) const {
   int64_t rects[4];
   int cols = 0, rows = 0;

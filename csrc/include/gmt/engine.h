@@ -61,6 +61,9 @@ int gmt_engine_jacobi_info(void* h, int64_t* out);
 /* The fused passes (sweeps per pass, in launch order) that run(steps) enqueues:
  * writes min(n, max) entries, returns n. */
 int gmt_engine_jacobi_plan(void* h, int steps, int* out, int max);
+/* The launch of the rank's one-rect K-sweep pass (gmt_jacobi5tb_plan's
+ * info[6]); returns its error code. */
+int gmt_engine_jacobi_tb_info(void* h, int K, int64_t* out);
 /* Launch one pass of every pass type run(steps) will use, then restore the
  * initial field (first-launch costs stay out of a timed run). */
 int gmt_engine_jacobi_prepare(void* h, int steps);

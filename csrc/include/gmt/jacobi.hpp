@@ -123,6 +123,11 @@ class JacobiSolver {
   // the CPU backend), samples, seconds sampled}.  GMT_CLOCK=0: no stamps.
   void clock_reset();
   void clock_read(double out[3]);
+  // The launch of this rank's one-rect K-sweep pass (the serial or inline-
+  // halo pass over the interior), without launching: gmt_jacobi5tb_plan's
+  // {workgroups, resident workgroups, threads per workgroup, segment rows,
+  // segments, VGPRs}.  Returns its error code (0: ok).
+  int tb_launch_info(int K, int64_t out[6]) const;
 
   int64_t nx() const { return nx_; }
   int64_t ny() const { return ny_; }

@@ -96,6 +96,8 @@ def load(device: str = "cuda") -> ctypes.CDLL:
     lib.gmt_engine_jacobi_residual.restype = ctypes.c_double
     lib.gmt_engine_jacobi_info.argtypes = [vp, ctypes.POINTER(i64)]
     lib.gmt_engine_jacobi_info.restype = c_int
+    lib.gmt_engine_jacobi_tb_info.argtypes = [vp, c_int, ctypes.POINTER(i64)]
+    lib.gmt_engine_jacobi_tb_info.restype = c_int
     lib.gmt_engine_jacobi_plan.argtypes = [vp, c_int, ctypes.POINTER(c_int), c_int]
     lib.gmt_engine_jacobi_plan.restype = c_int
     lib.gmt_engine_jacobi_prepare.argtypes = [vp, c_int]
@@ -402,6 +404,25 @@ class NativeJacobi:
         if self.lib.gmt_engine_jacobi_compare(self.h, other.h, out):
             raise EngineError("gmt_engine_jacobi_compare failed")
         return float(out[0]), int(out[1])
+
+    def tb_launch(self, k: int) -> dict:
+        """The launch shape of this rank's one-rect k-sweep pass
+        (gmt_jacobi5tb_plan, nothing launched): workgroups, resident slots,
+        threads per workgroup, segment rows and count, VGPRs; ``shape`` names
+        it — for two-stage strips 128 threads are one strip per workgroup,
+        256 two stage-major strips, 512 a shared hand-off group (default
+        wg_waves) — csrc/kernels/jacobi5tb.hpp launch_tb / sh_launch."""
+        out = (ctypes.c_int64 * 6)()
+        rc = self.lib.gmt_engine_jacobi_tb_info(self.h, int(k), out)
+        if rc != 0:
+            return {"error": int(rc)}
+        keys = ("workgroups", "resident", "threads", "seg_rows", "segments", "vgprs")
+        d = dict(zip(keys, (int(v) for v in out)))
+        if k > 10 and d["threads"] in (128, 256, 512):
+            d["shape"] = {128: "one two-stage strip per workgroup",
+                          256: "two two-stage strips per workgroup, stage-major waves",
+                          512: "shared hand-off group: four strips, stage-major waves"}[d["threads"]]
+        return d
 
     def clock_reset(self) -> None:
         """Zero the fused passes' shader-clock record (stream ordered)."""

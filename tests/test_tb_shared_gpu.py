@@ -94,3 +94,21 @@ def test_shared_not_for_narrow_or_push():
     u, dom = _field(k, 40, 2000, seed=1, xo=k)
     assert _plan(k, u, dom, 0, 1, wg_waves=2)["threads"] == 256
     assert _plan(k, u, dom, 0, -1)["threads"] == 128
+
+
+@pytest.mark.parametrize("ny,nx,mask,threads", [
+    (32768, 32768, 0, 256),   # the BASELINE domain, Dirichlet: two stage-major strips
+    (16384, 32768, 5, 256),   # an N = 2 share (2^29 points)
+    (16384, 16384, 0, 128),   # 2^28 points: one strip
+    (8192, 8192, 0, 128),     # one-round Dirichlet: one strip
+    (8192, 16384, 15, 512),   # x sides exchange halos: the shared group
+    (8192, 16384, 3, 512),
+    (8192, 16384, 13, 128),   # a Dirichlet x side (W: bit 0 clear)
+])
+def test_default_launch_shapes(ny, nx, mask, threads):
+    """The K = 20 default shapes (csrc/kernels/jacobi5tb.hpp sh_launch /
+    launch_tb; profiles/r06_shared/README.md), from the launch plan alone."""
+    k = 20
+    dom = (k, nx, k, ny)
+    p = ops.jacobi5tb_plan(k, [dom], dom, mask, nx + 2 * k + 8, ny + 2 * k)
+    assert p["threads"] == threads, p
