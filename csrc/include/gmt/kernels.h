@@ -225,9 +225,11 @@ typedef struct gmt_tb_opts {
      20 passes of one rect at least a group wide (920 columns at K = 20),
      with no push, signals or wg_waves, run as workgroups of four strips
      whose stage-1 waves read windows of one shared hand-off row — 6% fewer
-     level updates per output at K = 20.  Bitwise the same field.  1 = on,
-     -1 = off, 0 = default: rects whose x sides both exchange halos, or
-     larger than 2^28 points (GMT_TB_SHARED=1 / 0 forces it on / off). */
+     level updates per output at K = 20.  Bitwise the same field.
+     -1 = off, 1 = on (four-strip groups), 2 / 4 = on with groups of that
+     many strips (448 / 920 output columns at K = 20), 0 = default: four-
+     strip groups where both x sides exchange halos, two-strip groups for
+     other rects over 2^28 points (GMT_TB_SHARED=0 / 1 / 2 / 4 forces it). */
   int shared;
 } gmt_tb_opts;
 enum { GMT_PUSH_S = 0, GMT_PUSH_N = 1, GMT_PUSH_W = 2, GMT_PUSH_E = 3,

@@ -86,9 +86,9 @@ __host__ __device__ constexpr int64_t strip_lds() {
 // by 4-column groups g (lane l of a window starting at group g0 holds group
 // g0 + l): pair q of group g at byte q QS + 16 g, conflict-free for every
 // window offset.  NL even: every ownership boundary is a column pair.
-template <int K>
+template <int K, int NW_ = 4>
 struct Sh {
-  static constexpr int NW = 4;                             // strips per workgroup
+  static constexpr int NW = NW_;                           // strips per workgroup (2 or 4)
   static constexpr int NL = K / 2;                         // levels per stage
   static constexpr bool kOk = tb_stages(K) == 2 && NL % 2 == 0;
   static constexpr int S0 = 256 - 2 * NL;                  // stage-0 window spacing
@@ -101,7 +101,8 @@ struct Sh {
   // and S1 are multiples of 4)
   static constexpr int kJW = (ML - 1) % 4;
   static constexpr int kJE = (GOUT + ML) % 4;
-  static constexpr int NG = 256;                           // 4-column groups of a shared row
+  static constexpr int kCols = S0 * (NW - 1) + 256;        // input columns of a group
+  static constexpr int NG = kCols <= 512 ? 128 : 256;      // 4-column groups of a shared row
   static constexpr uint32_t QS = NG * 16;                  // pair-plane stride (bytes)
   static constexpr uint32_t ROWG = 2 * QS;                 // one shared row (bytes)
   static_assert(!kOk || (S0 % 4 == 0 && S1 > 0 && S1 <= S0 && O + S1 * (NW - 1) + 256 <= S0 * (NW - 1) + 256 - NL),
@@ -110,10 +111,10 @@ struct Sh {
 };
 
 // LDS of an SH workgroup: the shared hand-off ring, then NW DMA rings
-template <int K>
+template <int K, int NW = 4>
 __host__ __device__ constexpr int64_t sh_lds() {
   using C = Cfg<K>;
-  return static_cast<int64_t>(C::HS) * Sh<K>::ROWG + static_cast<int64_t>(Sh<K>::NW) * C::RS * C::ROW;
+  return static_cast<int64_t>(C::HS) * Sh<K, NW>::ROWG + static_cast<int64_t>(NW) * C::RS * C::ROW;
 }
 
 struct Args {
@@ -156,7 +157,7 @@ struct Args {
   // over the XCDs, after each XCD's contiguous range of the other tiles
   // (tail_swizzle); 0: every tile XCD-contiguous in tile order
   int64_t edges_last;
-  int sh;                        // an SH launch (Sh<K> groups of nw = Sh<K>::NW strips)
+  int sh;                        // an SH launch (Sh<K, nw> groups of nw = 2 or 4 strips)
   int shmap;                     // waves stage-major (SH: GMT_TB_SH_MAP, default on; several
                                  // two-stage strips per workgroup: GMT_TB_STRIP_MAP, A/B)
   int col_keep;                  // the one-column Dirichlet keep (GMT_TB_COL_KEEP=0: off, A/B)
@@ -409,7 +410,7 @@ __device__ __forceinline__ void keep_col(dv<NC>& v, double c, uint64_t m) {
 // a wave-uniform delta from the DMA ring's lane address, so both share one
 // address VGPR); otherwise cf = xs - KL and the hand-off rings are the
 // strip's own.
-template <int K, int J, bool EXACT, bool EDGE, int RULE, bool UP, int PUSH, bool SH>
+template <int K, int J, bool EXACT, bool EDGE, int RULE, bool UP, int PUSH, int SH>
 __device__ __forceinline__ void run_stage(const Args& a, const double* __restrict__ u, double* __restrict__ un,
                                           char* ring, int lane, int64_t xs, int64_t xe, int64_t ys, int64_t ye,
                                           int nsteps, int sig_step, int xd, int64_t cf, int hdelta, uint64_t hm0,
@@ -440,8 +441,9 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
   const double quarter = a.quarter;
   const int64_t dx0 = a.dom[0], dx1 = a.dom[0] + a.dom[1];
   const int64_t dy0 = a.dom[2], dy1 = a.dom[2] + a.dom[3];
-  static_assert(!SH || (Sh<K>::kOk && !EDGE && PUSH == 0 && !UP), "SH: one-rect passes, plain bodies");
-  constexpr uint32_t kQS = Sh<K>::QS, kRowG = Sh<K>::ROWG;
+  using SHG = Sh<K, SH ? SH : 4>;  // (SH: the group's strips, 2 or 4)
+  static_assert(!SH || (SHG::kOk && !EDGE && PUSH == 0 && !UP), "SH: one-rect passes, plain bodies");
+  constexpr uint32_t kQS = SHG::QS, kRowG = SHG::ROWG;
   char* const hsh = ring + 16 * lane + hdelta;
   const int64_t c0 = cf + NC * lane;    // this lane: columns c0 .. c0+NC-1
   const int64_t yl = ys - K;            // the window's first row
@@ -765,7 +767,7 @@ __device__ __forceinline__ void run_stage(const Args& a, const double* __restric
 // A workgroup = nw adjacent strips of one segment row, S waves per strip
 // (adjacent strips share their overlap columns in the CU's L1 / the XCD's
 // L2).  S == 1: every wave is independent (no barrier).
-template <int K, bool EXACT, bool EDGE, bool PUSH, bool SH>
+template <int K, bool EXACT, bool EDGE, bool PUSH, int SH>
 __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict__ u, double* __restrict__ un,
                                          int64_t t) {
   using C = Cfg<K>;
@@ -883,7 +885,7 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
     // rx1 (launch_tb: the rect is at least GOUT wide); stage 0 of strip sl
     // reads window ga + S0 sl, stage 1 window ga + O + S1 sl and stores its
     // slice of the group's output
-    using H = Sh<K>;
+    using H = Sh<K, SH>;
     int64_t gx = rx0 + gi * H::GOUT;
     if (gx + H::GOUT > rx1) gx = rx1 - H::GOUT;
     const int64_t ga = gx - H::ML;
@@ -930,7 +932,7 @@ __device__ __forceinline__ void tb_block(const Args& a, const double* __restrict
   // (SH only: in the per-strip K = 20 kernel the two extra bodies spilled
   // 12-14 VGPRs)
   constexpr bool kColBodies = SH;
-  constexpr int kJW = SH ? Sh<K>::kJW : 3, kJE = SH ? Sh<K>::kJE : 0;
+  constexpr int kJW = SH ? Sh<K, SH ? SH : 4>::kJW : 3, kJE = SH ? Sh<K, SH ? SH : 4>::kJE : 0;
   if constexpr (kColBodies) {
     const bool ry = (ys - K < a.dom[2] && !(a.mask & 4)) || (ye + K > a.dom[2] + a.dom[3] && !(a.mask & 8));
     const int64_t gw0 = a.dom[0] - 1, ge0 = a.dom[0] + a.dom[1];
@@ -1044,7 +1046,7 @@ inline bool tail_swizzle_ok(int64_t nb, int64_t ne) {
   return true;
 }
 
-template <int K, bool EXACT, bool EDGE, bool PUSH, bool SH>
+template <int K, bool EXACT, bool EDGE, bool PUSH, int SH>
 __global__ __launch_bounds__(kMaxThreads) __attribute__((amdgpu_waves_per_eu(2)))
 void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__ un, int64_t nblocks) {
   if constexpr (PUSH) {
@@ -1061,7 +1063,7 @@ void jacobi5tb_kernel(Args a, const double* __restrict__ u, double* __restrict__
   // the deltas go out by vector atomics once the workgroup's work is done
   extern __shared__ d2 lds_dyn[];
   uint64_t* stamp = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(lds_dyn) +
-                                                (SH ? sh_lds<K>() : a.nw * strip_lds<K>()));
+                                                (SH ? sh_lds<K, SH ? SH : 4>() : a.nw * strip_lds<K>()));
   const bool clk = a.clk && (b & 255) == 128 && threadIdx.x == 0;
   if (clk) {
     stamp[0] = __builtin_amdgcn_s_memtime();
@@ -1435,7 +1437,7 @@ SegPlan plan_segments(const Args& a, int seg_rows, int64_t lmax, int64_t residen
 // Fills the kernel arguments and the launch shape; info (optional) gets
 // {workgroups, resident workgroups, threads per workgroup, rows per interior
 // segment and interior segments of the first rect, VGPRs per lane}.
-template <int K, bool EXACT, bool EDGE, bool PUSH, bool SH>
+template <int K, bool EXACT, bool EDGE, bool PUSH, int SH>
 int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int64_t* dom, int mask, const double* u,
               double* un, int64_t ld, int64_t nrows, hipStream_t s, int64_t* info = nullptr) {
   using C = Cfg<K>;
@@ -1473,8 +1475,8 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
     a.shmap = strip_map != 0 && a.nw > 1;
   }
   if constexpr (SH) {
-    static_assert(Sh<K>::kOk && !EDGE && !PUSH, "SH launches: plain two-stage bodies");
-    a.nw = Sh<K>::NW;
+    static_assert(Sh<K, SH>::kOk && !EDGE && !PUSH, "SH launches: plain two-stage bodies");
+    a.nw = Sh<K, SH>::NW;
     a.sh = 1;
     // stage-major waves: each SIMD then holds one stage-0 and one stage-1
     // wave (the dispatcher deals a workgroup's waves to consecutive SIMDs,
@@ -1511,14 +1513,15 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
         (dom[1] + C::WOUT - 1) / C::WOUT < 2)
       return static_cast<int>(hipErrorInvalidValue);
   }
-  constexpr int64_t wout = SH ? Sh<K>::GOUT : C::WOUT;  // SH: a group's columns
+  using SHG = Sh<K, SH ? SH : 4>;
+  constexpr int64_t wout = SH ? SHG::GOUT : C::WOUT;  // SH: a group's columns
   int64_t maxh = 0;
   for (int k = 0; k < n_rect; ++k) {
     const int64_t* r = rects + 4 * k;
     if (r[1] <= 0 || r[3] <= 0) continue;
     if (SH && r[1] < wout) return static_cast<int>(hipErrorInvalidValue);  // (dispatch_k checks it)
     for (int j = 0; j < 4; ++j) a.r[a.n][j] = r[j];
-    a.nstrip[a.n] = SH ? Sh<K>::NW * ((r[1] + wout - 1) / wout) : (r[1] + wout - 1) / wout;
+    a.nstrip[a.n] = SH ? SHG::NW * ((r[1] + wout - 1) / wout) : (r[1] + wout - 1) / wout;
     maxh = std::max(maxh, r[3]);
     ++a.n;
   }
@@ -1533,7 +1536,7 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   if (lmax < 1) return static_cast<int>(hipErrorInvalidValue);
   (void)maxh;
   // + 16 B: the clock record's start stamps (jacobi5tb_kernel)
-  const size_t smem = static_cast<size_t>(SH ? sh_lds<K>() : a.nw * strip_lds<K>()) + 16;
+  const size_t smem = static_cast<size_t>(SH ? sh_lds<K, SH ? SH : 4>() : a.nw * strip_lds<K>()) + 16;
   if (smem > 65536) {  // above the default dynamic-LDS limit (gfx950 has 160 KB per CU)
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&jacobi5tb_kernel<K, EXACT, EDGE, PUSH, SH>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem));
@@ -1543,10 +1546,10 @@ int launch_tb(const gmt_tb_opts& o, int n_rect, const int64_t* rects, const int6
   // queried once per device, kernel and strips-per-workgroup (an idempotent
   // cache: a process driving several devices keeps one entry per device)
   constexpr int kMaxDev = 64;
-  static std::atomic<int> resident[kMaxDev][2][kMaxThreads / kWave + 1] = {};
+  static std::atomic<int> resident[kMaxDev][3][kMaxThreads / kWave + 1] = {};
   int dev = 0;
   (void)hipGetDevice(&dev);
-  std::atomic<int>* slot = dev >= 0 && dev < kMaxDev ? &resident[dev][SH ? 1 : 0][a.nw] : nullptr;
+  std::atomic<int>* slot = dev >= 0 && dev < kMaxDev ? &resident[dev][SH / 2][a.nw] : nullptr;
   int per_cu = slot ? slot->load(std::memory_order_relaxed) : 0;
   if (per_cu <= 0) {
     int occ = 0, cus = 256;
@@ -1733,31 +1736,44 @@ namespace tb {
 // signals or explicit workgroup shape.  gmt_tb_opts.shared: 1 on, -1 off,
 // 0 the default (GMT_TB_SHARED=1 / 0 forces it on / off).
 template <int K>
-bool sh_launch(const gmt_tb_opts& o, int n_rect, const int64_t* rects, int mask) {
+int sh_launch(const gmt_tb_opts& o, int n_rect, const int64_t* rects, int mask) {
   if constexpr (!Sh<K>::kOk) {
-    return false;
+    return 0;
   } else {
-    // GMT_TB_SHARED: 1 on wherever it applies, 0 off, unset: the default
+    // GMT_TB_SHARED: 1 on wherever it applies (four-strip groups), 2 / 4 on
+    // with groups of that many strips, 0 off; unset: the default
     static const int env = [] {
       const char* e = std::getenv("GMT_TB_SHARED");
-      return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
+      return e ? std::atoi(e) : -1;
     }();
-    if (o.shared < 0 || (o.shared == 0 && env == 0)) return false;
-    if (o.push_w > 0 || o.wg_waves > 0 || o.signal_rects > 0 || o.signal_rows > 0 || (o.signal_cols & 3)) return false;
-    int n = 0;
-    for (int k = 0; k < n_rect; ++k) {
-      const int64_t* r = rects + 4 * k;
-      if (r[1] <= 0 || r[3] <= 0) continue;
-      if (r[1] < Sh<K>::GOUT) return false;
-      // the default: a rect whose x sides both exchange halos (+2-3% on
-      // the one-round N = 8 shares, +7% at 32768^2).  With a Dirichlet x
-      // side the boundary groups (every strip waits for the rule strip at
-      // each step) cost it the gain: two-strip workgroups win at 32768^2
-      // and one-strip ones elsewhere (launch_tb; profiles/r06_shared/)
-      if (o.shared == 0 && env < 0 && (mask & 3) != 3) return false;
-      ++n;
+    if (o.shared < 0 || (o.shared == 0 && env == 0)) return 0;
+    if (o.push_w > 0 || o.wg_waves > 0 || o.signal_rects > 0 || o.signal_rows > 0 || (o.signal_cols & 3)) return 0;
+    // the default (o.shared == 0, GMT_TB_SHARED unset): four-strip groups
+    // for a rect whose x sides both exchange halos (+2-3% on the one-round
+    // N = 8 shares, +2% at 32768^2); two-strip groups for a larger rect
+    // (over 2^28 points: several rounds) with a Dirichlet x side — its
+    // boundary groups couple only two strips to the rule strip's pace:
+    // 32768^2 5.42-5.50M against 5.29-5.30M for two plain stage-major strips
+    // and 5.22-5.25M for four-strip groups, same box; one-round Dirichlet
+    // passes keep one strip per workgroup (profiles/r06_shared/ab_aa.txt)
+    const bool dflt = o.shared == 0 && env < 0;
+    int64_t area = 0, nonempty = 0;
+    for (int k = 0; k < n_rect; ++k)
+      if (rects[4 * k + 1] > 0 && rects[4 * k + 3] > 0) {
+        ++nonempty;
+        area = rects[4 * k + 1] * rects[4 * k + 3];
+      }
+    if (nonempty != 1) return 0;
+    int w = (o.shared > 0 ? o.shared : env) == 2 ? 2 : 4;
+    if (dflt) {
+      if ((mask & 3) == 3) w = 4;
+      else if (area > (int64_t(1) << 28)) w = 2;
+      else return 0;
     }
-    return n == 1;
+    const int64_t gout = w == 2 ? Sh<K, 2>::GOUT : Sh<K, 4>::GOUT;
+    for (int k = 0; k < n_rect; ++k)
+      if (rects[4 * k + 1] > 0 && rects[4 * k + 3] > 0 && rects[4 * k + 1] < gout) return 0;
+    return w;
   }
 }
 
@@ -1765,9 +1781,13 @@ template <int K>
 int dispatch_k(const gmt_tb_opts& o, bool exact, int n_rect, const int64_t* rects, const int64_t* dom, int mask,
                const double* u, double* un, int64_t ld, int64_t nrows, hipStream_t s, int64_t* info) {
   if constexpr (Sh<K>::kOk) {
-    if (sh_launch<K>(o, n_rect, rects, mask))
-      return exact ? launch_tb<K, true, false, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
-                   : launch_tb<K, false, false, false, true>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
+    const int w = sh_launch<K>(o, n_rect, rects, mask);
+    if (w == 4)
+      return exact ? launch_tb<K, true, false, false, 4>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
+                   : launch_tb<K, false, false, false, 4>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
+    if (w == 2)
+      return exact ? launch_tb<K, true, false, false, 2>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info)
+                   : launch_tb<K, false, false, false, 2>(o, n_rect, rects, dom, mask, u, un, ld, nrows, s, info);
   }
   // a rect narrower than a strip whose width is odd ends inside a lane pair:
   // that lane stores column 0 or 2 alone (wider rects end on a lane

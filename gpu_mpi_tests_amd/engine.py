@@ -420,7 +420,8 @@ class NativeJacobi:
         d = dict(zip(keys, (int(v) for v in out)))
         if k > 10 and d["threads"] in (128, 256, 512):
             d["shape"] = {128: "one two-stage strip per workgroup",
-                          256: "two two-stage strips per workgroup, stage-major waves",
+                          256: "two two-stage strips per workgroup, stage-major waves (a shared "
+                               "hand-off pair unless push / GMT_TB_SHARED=0)",
                           512: "shared hand-off group: four strips, stage-major waves"}[d["threads"]]
         return d
 

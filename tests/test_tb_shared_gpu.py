@@ -15,8 +15,9 @@ from gpu_mpi_tests_amd.ops import reference as ref
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
-# output columns of one group (Sh<K>::GOUT)
+# output columns of one group (Sh<K, 4>::GOUT, Sh<K, 2>::GOUT)
 GOUT = {12: 952, 16: 936, 20: 920}
+GOUT2 = {12: 472, 16: 464, 20: 448}
 
 
 @pytest.fixture(autouse=True, scope="module")
@@ -97,8 +98,8 @@ def test_shared_not_for_narrow_or_push():
 
 
 @pytest.mark.parametrize("ny,nx,mask,threads", [
-    (32768, 32768, 0, 256),   # the BASELINE domain, Dirichlet: two stage-major strips
-    (16384, 32768, 5, 256),   # an N = 2 share (2^29 points)
+    (32768, 32768, 0, 256),   # the BASELINE domain, Dirichlet: two-strip shared groups
+    (16384, 32768, 5, 256),   # an N = 2 share (2^29 points): the same
     (16384, 16384, 0, 128),   # 2^28 points: one strip
     (8192, 8192, 0, 128),     # one-round Dirichlet: one strip
     (8192, 16384, 15, 512),   # x sides exchange halos: the shared group
@@ -112,3 +113,31 @@ def test_default_launch_shapes(ny, nx, mask, threads):
     dom = (k, nx, k, ny)
     p = ops.jacobi5tb_plan(k, [dom], dom, mask, nx + 2 * k + 8, ny + 2 * k)
     assert p["threads"] == threads, p
+
+
+@pytest.mark.parametrize("k", [12, 16, 20])
+@pytest.mark.parametrize("dw", [0, 1, 3, None])
+@pytest.mark.parametrize("mask", [0, 15, 6])
+def test_shared_two_strip_groups_bitwise(k, dw, mask):
+    """Two-strip groups (gmt_tb_opts.shared = 2: 448 output columns per
+    4 waves at K = 20) against the reference and the per-strip launch."""
+    nx = 3 * GOUT2[k] + 41 if dw is None else GOUT2[k] + dw
+    xo = 24 + (dw or 0) % 2
+    u, dom = _field(k, 45, nx, seed=13 * k + nx, xo=xo)
+    assert _plan(k, u, dom, mask, 2)["threads"] == 256
+    got = _run(k, u, dom, mask, 2)
+    exp = torch.full(u.shape, 7.0, dtype=torch.float64)
+    ref.jacobi5xk(k, u.cpu(), exp, [dom], dom, mask)
+    assert torch.equal(got, exp), (got - exp).abs().max()
+    assert torch.equal(got, _run(k, u, dom, mask, -1))
+
+
+@pytest.mark.parametrize("mask", [0, 15])
+def test_shared_two_strip_groups_multi_round(mask):
+    k = 20
+    u, dom = _field(k, 32768, 16384, seed=9, xo=k)
+    p = _plan(k, u, dom, mask, 2)
+    assert p["threads"] == 256 and p["workgroups"] > p["resident"], p
+    a = _run(k, u, dom, mask, 2, cpu=False)
+    b = _run(k, u, dom, mask, -1, cpu=False)
+    assert torch.equal(a, b), int((a != b).sum())
