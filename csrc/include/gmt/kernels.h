@@ -229,7 +229,7 @@ typedef struct gmt_tb_opts {
      -1 = off, 1 = on (four-strip groups), 2 / 4 = on with groups of that
      many strips (448 / 920 output columns at K = 20), 0 = default: four-
      strip groups where both x sides exchange halos, two-strip groups for
-     other rects over 2^28 points (GMT_TB_SHARED=0 / 1 / 2 / 4 forces it). */
+     other rects of 2^28 points or more (GMT_TB_SHARED=0 / 1 / 2 / 4 forces it). */
   int shared;
 } gmt_tb_opts;
 enum { GMT_PUSH_S = 0, GMT_PUSH_N = 1, GMT_PUSH_W = 2, GMT_PUSH_E = 3,

@@ -1751,11 +1751,13 @@ int sh_launch(const gmt_tb_opts& o, int n_rect, const int64_t* rects, int mask) 
     // the default (o.shared == 0, GMT_TB_SHARED unset): four-strip groups
     // for a rect whose x sides both exchange halos (+2-3% on the one-round
     // N = 8 shares, +2% at 32768^2); two-strip groups for a larger rect
-    // (over 2^28 points: several rounds) with a Dirichlet x side — its
+    // (2^28 points or more: several rounds) with a Dirichlet x side — its
     // boundary groups couple only two strips to the rule strip's pace:
     // 32768^2 5.42-5.50M against 5.29-5.30M for two plain stage-major strips
     // and 5.22-5.25M for four-strip groups, same box; one-round Dirichlet
-    // passes keep one strip per workgroup (profiles/r06_shared/ab_aa.txt)
+    // passes keep one strip per workgroup (profiles/r06_shared/ab_aa.txt).
+    // From 2^28 points on: the N = 4 shares (8192 x 32768, three rounds)
+    // gain 3-5% on every side pattern (ab_cc.txt)
     const bool dflt = o.shared == 0 && env < 0;
     int64_t area = 0, nonempty = 0;
     for (int k = 0; k < n_rect; ++k)
@@ -1767,7 +1769,7 @@ int sh_launch(const gmt_tb_opts& o, int n_rect, const int64_t* rects, int mask) 
     int w = (o.shared > 0 ? o.shared : env) == 2 ? 2 : 4;
     if (dflt) {
       if ((mask & 3) == 3) w = 4;
-      else if (area > (int64_t(1) << 28)) w = 2;
+      else if (area >= (int64_t(1) << 28)) w = 2;
       else return 0;
     }
     const int64_t gout = w == 2 ? Sh<K, 2>::GOUT : Sh<K, 4>::GOUT;

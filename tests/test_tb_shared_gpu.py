@@ -100,7 +100,9 @@ def test_shared_not_for_narrow_or_push():
 @pytest.mark.parametrize("ny,nx,mask,threads", [
     (32768, 32768, 0, 256),   # the BASELINE domain, Dirichlet: two-strip shared groups
     (16384, 32768, 5, 256),   # an N = 2 share (2^29 points): the same
-    (16384, 16384, 0, 128),   # 2^28 points: one strip
+    (16384, 16384, 0, 256),   # 2^28 points: two-strip shared groups
+    (8192, 32768, 12, 256),   # the N = 4 share of a 4 x 1 grid
+    (8192, 16384, 0, 128),    # 2^27 points (one round): one strip
     (8192, 8192, 0, 128),     # one-round Dirichlet: one strip
     (8192, 16384, 15, 512),   # x sides exchange halos: the shared group
     (8192, 16384, 3, 512),
